@@ -1,0 +1,522 @@
+"""CPU fp32 ORACLE for the MapAnything feed-forward path — TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the thing measured or shipped: only `tests/`, `__graft_entry__.smoke()` and
+`bench.py`'s `cpu_baseline` leg may import it.  The product path (`map-anything_amd/mapanything`) never
+imports it and fails loudly when its HIP library is missing.
+
+It restates, in PyTorch-CPU fp32 functional ops (the same ATen kernels the reference's CPU path calls), the
+arithmetic of `MapAnything.infer` (model.py:2206-2355) for the released config (configs/inference.json):
+
+  validate/preprocess      inference.py:130-311, geometry.py:186-241 (rays), :655-713 (R->quat)
+  image encoder            dinov2.py:146-178 -> vision_transformer.py:208-312 (+ layers/block.py:93-118)
+  geometric fusion         model.py:1292-1438 (+ :792-1289, dense_rep_encoder.py:234-287,
+                           global_rep_encoder.py:85-104, geometry.py:1594-1666, 1737-1750, 745-852)
+  AAT-IFR                  alternating_attention_transformer.py:530-771, transformer_blocks.py:163-212, 452-469
+  DPT feature + regressor  dpt.py:180-232, 285-311, dpt_block.py:114-255
+  pose / scale heads       pose_head.py:18-159, mlp_head.py:13-92
+  adaptors                 adaptors.py:171-212, 237-280, 393-523, 586-732, 1012-1133, 1740-1796
+  output assembly          model.py:1865-1923, 2116-2150, geometry.py:601-652, 855-907
+  postprocess (no mask)    inference.py:314-400, geometry.py:304-447, image.py:93-131
+
+Parity pinning: this oracle is checked against fixtures produced by running the reference itself
+(tests/golden/make_golden.py -> tests/golden/golden_*.npz) on the same synthetic weights and inputs.
+In image-only mode the reference still runs the ray/depth/pose encoders on zeros and multiplies their
+features by an all-False mask (model.py:962-968, 1134-1137, 1200-1202, 1258-1279); that contributes exactly
++0.0, so the oracle skips those encoders in image-only mode.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ENC_DIM, ENC_HEADS, PATCH = 1024, 16, 14
+AAT_DIM, AAT_HEADS = 768, 12
+LN_EPS = 1e-6
+DINOV2_MEAN = torch.tensor([0.485, 0.456, 0.406])
+DINOV2_STD = torch.tensor([0.229, 0.224, 0.225])
+
+
+def _t(x):
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x)
+    return x
+
+
+class MapAnythingOracle:
+    """fp32 CPU restatement. `sd` = canonical state dict (names of spec.canonical_spec())."""
+
+    def __init__(self, sd: Dict[str, object]):
+        self.sd = {k: _t(v).float() for k, v in sd.items()}
+        self.taps: Dict[str, torch.Tensor] = {}
+
+    def p(self, name):
+        return self.sd[name]
+
+    # ---------------------------------------------------------------------------------------------- blocks
+    def ln(self, x, name):
+        return F.layer_norm(x, (x.shape[-1],), self.p(f"{name}.weight"), self.p(f"{name}.bias"), LN_EPS)
+
+    def lin(self, x, name):
+        return F.linear(x, self.p(f"{name}.weight"), self.sd.get(f"{name}.bias"))
+
+    def conv(self, x, name, stride=1, padding=0):
+        return F.conv2d(x, self.p(f"{name}.weight"), self.sd.get(f"{name}.bias"), stride=stride, padding=padding)
+
+    def attention(self, x, name, heads):
+        """transformer_blocks.py:163-212 / dinov2.py:125-141: qkv -> SDPA (scale hd^-0.5) -> proj."""
+        B, N, C = x.shape
+        qkv = self.lin(x, f"{name}.qkv").reshape(B, N, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        o = F.scaled_dot_product_attention(q, k, v)
+        o = o.transpose(1, 2).reshape(B, N, C)
+        return self.lin(o, f"{name}.proj")
+
+    def mlp(self, x, name):
+        return self.lin(F.gelu(self.lin(x, f"{name}.fc1")), f"{name}.fc2")
+
+    def dinov2_block(self, x, name):
+        """layers/block.py:93-118 with LayerScale (layer_scale.py:14-26)."""
+        x = x + self.p(f"{name}.ls1.gamma") * self.attention(self.ln(x, f"{name}.norm1"), f"{name}.attn", ENC_HEADS)
+        x = x + self.p(f"{name}.ls2.gamma") * self.mlp(self.ln(x, f"{name}.norm2"), f"{name}.mlp")
+        return x
+
+    def aat_block(self, x, name):
+        """transformer_blocks.py:452-469 (init_values=None -> no LayerScale, eval -> no drop path)."""
+        x = x + self.attention(self.ln(x, f"{name}.norm1"), f"{name}.attn", AAT_HEADS)
+        x = x + self.mlp(self.ln(x, f"{name}.norm2"), f"{name}.mlp")
+        return x
+
+    # ---------------------------------------------------------------------------------------------- encoder
+    def pos_embed_for(self, H, W):
+        """vision_transformer.py:208-242: identity at 37x37, else bicubic (scale_factor=(h0+0.1)/37, ...)."""
+        pe = self.p("encoder.model.pos_embed")
+        h0, w0 = H // PATCH, W // PATCH
+        N = pe.shape[1] - 1
+        if h0 * w0 == N and H == W:
+            return pe
+        M = int(math.sqrt(N))
+        cls_pe, patch_pe = pe[:, 0], pe[:, 1:]
+        sx, sy = float(h0 + 0.1) / M, float(w0 + 0.1) / M
+        patch_pe = F.interpolate(patch_pe.reshape(1, M, M, ENC_DIM).permute(0, 3, 1, 2), mode="bicubic",
+                                 antialias=False, scale_factor=(sx, sy))
+        assert patch_pe.shape[-2:] == (h0, w0)
+        patch_pe = patch_pe.permute(0, 2, 3, 1).reshape(1, -1, ENC_DIM)
+        return torch.cat((cls_pe.unsqueeze(0), patch_pe), dim=1)
+
+    def dinov2(self, img):
+        """dinov2.py:146-178 + vision_transformer.py:244-312 (no registers, no masks)."""
+        B, _, H, W = img.shape
+        x = self.conv(img, "encoder.model.patch_embed.proj", stride=PATCH)      # (B,1024,h,w)
+        x = x.flatten(2).transpose(1, 2)
+        x = torch.cat((self.p("encoder.model.cls_token").expand(B, -1, -1), x), dim=1)
+        x = x + self.pos_embed_for(H, W)
+        for b in range(24):
+            x = self.dinov2_block(x, f"encoder.model.blocks.{b}")
+        x = self.ln(x, "encoder.model.norm")[:, 1:]
+        return x.permute(0, 2, 1).reshape(B, ENC_DIM, H // PATCH, W // PATCH)
+
+    # -------------------------------------------------------------------------------- geometric encoders
+    def dense_rep_encoder(self, data, name):
+        """dense_rep_encoder.py:234-287 (apply_pe=False) with ResidualBlock :31-52 (GELU)."""
+        B, C, H, W = data.shape
+        x = F.pixel_unshuffle(data, PATCH)
+        x = self.conv(x, f"{name}.conv_in", padding=1)
+        for i in range(2):
+            idt = self.conv(x, f"{name}.encoder.{i}.shortcut")
+            o = F.gelu(self.conv(x, f"{name}.encoder.{i}.conv1", padding=1))
+            o = self.conv(o, f"{name}.encoder.{i}.conv2", padding=1)
+            x = F.gelu(o + idt)
+        x = self.conv(x, f"{name}.encoder.2")
+        x = x.flatten(2).transpose(1, 2)
+        x = self.ln(x, f"{name}.norm_layer")
+        return x.permute(0, 2, 1).reshape(B, ENC_DIM, H // PATCH, W // PATCH)
+
+    def global_rep_encoder(self, data, name):
+        """global_rep_encoder.py:85-104: Linear/GELU x3 -> Linear -> LayerNorm."""
+        x = F.gelu(self.lin(data, f"{name}.encoder.0.0.0.0"))
+        x = F.gelu(self.lin(x, f"{name}.encoder.0.0.1"))
+        x = F.gelu(self.lin(x, f"{name}.encoder.0.1"))
+        x = self.lin(x, f"{name}.encoder.1")
+        return self.ln(x, f"{name}.norm_layer")
+
+    # ------------------------------------------------------------------------------------ fused features
+    def encode_and_fuse(self, views):
+        """model.py:1292-1438 with the deterministic 0/1 masks of infer() (model.py:2154-2197)."""
+        V = len(views)
+        B, _, H, W = views[0]["img"].shape
+        imgs = torch.cat([v["img"] for v in views], 0)
+        feats = self.dinov2(imgs)                                             # (V*B,1024,h,w)
+        self.taps["encoder"] = feats
+        has_geo = any(k in v for v in views for k in ("ray_directions_cam", "depth_along_ray",
+                                                     "camera_pose_quats"))
+        if has_geo:
+            feats = feats + self._geometric_features(views, B, H, W)
+        x = self.ln(feats.permute(0, 2, 3, 1), "fusion_norm_layer")
+        self.taps["fused_nhwc"] = x
+        return x.permute(0, 3, 1, 2).contiguous().chunk(V, 0)
+
+    def _geometric_features(self, views, B, H, W):
+        V = len(views)
+        out = 0
+        # ray directions: model.py:898-970
+        ray_mask = torch.tensor([("ray_directions_cam" in v) for v in views for _ in range(B)])
+        rays = torch.cat([v["ray_directions_cam"] if "ray_directions_cam" in v else torch.zeros(B, H, W, 3)
+                          for v in views], 0).permute(0, 3, 1, 2)
+        f = self.dense_rep_encoder(rays, "ray_dirs_encoder")
+        out = out + f * ray_mask.float().view(-1, 1, 1, 1)
+        # depth: model.py:973-1168 (dense depth; sparse_depth_prob = 0 in infer)
+        dep_mask = torch.tensor([("depth_along_ray" in v) for v in views for _ in range(B)])
+        depths, factors, metric = [], [], []
+        for v in views:
+            if "depth_along_ray" in v:
+                d = v["depth_along_ray"]
+                valid = d > 0
+                s = torch.sum(d * valid, dim=(1, 2, 3))
+                c = torch.sum(valid, dim=(1, 2, 3))
+                nf = (s / (c + 1e-8)).clip(min=1e-8)                           # geometry.py:1594-1626
+                depths.append(d / nf.view(-1, 1, 1, 1))
+                factors.append(nf)
+                metric.append(v.get("is_metric_scale", torch.zeros(B, dtype=torch.bool)).reshape(B))
+            else:
+                depths.append(torch.zeros(B, H, W, 1))
+                factors.append(torch.zeros(B))
+                metric.append(torch.zeros(B, dtype=torch.bool))
+        d = torch.cat(depths, 0)
+        n = d.norm(dim=-1, keepdim=True)                                       # geometry.py:1737-1750
+        d = d / n.clip(min=1e-8) * torch.log1p(n)
+        f = self.dense_rep_encoder(d.permute(0, 3, 1, 2), "depth_encoder")
+        out = out + f * dep_mask.float().view(-1, 1, 1, 1)
+        ds = self.global_rep_encoder(torch.log(torch.cat(factors) + 1e-8).unsqueeze(-1), "depth_scale_encoder")
+        ds = ds * dep_mask.float().unsqueeze(-1) * torch.cat(metric).float().unsqueeze(-1)
+        out = out + ds[:, :, None, None]
+        # camera poses: model.py:792-896, 1170-1289
+        cam_mask = torch.tensor([("camera_pose_quats" in v) for v in views for _ in range(B)])
+        quats = torch.tensor([0.0, 0.0, 0.0, 1.0]).repeat(V * B, 1)
+        trans = torch.zeros(V * B, 3)
+        if bool(cam_mask.any()):
+            q0, t0 = views[0]["camera_pose_quats"], views[0]["camera_pose_trans"]
+            for i, v in enumerate(views):
+                if "camera_pose_quats" in v:
+                    q, t = _pose_2_to_1(q0, t0, v["camera_pose_quats"], v["camera_pose_trans"])
+                    quats[i * B:(i + 1) * B] = q
+                    trans[i * B:(i + 1) * B] = t
+        fq = self.global_rep_encoder(quats, "cam_rot_encoder") * cam_mask.float().unsqueeze(-1)
+        metric_pose = torch.cat([v.get("is_metric_scale", torch.zeros(B, dtype=torch.bool)).reshape(B)
+                                 for v in views]).float()
+        tv = torch.stack(torch.split(trans, B, 0), 1)                          # (B,V,3)
+        dis = tv.norm(dim=-1)
+        nf = (dis.sum(1) / ((dis > 0).sum(1) + 1e-8)).clip(min=1e-8)            # geometry.py:1629-1666
+        tv = tv / nf.view(-1, 1, 1)
+        ts = torch.cat(tv.unbind(1), 0)
+        ft = self.global_rep_encoder(ts, "cam_trans_encoder") * cam_mask.float().unsqueeze(-1)
+        lnf = torch.log(nf.unsqueeze(-1).repeat(V, 1) + 1e-8)
+        fs = self.global_rep_encoder(lnf, "cam_trans_scale_encoder") * cam_mask.float().unsqueeze(-1)
+        fs = fs * metric_pose.unsqueeze(-1)
+        out = out + (fq + ft + fs)[:, :, None, None]
+        return out
+
+    # ------------------------------------------------------------------------------------------------- AAT
+    def aat(self, feats: List[torch.Tensor], scale_token: torch.Tensor):
+        """alternating_attention_transformer.py:530-771 (IFR, indices [11, 17], norm_intermediate)."""
+        V = len(feats)
+        B, C, h, w = feats[0].shape
+        T = h * w
+        x = torch.stack(feats, 1).permute(0, 1, 3, 4, 2).reshape(B, V * T, C)
+        x = torch.cat([x, scale_token.permute(0, 2, 1)], 1)
+        x = self.lin(x, "info_sharing.proj_embed")
+        pe = self.p("info_sharing.view_pos_table")[0].reshape(1, 1, AAT_DIM)
+        x = torch.cat([x[:, :T] + pe, x[:, T:V * T], x[:, V * T:]], 1)
+        inter = []
+        for d in range(24):
+            name = f"info_sharing.self_attention_blocks.{d}"
+            if d % 2 == 0:
+                x = self.aat_block(x, name)
+            else:
+                extra = x[:, V * T:]
+                xv = x[:, :V * T].reshape(B * V, T, AAT_DIM)
+                xv = self.aat_block(xv, name).reshape(B, V * T, AAT_DIM)
+                x = torch.cat([xv, extra], 1)
+            if d in (11, 17):
+                inter.append(self.ln(x, "info_sharing.norm"))
+        out = self.ln(x, "info_sharing.norm")
+
+        def split(y):
+            f = y[:, :V * T].reshape(B, V, h, w, AAT_DIM).permute(0, 1, 4, 2, 3)
+            return [f[:, i] for i in range(V)], y[:, V * T:].permute(0, 2, 1)
+
+        final_feats, tok = split(out)
+        l11, _ = split(inter[0])
+        l17, _ = split(inter[1])
+        self.taps["aat_final"] = torch.stack(final_feats, 1)
+        self.taps["aat_l11"] = torch.stack(l11, 1)
+        self.taps["aat_l17"] = torch.stack(l17, 1)
+        self.taps["scale_token"] = tok
+        return final_feats, l11, l17, tok
+
+    # ------------------------------------------------------------------------------------------------- DPT
+    def rcu(self, x, name):
+        """dpt_block.py:114-177 (ReLU not in place, no BN)."""
+        o = self.conv(F.relu(x), f"{name}.conv1", padding=1)
+        o = self.conv(F.relu(o), f"{name}.conv2", padding=1)
+        return o + x
+
+    def fusion(self, name, x0, x1=None):
+        """dpt_block.py:180-255 (width_ratio 1, align_corners True)."""
+        out = x0
+        if x1 is not None:
+            out = out + self.rcu(x1, f"{name}.resConfUnit1")
+        out = self.rcu(out, f"{name}.resConfUnit2")
+        out = F.interpolate(out, scale_factor=2, mode="bilinear", align_corners=True)
+        return self.conv(out, f"{name}.out_conv")
+
+    def dpt_feature(self, layers):
+        """dpt.py:180-232 with input_process of dpt.py:94-178."""
+        h = "dpt_feature_head"
+        p = f"{h}.input_process"
+        w = self.p
+        l0 = self.conv(layers[0], f"{p}.0.0.0")
+        l0 = F.conv_transpose2d(l0, w(f"{p}.0.0.1.weight"), w(f"{p}.0.0.1.bias"), stride=4)
+        l0 = F.conv2d(l0, w(f"{h}.scratch.layer1_rn.weight"), padding=1)
+        l1 = self.conv(layers[1], f"{p}.1.0.0")
+        l1 = F.conv_transpose2d(l1, w(f"{p}.1.0.1.weight"), w(f"{p}.1.0.1.bias"), stride=2)
+        l1 = F.conv2d(l1, w(f"{h}.scratch.layer2_rn.weight"), padding=1)
+        l2 = self.conv(layers[2], f"{p}.2.0.0")
+        l2 = F.conv2d(l2, w(f"{h}.scratch.layer3_rn.weight"), padding=1)
+        l3 = self.conv(layers[3], f"{p}.3.0.0")
+        l3 = self.conv(l3, f"{p}.3.0.1", stride=2, padding=1)
+        l3 = F.conv2d(l3, w(f"{h}.scratch.layer4_rn.weight"), padding=1)
+        path4 = self.fusion(f"{h}.scratch.refinenet4", l3)[:, :, :l2.shape[2], :l2.shape[3]]
+        path3 = self.fusion(f"{h}.scratch.refinenet3", path4, l2)
+        path2 = self.fusion(f"{h}.scratch.refinenet2", path3, l1)
+        return self.fusion(f"{h}.scratch.refinenet1", path2, l0)
+
+    def dpt_regressor(self, x, out_hw):
+        """dpt.py:285-311."""
+        x = self.conv(x, "dpt_regressor_head.conv1", padding=1)
+        x = F.interpolate(x, size=out_hw, mode="bilinear", align_corners=True)
+        x = F.relu(self.conv(x, "dpt_regressor_head.conv2.0", padding=1))
+        return self.conv(x, "dpt_regressor_head.conv2.2")
+
+    def pose_head(self, x):
+        """pose_head.py:18-159."""
+        f = self.conv(x, "pose_head.proj")
+        for b in range(2):
+            n = f"pose_head.res_conv.{b}"
+            r = F.relu(self.conv(f, f"{n}.res_conv1"))
+            r = F.relu(self.conv(r, f"{n}.res_conv2"))
+            r = F.relu(self.conv(r, f"{n}.res_conv3"))
+            f = f + r
+        f = f.mean(dim=(2, 3))
+        f = F.relu(self.lin(f, "pose_head.more_mlps.0"))
+        f = F.relu(self.lin(f, "pose_head.more_mlps.2"))
+        return torch.cat([self.lin(f, "pose_head.fc_t"), self.lin(f, "pose_head.fc_rot")], 1)
+
+    def scale_head(self, tok):
+        """mlp_head.py:13-92 on the (B, C, 1) scale-token feature."""
+        f = self.lin(tok.permute(0, 2, 1), "scale_head.proj")
+        f = F.relu(self.lin(f, "scale_head.mlp.0.0"))
+        f = F.relu(self.lin(f, "scale_head.mlp.1.0"))
+        return self.lin(f, "scale_head.output_proj").permute(0, 2, 1)
+
+    # ------------------------------------------------------------------------------------------- forward
+    def forward(self, views):
+        """model.py:1657-2152 for pred_head 'dpt+pose', scene rep 'raydirs+depth+pose+confidence+mask'."""
+        self.taps = {}
+        B, _, H, W = views[0]["img"].shape
+        V = len(views)
+        fused = self.encode_and_fuse(views)
+        scale_tok = self.p("scale_token").view(1, -1, 1).repeat(B, 1, 1)
+        final, l11, l17, tok = self.aat(list(fused), scale_tok)
+        layers = [torch.cat(fused, 0), torch.cat(l11, 0), torch.cat(l17, 0), torch.cat(final, 0)]
+        feat = self.dpt_feature(layers)
+        self.taps["dpt_feature"] = feat
+        dense = self.dpt_regressor(feat, (H, W))                              # (V*B, 6, H, W)
+        self.taps["dense_raw"] = dense
+        pose = self.pose_head(layers[3])                                      # (V*B, 7)
+        self.taps["pose_raw"] = pose
+        scale_raw = self.scale_head(tok)                                      # (B, 1, 1)
+        self.taps["scale_raw"] = scale_raw
+        # adaptors (adaptors.py:1740-1796, 469-523, 393-466, 237-280, 1012-1073, 1114-1133, 688-732, 171-212)
+        rays = dense[:, 0:3]
+        rays = rays / rays.norm(dim=1, keepdim=True).clip(min=1e-8)
+        depth = torch.exp(dense[:, 3:4]).clip(0, float("inf"))
+        conf = 1.0 + dense[:, 4:5].exp().clip(max=float("inf"))
+        logits = dense[:, 5:6]
+        mask = torch.sigmoid(logits)
+        t = pose[:, 0:3]
+        q = pose[:, 3:7]
+        q = q / q.norm(dim=1, keepdim=True).clip(min=1e-8)
+        scale = torch.exp(scale_raw).clip(1e-8, float("inf")).squeeze(-1)  # (B, 1)
+        # output assembly (model.py:1871-1923)
+        rays_hw = rays.permute(0, 2, 3, 1)
+        depth_hw = depth.permute(0, 2, 3, 1)
+        pts_world = ray_depth_pose_to_pointmap(rays_hw, depth_hw, t, q)
+        pts_cam = rays_hw * depth_hw
+        s4 = scale.unsqueeze(-1).unsqueeze(-1)
+        res = []
+        for i in range(V):
+            sl = slice(i * B, (i + 1) * B)
+            res.append({
+                "pts3d": pts_world[sl] * s4,
+                "pts3d_cam": pts_cam[sl] * s4,
+                "ray_directions": rays_hw[sl],
+                "depth_along_ray": depth_hw[sl] * s4,
+                "cam_trans": t[sl] * scale,
+                "cam_quats": q[sl],
+                "metric_scaling_factor": scale,
+                "conf": conf.permute(0, 2, 3, 1).squeeze(-1)[sl],
+                "non_ambiguous_mask": (mask.permute(0, 2, 3, 1).squeeze(-1) > 0.5)[sl],
+                "non_ambiguous_mask_logits": logits.permute(0, 2, 3, 1).squeeze(-1)[sl],
+            })
+        return res
+
+    @torch.no_grad()
+    def infer(self, views, apply_mask=False):
+        """model.py:2206-2355 (fp32, apply_mask=False path of postprocess, inference.py:314-400)."""
+        if apply_mask:
+            raise NotImplementedError("oracle covers the apply_mask=False postprocess")
+        pv = preprocess_views(views)
+        raw = self.forward(pv)
+        out = []
+        for r, v in zip(raw, pv):
+            o = dict(r)
+            img = v["img"]
+            o["img_no_norm"] = (img.permute(0, 2, 3, 1) * DINOV2_STD + DINOV2_MEAN).clip(0, 1)
+            o["depth_z"] = o["pts3d_cam"][..., 2:3]
+            o["intrinsics"] = recover_pinhole_intrinsics(o["ray_directions"])
+            Bv = o["cam_trans"].shape[0]
+            P = torch.eye(4).unsqueeze(0).repeat(Bv, 1, 1)
+            P[:, :3, :3] = quat_to_rot(o["cam_quats"])
+            P[:, :3, 3] = o["cam_trans"]
+            o["camera_poses"] = P
+            out.append(o)
+        return out
+
+
+# ------------------------------------------------------------------------------------------------ geometry
+def quat_to_rot(q):
+    """geometry.py:601-652."""
+    q = q / q.norm(dim=1, keepdim=True)
+    x, y, z, w = q.unbind(1)
+    return torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                        2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                        2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)], 1).view(-1, 3, 3)
+
+
+def ray_depth_pose_to_pointmap(rays, depth, t, q):
+    """geometry.py:855-907."""
+    q = q / torch.norm(q, dim=-1, keepdim=True)
+    R = quat_to_rot(q)
+    Bn = rays.shape[0]
+    P = torch.eye(4).unsqueeze(0).repeat(Bn, 1, 1)
+    P[:, :3, :3] = R
+    P[:, :3, 3] = t
+    loc = depth * rays
+    homo = torch.cat([loc, torch.ones_like(loc[..., :1])], -1)
+    return torch.einsum("bik,bhwk->bhwi", P, homo)[..., :3]
+
+
+def _pose_2_to_1(q1, t1, q2, t2):
+    """geometry.py:745-852."""
+    qc = q1.clone()
+    qc[:, :3] = -qc[:, :3]
+    inv = qc / torch.sum(q1 * q1, dim=1, keepdim=True)
+    R = quat_to_rot(inv)
+    tinv = -torch.einsum("bij,bj->bi", R, t1)
+    x1, y1, z1, w1 = inv.unbind(1)
+    x2, y2, z2, w2 = q2.unbind(1)
+    q = torch.stack([w1 * x2 + x1 * w2 + y1 * z2 - z1 * y2, w1 * y2 - x1 * z2 + y1 * w2 + z1 * x2,
+                     w1 * z2 + x1 * y2 - y1 * x2 + z1 * w2, w1 * w2 - x1 * x2 - y1 * y2 - z1 * z2], 1)
+    return q, torch.einsum("bij,bj->bi", R, t2) + tinv
+
+
+def rays_from_intrinsics(K, H, W):
+    """geometry.py:186-241 (normalize_to_unit_sphere=True)."""
+    xg, yg = torch.meshgrid(torch.arange(W).float(), torch.arange(H).float(), indexing="xy")
+    B = K.shape[0]
+    xg = xg.unsqueeze(0).expand(B, -1, -1)
+    yg = yg.unsqueeze(0).expand(B, -1, -1)
+    fx, fy = K[:, 0, 0].view(-1, 1, 1), K[:, 1, 1].view(-1, 1, 1)
+    cx, cy = K[:, 0, 2].view(-1, 1, 1), K[:, 1, 2].view(-1, 1, 1)
+    d = torch.stack(((xg - cx) / fx, (yg - cy) / fy, torch.ones_like(xg)), -1)
+    return d / torch.norm(d, dim=-1, keepdim=True)
+
+
+def recover_pinhole_intrinsics(rays):
+    """geometry.py:304-447 (regression branch for <=1 MPix)."""
+    B, H, W, _ = rays.shape
+    xg, yg = torch.meshgrid(torch.arange(W).float(), torch.arange(H).float(), indexing="xy")
+    xg = xg.unsqueeze(0).expand(B, -1, -1)
+    yg = yg.unsqueeze(0).expand(B, -1, -1)
+    if H * W > 1000000:
+        raise NotImplementedError("high-res geometric branch")
+    hi = torch.arange(0, H, max(1, H // 50))
+    wi = torch.arange(0, W, max(1, W // 50))
+    xs = xg[:, hi[:, None], wi[None, :]].reshape(B, -1)
+    ys = yg[:, hi[:, None], wi[None, :]].reshape(B, -1)
+    r = rays[:, hi[:, None], wi[None, :], :]
+    rx = (r[..., 0] / r[..., 2]).reshape(B, -1)
+    ry = (r[..., 1] / r[..., 2]).reshape(B, -1)
+    ones = torch.ones_like(xs)
+
+    def solve(ratio, tgt):
+        A = torch.stack([ones, ratio], 2)
+        return torch.linalg.solve(torch.bmm(A.transpose(1, 2), A), torch.bmm(A.transpose(1, 2), tgt.unsqueeze(2)))[..., 0]
+
+    sx, sy = solve(rx, xs), solve(ry, ys)
+    K = torch.zeros(B, 3, 3)
+    K[:, 0, 0], K[:, 1, 1], K[:, 0, 2], K[:, 1, 2], K[:, 2, 2] = sx[:, 1], sy[:, 1], sx[:, 0], sy[:, 0], 1.0
+    return K
+
+
+def rot_to_quat(m):
+    """geometry.py:655-713 (+ standardize_quaternion: w >= 0)."""
+    bd = m.shape[:-2]
+    m00, m01, m02, m10, m11, m12, m20, m21, m22 = torch.unbind(m.reshape(bd + (9,)), -1)
+    qa = torch.stack([1 + m00 + m11 + m22, 1 + m00 - m11 - m22, 1 - m00 + m11 - m22, 1 - m00 - m11 + m22], -1)
+    qa = torch.where(qa > 0, torch.sqrt(torch.clamp(qa, min=0)), torch.zeros_like(qa))
+    cand = torch.stack([
+        torch.stack([qa[..., 0] ** 2, m21 - m12, m02 - m20, m10 - m01], -1),
+        torch.stack([m21 - m12, qa[..., 1] ** 2, m10 + m01, m02 + m20], -1),
+        torch.stack([m02 - m20, m10 + m01, qa[..., 2] ** 2, m12 + m21], -1),
+        torch.stack([m10 - m01, m20 + m02, m21 + m12, qa[..., 3] ** 2], -1)], -2)
+    cand = cand / (2.0 * qa[..., None].max(torch.tensor(0.1)))
+    out = cand[F.one_hot(qa.argmax(-1), 4) > 0.5, :].reshape(bd + (4,))
+    out = out[..., [1, 2, 3, 0]]
+    return torch.where(out[..., 3:4] < 0, -out, out)
+
+
+def preprocess_views(views):
+    """inference.py:222-311."""
+    out = []
+    for v in views:
+        pv = {k: (_t(x) if not isinstance(x, (list, tuple)) else x) for k, x in v.items()}
+        H, W = pv["img"].shape[-2:]
+        if "intrinsics" in pv:
+            pv["ray_directions"] = rays_from_intrinsics(pv.pop("intrinsics"), H, W)
+        elif "ray_directions" in pv:
+            rd = pv["ray_directions"]
+            pv["ray_directions"] = rd / (torch.norm(rd, dim=-1, keepdim=True) + 1e-8)
+        if "depth_z" in pv:
+            dz = pv.pop("depth_z")
+            rd = pv["ray_directions"]
+            pts = dz[..., None] * (rd / rd[..., 2:3])
+            pv["depth_along_ray"] = torch.norm(pts, dim=-1, keepdim=True)
+        if "camera_poses" in pv:
+            cp = pv.pop("camera_poses")
+            if isinstance(cp, (tuple, list)):
+                pv["camera_pose_quats"], pv["camera_pose_trans"] = _t(cp[0]), _t(cp[1])
+            else:
+                pv["camera_pose_quats"] = rot_to_quat(cp[:, :3, :3])
+                pv["camera_pose_trans"] = cp[:, :3, 3]
+        if "is_metric_scale" not in pv:
+            pv["is_metric_scale"] = torch.ones(pv["img"].shape[0], dtype=torch.bool)
+        if "ray_directions" in pv:
+            pv["ray_directions_cam"] = pv.pop("ray_directions")
+        out.append(pv)
+    return out

@@ -1,0 +1,79 @@
+"""Pin the CPU oracle (oracle/mapa_oracle.py) against fixtures produced by the REAL reference
+(tests/golden/make_golden.py).  Same synthetic weights, same seeded inputs; fp32 both sides, so the only
+differences are ATen op-grouping rounding: tolerance 2e-5 rel-L2 (measured ~1e-6)."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, rel_l2
+from mapanything.utils import synthetic
+
+TOL = 2e-5
+
+CASES = {
+    "cfg1_224": dict(views=2, h=224, w=224, seed=1),
+    "v2_518": dict(views=2, h=518, w=518, seed=2),
+    "mm_224": dict(views=2, h=224, w=224, seed=4, multimodal=True),
+}
+
+
+def make_views(case):
+    n, h, w, seed = case["views"], case["h"], case["w"], case["seed"]
+    imgs = synthetic.synthetic_images(n, h, w, seed)
+    views = []
+    for v in range(n):
+        view = {"img": torch.from_numpy(imgs[v]), "data_norm_type": ["dinov2"]}
+        if case.get("multimodal"):
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
+            view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
+            view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
+        views.append(view)
+    return views
+
+
+@pytest.fixture(scope="module")
+def oracle(synthetic_sd):
+    from oracle.mapa_oracle import MapAnythingOracle
+
+    torch.set_num_threads(min(8, os.cpu_count()))
+    return MapAnythingOracle(synthetic_sd)
+
+
+def _steps(name):
+    meta = json.load(open(os.path.join(GOLDEN, "golden_meta.json")))
+    return meta[name]["steps_out_tap_dpt"]
+
+
+@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "v2_518"])
+def test_oracle_matches_reference(oracle, golden, name):
+    g = golden(name)
+    out_step, tap_step, dpt_step = _steps(name)
+    with torch.no_grad():
+        preds = oracle.infer(make_views(CASES[name]))
+    taps = oracle.taps
+    checked = 0
+    for key, ref in g.items():
+        if key.startswith("out_"):
+            k = key[4:]
+            mine = torch.stack([p[k].float() for p in preds], 0).numpy()
+            if mine.ndim >= 4 and k not in ("intrinsics", "camera_poses"):
+                mine = mine[:, :, ::out_step, ::out_step]
+        elif key == "tap_encoder":
+            mine = taps["encoder"].numpy()[:, :, ::tap_step, ::tap_step]
+        elif key == "tap_fused_nhwc":
+            mine = taps["fused_nhwc"].numpy()[:, ::tap_step, ::tap_step, :]
+        elif key in ("tap_aat_final", "tap_aat_l11", "tap_aat_l17"):
+            mine = taps[key[4:]].numpy()[:, :, :, ::tap_step, ::tap_step]
+        elif key == "tap_dpt_feature":
+            mine = taps["dpt_feature"].numpy()[:, :, ::dpt_step, ::dpt_step]
+        else:
+            mine = taps[key[4:]].numpy()
+        assert mine.shape == ref.shape, (key, mine.shape, ref.shape)
+        err = rel_l2(mine, ref)
+        assert err < TOL, f"{name}:{key} rel-L2 {err:.3e}"
+        checked += 1
+    assert checked >= 15
