@@ -1,0 +1,155 @@
+"""MapAnything feed-forward inference benchmark on MI355X (views/sec, N-view 518x518 bf16).
+
+  python bench.py                        # N=1: configs[1] = 8 views 518x518 bf16 image-only infer on 1 GPU
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+      bench.py --gpus N                  # 8 views per GPU (weak scaling), global-attention K/V all-gathered
+
+One step = one full `MapAnything.infer(views)` (validation, forward, post-processing with edge masks) over
+synthetic images with inputs already resident in HBM.  Prints ONE JSON line on rank 0.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "map-anything_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_HBM_GBS = 8000.0
+
+
+def enc_linear_flops_per_view(T):
+    """DINOv2 linears + patch-embed per view (2*M*N*K), M = T+1 tokens (T for patch embed)."""
+    R = T + 1
+    per_block = 2 * R * (1024 * 3072 + 1024 * 1024 + 1024 * 4096 * 2)
+    return 24 * per_block + 2 * T * 588 * 1024
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--views-per-gpu", type=int, default=8)
+    ap.add_argument("--res", type=int, default=518)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from mapanything.models import MapAnything
+    from mapanything.utils import synthetic
+    from tests_helpers import released_config
+
+    V_total = args.views_per_gpu * world
+    H = W = args.res
+    model = MapAnything(**released_config(), precision=args.precision).load_synthetic_weights().to(dev).eval()
+    if world > 1:
+        model.enable_view_sharding(dist.group.WORLD)
+    imgs = synthetic.synthetic_images(V_total, H, W, seed=2)
+    views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in imgs]
+
+    def step():
+        return model.infer(views)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    eng = model.engine()
+    if not args.no_kernel_timing:
+        eng.enable_kernel_timing()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ktimes = eng.collect_kernel_timing() if not args.no_kernel_timing else {}
+    ms = dt / args.steps * 1e3
+    value = V_total * args.steps / dt
+
+    if rank == 0:
+        T = (H // 14) * (W // 14)
+        roofline = None
+        if ktimes:
+            # dominant kernel by total time inside the timed region
+            kind = max(ktimes, key=lambda k: ktimes[k]["ms"])
+            kt = ktimes[kind]
+            achieved = kt["flops"] / (kt["ms"] * 1e-3) / 1e12 if kt["flops"] else None
+            roofline = {"kernel": kind, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
+                        "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
+                        "traffic": None, "launches": kt["count"], "avg_launch_us": kt["ms"] * 1e3 / kt["count"],
+                        "per_kernel": {k: {"ms_per_step": v["ms"] / args.steps,
+                                           "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["flops"] else None}
+                                       for k, v in ktimes.items()}}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(model, imgs, H, W)
+        L = V_total * T + 1
+        gf_view = (1870.9e9 + 36864.0 * L * L / V_total) / 1e12 if H == 518 else None
+        line = {
+            "metric": "views/sec + ms/infer, N-view 518x518 bf16 at 1/2/4/8 MI355X",
+            "value": value, "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
+            "config": {"workload": f"{V_total}-view {H}x{W} image-only MapAnything.infer (configs[1] at N=1)",
+                       "views": V_total, "views_per_gpu": args.views_per_gpu, "height": H, "width": W,
+                       "batch_per_view": 1,
+                       "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else "single"},
+            "tflops_effective": (gf_view * value) if gf_view else None,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(model, imgs, H, W):
+    """The fp32 CPU oracle (oracle/mapa_oracle.py, test infrastructure) timed on this host's cores on the same
+    8-view workload, one repetition."""
+    from oracle.mapa_oracle import MapAnythingOracle
+
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    oracle = MapAnythingOracle(model._sd)
+    views = [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]} for i in imgs]
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        oracle.infer(views)
+    dt = time.perf_counter() - t0
+    return {"value": len(views) / dt, "unit": "views/s", "cores": cores, "kind": "port",
+            "sample": f"{len(views)} views {H}x{W}, 1 infer (apply_mask=False), fp32 torch-CPU oracle",
+            "seconds": dt}
+
+
+if __name__ == "__main__":
+    main()

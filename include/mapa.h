@@ -1,0 +1,164 @@
+/* mapa.h — C ABI of the MI355X-native MapAnything hot path (libmapa.so, gfx950).
+ *
+ * The reference has no native code on this path: every op below replaces a PyTorch ATen call of the
+ * reference's feed-forward `MapAnything.forward` (mapanything/models/mapanything/model.py:1657-2152) and is
+ * bound from Python with ctypes by the host mirror `map-anything_amd/mapanything/_native.py`
+ * (INTEGRATION.md shows the binding).  Conventions:
+ *   - every pointer is a device pointer owned by the caller; the library never allocates or frees;
+ *   - all work is enqueued on `stream`; no host synchronisation inside any call (graph-capturable);
+ *   - return 0 on success, non-zero on a rejected argument or a failed launch; `mapa_last_error()` then
+ *     returns a thread-local message;
+ *   - activations are row-major "token x channel" (NHWC for images); weights keep nn.Linear's [out][in]
+ *     layout (convs re-packed once to [out][ky][kx][in]).
+ */
+#ifndef MAPA_H
+#define MAPA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
+
+enum { MAPA_F32 = 0, MAPA_BF16 = 1 };
+enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
+enum { MAPA_OUT_ROWMAJOR = 0, MAPA_OUT_PIXSHUF = 1 };
+enum { MAPA_ACT_NONE = 0, MAPA_ACT_GELU = 1, MAPA_ACT_RELU = 2 };
+
+const char* mapa_last_error(void);
+int mapa_version(void);
+/* 1 if a gfx950 device is visible and the code object loads on it, else 0 (message in mapa_last_error). */
+int mapa_device_check(int device);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * GEMM / implicit-GEMM convolution: C[M,N] = A[M,K] * W[N,K]^T, fused epilogue
+ *   v = acc + bias[n % bias_mod]; v = act(v); v *= gamma[n]; v += resid1[o] + resid2[o];
+ *   out_f32[o] = v; out_lp[o] = lowp(v); out_lp_relu[o] = lowp(max(v,0))
+ * Replaces nn.Linear (transformer_blocks.py:65-212, dinov2 layers/block.py:93-118, mlp_head.py, pose_head.py),
+ * nn.Conv2d 1x1/3x3 (dpt.py:94-311, dpt_block.py:114-177, pose_head.py:18-48, dense_rep_encoder.py:31-287),
+ * nn.ConvTranspose2d k=s (dpt.py:101-131; out_mode PIXSHUF) and the 14x14/14 patch-embed conv.
+ * dtype BF16: A, W, out_lp bf16 (fp32 accumulate); dtype F32: everything fp32 (exact-fp32 parity mode).
+ * ------------------------------------------------------------------------------------------------------- */
+typedef struct {
+  int dtype;
+  int M, N, K;
+  const void* A;
+  int64_t lda;
+  const void* W;
+  int64_t ldw;
+  int a_mode; /* MAPA_A_DENSE or MAPA_A_CONV3X3 (A = NHWC [img][IH][IW][C], K = 9*C, pad 1) */
+  int conv_C, conv_IH, conv_IW, conv_OH, conv_OW, conv_stride;
+  const float* bias;
+  int bias_mod; /* 0 -> N */
+  const float* gamma;
+  int act;
+  const float* resid1;
+  const float* resid2;
+  float* out_f32;
+  void* out_lp;
+  void* out_lp_relu;
+  int64_t ldo;
+  int out_mode; /* MAPA_OUT_ROWMAJOR or MAPA_OUT_PIXSHUF (n = (ky*s+kx)*cout + co, m = img*h*w + y*w + x) */
+  int ps_s, ps_h, ps_w, ps_cout;
+} mapa_gemm_desc;
+
+int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Flash attention forward, head_dim 64, non-causal, softmax scale 1/8 (F.scaled_dot_product_attention at
+ * dinov2.py:136 and transformer_blocks.py:198-201).  Element (b, h, i, d) of Q lives at
+ *   q + b*q_bstride + i*q_rstride + h*64 + d   (same for k, v, o), so the packed qkv GEMM output is read in place.
+ * Q rows [0, seq_q) attend to K/V rows [0, seq_kv) of the same batch; o receives the per-head outputs.
+ * lse (optional, f32 [batch][heads][seq_q]) receives log-sum-exp of the scaled scores for chunk merging.
+ * ------------------------------------------------------------------------------------------------------- */
+typedef struct {
+  int dtype;
+  int batch, heads, seq_q, seq_kv;
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  int64_t q_bstride, q_rstride, k_bstride, k_rstride, v_bstride, v_rstride, o_bstride, o_rstride;
+  float* lse;
+} mapa_attn_desc;
+
+int mapa_attention(const mapa_attn_desc* d, mapa_stream_t stream);
+
+/* LayerNorm over the last dim (nn.LayerNorm eps=1e-6): y = (x-mean)/sqrt(var+eps)*w + b.
+ * x: f32 rows (row stride ldx); outputs optional: y_f32 (ldy), y_lp (bf16 or f32 per lp_dtype, ldy).
+ * Output row r reads input row (in_group > 0 ? (r / in_group) * in_group_stride + r % in_group : r) + in_row_off
+ * (e.g. drop the DINOv2 cls row of every view: group T, stride T+1, offset 1). */
+int mapa_layernorm(const float* x, int64_t ldx, int rows, int dim, const float* w, const float* b, float eps,
+                   float* y_f32, void* y_lp, int lp_dtype, int64_t ldy, int in_group, int64_t in_group_stride,
+                   int in_row_off, mapa_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Elementwise / layout kernels of the path
+ * ------------------------------------------------------------------------------------------------------- */
+/* img NCHW f32 [n][3][H][W] -> patches [n*(H/14)*(W/14)][kpad] (k = c*196 + ky*14 + kx, zero for k >= 588),
+ * dtype bf16 or f32 (vision_transformer.py:244-249 PatchEmbed as GEMM). */
+int mapa_patchify(const float* img, int n, int H, int W, void* out, int dtype, int kpad, mapa_stream_t stream);
+
+/* x[v][0] = cls + pos[0]; x[v][1+t] = patch[v*T+t] + pos[1+t]  (vision_transformer.py:250-252) */
+int mapa_assemble_tokens(const float* patch, const float* cls, const float* pos, int n, int T, int dim, float* x,
+                         mapa_stream_t stream);
+
+/* rows r in [r0, r1): x[r][:] += vec[:]   (ref-view PE, alternating_attention_transformer.py:618-626) */
+int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, const float* vec, mapa_stream_t stream);
+
+/* Bilinear resize, align_corners=True, NHWC.  Output grid is the full (OHf, OWf) grid of F.interpolate; only
+ * rows < OH and cols < OW are written (fused crop, dpt.py:213).  in: f32 or bf16 (in_dtype), out: out_dtype. */
+int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH, int OW,
+                     void* out, int out_dtype, mapa_stream_t stream);
+
+/* mean over `tokens` rows per image: x [n][tokens][C] f32 -> y [n][C] (AdaptiveAvgPool2d(1), pose_head.py:150) */
+int mapa_mean_tokens(const float* x, int n, int tokens, int C, float* y, mapa_stream_t stream);
+
+/* small fp32 linear for M <= 64 rows: y[m][n] = act(sum_k x[m][k] w[n][k] + b[n])  (pose/scale MLPs) */
+int mapa_linear_small(const float* x, int M, int K, const float* w, const float* b, int N, int act, float* y,
+                      mapa_stream_t stream);
+
+/* per view: pose raw (7) -> t, unit quat, R; scale raw -> s = clip(exp(.), 1e-8)   (adaptors.py:171-212, 586-732)
+ * pose_out[v] = {t(3) * s, q(4), R(9), t(3) raw} (19 floats); poses44[v] (optional) = 4x4 [R | t*s];
+ * scale_out[b] = s.  Rows are view-major: v = view * batch + b. */
+int mapa_pose_scale_finalize(const float* pose_raw, const float* scale_raw, int nviews, int batch, float* pose_out,
+                             float* scale_out, float* poses44, mapa_stream_t stream);
+
+/* Dense head tail: conv1x1 128->6 on the ReLU'd hidden map + adaptors + output assembly (dpt.py:306-310,
+ * adaptors.py:393-523/1012-1133/1740-1796, model.py:1871-1923/2116-2150, geometry.py:855-907).
+ * hidden: [n][H*W][128] (bf16 or f32, dtype); w6 [6][128] f32, b6 [6]; pose_out/scale from finalize.
+ * Outputs (NHWC f32, [n][H][W][c]): pts3d(3) pts3d_cam(3) rays(3) depth(1) conf(1) logits(1) mask(u8). */
+int mapa_dense_head_out(const void* hidden, int dtype, int n, int HW, const float* w6, const float* b6,
+                        const float* pose_out, const float* scale, int batch, float* pts3d,
+                        float* pts3d_cam, float* rays, float* depth, float* conf, float* logits, uint8_t* mask,
+                        mapa_stream_t stream);
+
+/* infer() post-processing (inference.py:407-480): mask_out = mask_in & ~(depth_edge & normal_edge) per view
+ * (geometry.py:1788-1853, 2102-2145, 2200-2258).  pts3d/pts3d_cam [n][H][W][3] f32 (depth_z = pts3d_cam z),
+ * masks u8 [n][H][W].  work: n*H*W*17 bytes of scratch when use_edges. */
+int mapa_postprocess_mask(const float* pts3d, const float* pts3d_cam, const uint8_t* mask_in, uint8_t* mask_out,
+                          int n, int H, int W, float normal_tol_deg, float depth_rtol, int use_edges, void* work,
+                          mapa_stream_t stream);
+
+/* recover_pinhole_intrinsics_from_ray_directions (geometry.py:304-447, <= 1 MPix branch): rays [n][H][W][3]
+ * unit directions -> K [n][3][3]. */
+int mapa_recover_intrinsics(const float* rays, int n, int H, int W, float* K, mapa_stream_t stream);
+
+/* rgb() of image.py:93-131: img NCHW [n][3][H][W] -> clip(img*std+mean, 0, 1) as NHWC [n][H][W][3]. */
+int mapa_denorm_image(const float* img, int n, int H, int W, const float* mean, const float* stdv, float* out,
+                      mapa_stream_t stream);
+
+/* Copy/convert a strided row block: dst[r][c] = src[r][c] (f32 -> bf16/f32). */
+int mapa_convert_rows(const float* src, int64_t lds, int rows, int cols, void* dst, int dst_dtype, int64_t ldd,
+                      mapa_stream_t stream);
+
+/* Deterministic synthetic weights on device: out[i] = (2*u_i - 1)*half + mid, u_i = splitmix64 stream of
+ * `seed` (bit-identical to mapanything/utils/synthetic.py). */
+int mapa_fill_splitmix(float* out, int64_t n, uint64_t seed, float half, float mid, mapa_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAPA_H */

@@ -1,0 +1,368 @@
+// Flash-attention forward for gfx950, head_dim 64, non-causal, softmax scale 1/8.
+//
+// Replaces F.scaled_dot_product_attention of the DINOv2 SDPA wrapper (uniception/models/encoders/dinov2.py:136,
+// q,k,v (V*B, 16, 1370, 64)) and of the AAT SelfAttentionBlock (uniception/models/utils/transformer_blocks.py:
+// 198-201): global layers over all V*1369+1 tokens, frame layers per view over 1369 tokens.
+//
+// Structure (one workgroup = 4 waves = 128 query rows of one (batch, head); each wave owns 32 query rows):
+//  * Q stays in registers for the whole K/V sweep; K/V tiles of 64 keys are staged HBM -> LDS with
+//    global_load_lds into a two-slot ring (one barrier per tile).
+//  * Swapped QK^T: S^T = K * Q^T with v_mfma_f32_32x32x16_bf16, so a lane owns one query row (lane & 31) and
+//    32 of its key scores in registers: the row max / row sum are in-lane plus one cross-half exchange.
+//  * The S^T accumulator is re-used directly as the B operand of O^T = V^T * P^T (accumulator-as-operand,
+//    no LDS round trip for P); V^T fragments come from ds_read_b64_tr_b16 transposed LDS reads.
+//  * Online softmax in the log2 domain (v_exp_f32), fp32 running max / sum, O^T in 32 fp32 accumulators.
+//  * K LDS rows are XOR-swizzled by (row>>1)&7 and V rows by ((row>>1)&1)<<2 (applied on the LDS-DMA source
+//    address), which makes both the b128 K reads and the transposed V reads bank-conflict free.
+//  * Precise variant (dtype f32): identical dataflow on v_mfma_f32_32x32x2_f32 (exact fp32 products).
+#include "mapa_common.h"
+
+namespace {
+
+constexpr int NT = 256;        // 4 waves
+constexpr int QBLK = 128;      // query rows per workgroup
+constexpr int KT = 64;         // keys per K/V tile
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+struct AttnArgs {
+  const void* q;
+  const void* k;
+  const void* v;
+  void* o;
+  float* lse;
+  int64_t qb, qr, kb, kr, vb, vr, ob, orr;
+  int batch, heads, seq_q, seq_kv;
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q = nblk / 8, r = nblk % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef short s8v __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ s4v tr_read(const char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(p));
+}
+
+// ------------------------------------------------------------------------------------------------ bf16
+__global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
+  constexpr int TILE = KT * 128;  // 64 rows x 128 B
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hl = lane >> 5, l32 = lane & 31;
+  const int nqt = (p.seq_q + QBLK - 1) / QBLK;
+  const int nblk = nqt * p.heads * p.batch;
+  const int bid = xcd_remap(blockIdx.x, nblk);
+  const int qt = bid % nqt, hb = bid / nqt, h = hb % p.heads, b = hb / p.heads;
+
+  const bf16_t* qbase = reinterpret_cast<const bf16_t*>(p.q) + b * p.qb + h * 64;
+  const bf16_t* kbase = reinterpret_cast<const bf16_t*>(p.k) + b * p.kb + h * 64;
+  const bf16_t* vbase = reinterpret_cast<const bf16_t*>(p.v) + b * p.vb + h * 64;
+  const int qrow = qt * QBLK + wave * 32 + l32;
+  const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
+
+  // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 (exact).
+  b8 qf[4];
+#pragma unroll
+  for (int kk = 0; kk < 4; ++kk) {
+    const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
+    s8v sc;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sc[j] = (short)f32_to_bf16(bf16_to_f32((bf16_t)raw[j]) * 0.125f);
+    qf[kk] = __builtin_bit_cast(b8, sc);
+  }
+
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  const int nkt = (p.seq_kv + KT - 1) / KT;
+
+  auto stage = [&](int slot, int kt) {
+    char* Ks = lds + slot * 2 * TILE;
+    char* Vs = Ks + TILE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (i * 4 + wave) * 8 + (lane >> 3), pos = lane & 7;
+      const int key = kt * KT + row;
+      const int kc = pos ^ ((row >> 1) & 7);
+      const int vc = pos ^ (((row >> 1) & 1) << 2);
+      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)key * p.kr + kc * 8) : zero;
+      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)key * p.vr + vc * 8) : zero;
+      const int base = (i * 4 + wave) * 64 * 16;
+      __builtin_amdgcn_global_load_lds(ks, Ks + base, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(vs, Vs + base, 16, 0, 0);
+    }
+  };
+
+  f32x16 o[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    const char* Ks = lds + cur * 2 * TILE;
+    const char* Vs = Ks + TILE;
+
+    // S^T = K Q^T  (2 x 32x32 tiles = 64 keys x 32 queries)
+    f32x16 st[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[kb][r] = 0.f;
+      const int row = kb * 32 + l32;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int chunk = kk * 2 + hl;
+        const b8 kf = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], st[kb], 0, 0, 0);
+      }
+    }
+    // mask the tail tile, go to the log2 domain, running max
+    const bool tail = (kt + 1) * KT > p.seq_kv;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float s = st[kb][r] * LOG2E;
+        if (tail) {
+          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= p.seq_kv) s = -INFINITY;
+        }
+        st[kb][r] = s;
+        mx = fmaxf(mx, s);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = __builtin_amdgcn_exp2f(st[kb][r] - m_new);
+        st[kb][r] = e;
+        ls += e;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+
+    // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T via transposed LDS reads
+    b8 pf[2][2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        s8v t;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = (short)f32_to_bf16(st[kb][8 * s + j]);
+        pf[kb][s] = __builtin_bit_cast(b8, t);
+      }
+    const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+      const int c0 = dt * 32 + 16 * grp + 4 * p4;  // column (d) this lane addresses
+      const int chunk = c0 >> 3, within = (c0 & 7) * 2;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int R0 = kb * 32 + 16 * s + 4 * hl + q4;
+          const int R1 = R0 + 8;
+          const s4v lo = tr_read(Vs + R0 * 128 + ((chunk ^ (((R0 >> 1) & 1) << 2)) << 4) + within);
+          const s4v hi = tr_read(Vs + R1 * 128 + ((chunk ^ (((R1 >> 1) & 1) << 2)) << 4) + within);
+          const s8v vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8, vv), pf[kb][s], o[dt], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (qrow < p.seq_q) {
+    const float inv = 1.f / l_tot;
+    bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hl;
+        uint2 pk;
+        pk.x = pack_bf16x2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        pk.y = pack_bf16x2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(obase + d) = pk;
+      }
+    if (p.lse && hl == 0) p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_run + __log2f(l_tot)) * LN2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ f32
+__global__ void __launch_bounds__(NT, 1) attn_fwd_f32(AttnArgs p) {
+  constexpr int TILE = KT * 256;  // 64 rows x 256 B
+  __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hl = lane >> 5, l32 = lane & 31;
+  const int nqt = (p.seq_q + QBLK - 1) / QBLK;
+  const int nblk = nqt * p.heads * p.batch;
+  const int bid = xcd_remap(blockIdx.x, nblk);
+  const int qt = bid % nqt, hb = bid / nqt, h = hb % p.heads, b = hb / p.heads;
+
+  const float* qbase = reinterpret_cast<const float*>(p.q) + b * p.qb + h * 64;
+  const float* kbase = reinterpret_cast<const float*>(p.k) + b * p.kb + h * 64;
+  const float* vbase = reinterpret_cast<const float*>(p.v) + b * p.vb + h * 64;
+  const int qrow = qt * QBLK + wave * 32 + l32;
+  const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
+
+  // lane half hl owns hd chunks 2c+hl (c = 0..7); step s of chunk-pair c uses hd 8c + 4hl + s
+  f32x4 qf[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    qf[c] = *reinterpret_cast<const f32x4*>(qbase + (int64_t)qrow_c * p.qr + (2 * c + hl) * 4);
+    qf[c] *= 0.125f;
+  }
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  const int nkt = (p.seq_kv + KT - 1) / KT;
+
+  auto stage = [&](int slot, int kt) {
+    char* Ks = lds + slot * 2 * TILE;
+    char* Vs = Ks + TILE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (i * 4 + wave) * 4 + (lane >> 4), pos = lane & 15;
+      const int key = kt * KT + row;
+      const int kc = pos ^ (row & 15);
+      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)key * p.kr + kc * 4) : zero;
+      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)key * p.vr + pos * 4) : zero;
+      const int base = (i * 4 + wave) * 64 * 16;
+      __builtin_amdgcn_global_load_lds(ks, Ks + base, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(vs, Vs + base, 16, 0, 0);
+    }
+  };
+
+  f32x16 o[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+    const char* Ks = lds + cur * 2 * TILE;
+    const float* Vs = reinterpret_cast<const float*>(Ks + TILE);
+
+    f32x16 st[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[kb][r] = 0.f;
+      const int row = kb * 32 + l32;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int chunk = 2 * c + hl;
+        const f32x4 kf = *reinterpret_cast<const f32x4*>(Ks + row * 256 + ((chunk ^ (row & 15)) << 4));
+#pragma unroll
+        for (int s = 0; s < 4; ++s) st[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kf[s], qf[c][s], st[kb], 0, 0, 0);
+      }
+    }
+    const bool tail = (kt + 1) * KT > p.seq_kv;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float s = st[kb][r] * LOG2E;
+        if (tail) {
+          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= p.seq_kv) s = -INFINITY;
+        }
+        st[kb][r] = s;
+        mx = fmaxf(mx, s);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    m_run = m_new;
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float e = exp2f(st[kb][r] - m_new);
+        st[kb][r] = e;
+        ls += e;
+      }
+    l_run = l_run * alpha + ls;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    // O^T += V^T P^T, k-step s of key block kb uses key (s&3) + 8(s>>2) + 4hl: register s of the S^T tile.
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int key = kb * 32 + (s & 3) + 8 * (s >> 2) + 4 * hl;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(Vs[key * 64 + dt * 32 + l32], st[kb][s], o[dt], 0, 0, 0);
+      }
+    __syncthreads();
+  }
+
+  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (qrow < p.seq_q) {
+    const float inv = 1.f / l_tot;
+    float* obase = reinterpret_cast<float*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hl;
+        f32x4 v = {o[dt][4 * g] * inv, o[dt][4 * g + 1] * inv, o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv};
+        *reinterpret_cast<f32x4*>(obase + d) = v;
+      }
+    if (p.lse && hl == 0) p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_run + log2f(l_tot)) * LN2;
+  }
+}
+
+}  // namespace
+
+extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
+  MAPA_CHECK_ARG(d != nullptr, "mapa_attention: null descriptor");
+  MAPA_CHECK_ARG(d->batch > 0 && d->heads > 0 && d->seq_q > 0 && d->seq_kv > 0,
+                 "mapa_attention: bad shape b=%d h=%d q=%d kv=%d", d->batch, d->heads, d->seq_q, d->seq_kv);
+  MAPA_CHECK_ARG(d->q && d->k && d->v && d->o, "mapa_attention: null pointer");
+  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32, "mapa_attention: bad dtype");
+  const int align = d->dtype == MAPA_BF16 ? 8 : 4;
+  MAPA_CHECK_ARG(d->q_rstride % align == 0 && d->k_rstride % align == 0 && d->v_rstride % align == 0 &&
+                     d->o_rstride % 4 == 0,
+                 "mapa_attention: row strides must keep 16-B alignment");
+  AttnArgs a;
+  a.q = d->q; a.k = d->k; a.v = d->v; a.o = d->o; a.lse = d->lse;
+  a.qb = d->q_bstride; a.qr = d->q_rstride; a.kb = d->k_bstride; a.kr = d->k_rstride;
+  a.vb = d->v_bstride; a.vr = d->v_rstride; a.ob = d->o_bstride; a.orr = d->o_rstride;
+  a.batch = d->batch; a.heads = d->heads; a.seq_q = d->seq_q; a.seq_kv = d->seq_kv;
+  const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
+  if (d->dtype == MAPA_BF16)
+    hipLaunchKernelGGL(attn_fwd_bf16, dim3(nblk), dim3(NT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(attn_fwd_f32, dim3(nblk), dim3(NT), 0, stream, a);
+  MAPA_CHECK_LAUNCH("mapa_attention");
+  return 0;
+}

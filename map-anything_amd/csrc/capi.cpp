@@ -1,0 +1,39 @@
+// Library-level C ABI: thread-local error string, version, device probe.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/mapa.h"
+
+static thread_local char g_err[512] = "";
+
+int mapa_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return 1;
+}
+
+extern "C" const char* mapa_last_error(void) { return g_err; }
+
+extern "C" int mapa_version(void) { return 1; }
+
+extern "C" int mapa_device_check(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device) {
+    mapa_set_error("mapa_device_check: no HIP device %d (count %d)", device, n);
+    return 0;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    mapa_set_error("mapa_device_check: hipGetDeviceProperties failed");
+    return 0;
+  }
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    mapa_set_error("mapa_device_check: device %d is %s, library is built for gfx950", device, prop.gcnArchName);
+    return 0;
+  }
+  return 1;
+}

@@ -1,0 +1,377 @@
+// Memory-bound layout / elementwise kernels of the MapAnything hot path (gfx950).
+// Each is HBM-bound; loads/stores are 16-B vectorised where the layout allows.
+#include "mapa_common.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+inline int grid_for(int64_t n, int per_block = TPB) {
+  int64_t g = (n + per_block - 1) / per_block;
+  if (g > 65536) g = 65536;
+  return (int)(g < 1 ? 1 : g);
+}
+
+// ---------------------------------------------------------------------------------------------- patchify
+// PatchEmbed (vision_transformer.py:244-249, Conv2d 3->1024 k14 s14) as im2col rows for the GEMM.
+template <typename T>
+__global__ void patchify_kernel(const float* __restrict__ img, int n, int H, int W, T* __restrict__ out, int kpad) {
+  const int hp = H / 14, wp = W / 14;
+  const int64_t total = (int64_t)n * hp * wp * kpad;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(e % kpad);
+    const int64_t row = e / kpad;
+    float v = 0.f;
+    if (k < 588) {
+      const int px = (int)(row % wp);
+      const int64_t r2 = row / wp;
+      const int py = (int)(r2 % hp);
+      const int im = (int)(r2 / hp);
+      const int c = k / 196, rem = k - c * 196, ky = rem / 14, kx = rem - ky * 14;
+      v = img[(((int64_t)im * 3 + c) * H + py * 14 + ky) * W + px * 14 + kx];
+    }
+    if constexpr (sizeof(T) == 2) out[e] = f32_to_bf16(v);
+    else out[e] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------- token assembly
+__global__ void assemble_tokens_kernel(const float* __restrict__ patch, const float* __restrict__ cls,
+                                       const float* __restrict__ pos, int n, int T, int dim, float* __restrict__ x) {
+  const int d4 = dim / 4;
+  const int64_t total = (int64_t)n * (T + 1) * d4;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % d4) * 4;
+    const int64_t r = e / d4;
+    const int t = (int)(r % (T + 1));
+    const int im = (int)(r / (T + 1));
+    f32x4 base = t == 0 ? *reinterpret_cast<const f32x4*>(cls + c)
+                        : *reinterpret_cast<const f32x4*>(patch + ((int64_t)im * T + t - 1) * dim + c);
+    base += *reinterpret_cast<const f32x4*>(pos + (int64_t)t * dim + c);
+    *reinterpret_cast<f32x4*>(x + r * dim + c) = base;
+  }
+}
+
+__global__ void add_rowvec_kernel(float* __restrict__ x, int64_t ldx, int r0, int r1, int dim,
+                                  const float* __restrict__ vec) {
+  const int64_t total = (int64_t)(r1 - r0) * dim;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % dim);
+    const int64_t r = r0 + e / dim;
+    x[r * ldx + c] += vec[c];
+  }
+}
+
+// -------------------------------------------------------------------------- bilinear, align_corners=True
+template <typename T>
+__device__ __forceinline__ f32x4 load4(const T* p) {
+  if constexpr (sizeof(T) == 2) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    return f32x4{bf16_to_f32(u.x & 0xffff), bf16_to_f32(u.x >> 16), bf16_to_f32(u.y & 0xffff), bf16_to_f32(u.y >> 16)};
+  } else {
+    return *reinterpret_cast<const f32x4*>(p);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store4(T* p, f32x4 v) {
+  if constexpr (sizeof(T) == 2) {
+    uint2 u;
+    u.x = pack_bf16x2(v[0], v[1]);
+    u.y = pack_bf16x2(v[2], v[3]);
+    *reinterpret_cast<uint2*>(p) = u;
+  } else {
+    *reinterpret_cast<f32x4*>(p) = v;
+  }
+}
+
+// F.interpolate(mode="bilinear", align_corners=True) as ATen computes it (scale = (in-1)/(out-1) in fp32,
+// h1 = h0 + (h0 < in-1), lambdas 1-l / l), NHWC, 4 channels per thread.
+template <typename TI, typename TO>
+__global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
+                                   int OW, TO* __restrict__ out) {
+  const int c4 = C / 4;
+  const int64_t total = (int64_t)n * OH * OW * c4;
+  const float sh = OHf > 1 ? (float)(IH - 1) / (float)(OHf - 1) : 0.f;
+  const float sw = OWf > 1 ? (float)(IW - 1) / (float)(OWf - 1) : 0.f;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % c4) * 4;
+    int64_t r = e / c4;
+    const int ox = (int)(r % OW);
+    r /= OW;
+    const int oy = (int)(r % OH);
+    const int im = (int)(r / OH);
+    const float fy = sh * oy, fx = sw * ox;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < IH - 1 ? 1 : 0), x1 = x0 + (x0 < IW - 1 ? 1 : 0);
+    const float ly1 = fy - y0, ly0 = 1.f - ly1, lx1 = fx - x0, lx0 = 1.f - lx1;
+    const TI* base = in + (int64_t)im * IH * IW * C + c;
+    const f32x4 v00 = load4(base + ((int64_t)y0 * IW + x0) * C);
+    const f32x4 v01 = load4(base + ((int64_t)y0 * IW + x1) * C);
+    const f32x4 v10 = load4(base + ((int64_t)y1 * IW + x0) * C);
+    const f32x4 v11 = load4(base + ((int64_t)y1 * IW + x1) * C);
+    const f32x4 o = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+    store4(out + (((int64_t)im * OH + oy) * OW + ox) * C + c, o);
+  }
+}
+
+// ------------------------------------------------------------------------------------------ mean over T
+__global__ void mean_tokens_kernel(const float* __restrict__ x, int n, int T, int C, float* __restrict__ y) {
+  const int64_t total = (int64_t)n * C;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const int im = (int)(e / C);
+    const float* p = x + (int64_t)im * T * C + c;
+    float s = 0.f;
+    for (int t = 0; t < T; ++t) s += p[(int64_t)t * C];
+    y[e] = s / (float)T;
+  }
+}
+
+// -------------------------------------------------------------------------------------- small linear
+__global__ void linear_small_kernel(const float* __restrict__ x, int M, int K, const float* __restrict__ w,
+                                    const float* __restrict__ b, int N, int act, float* __restrict__ y) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= M * N) return;
+  const int m = wave / N, n = wave % N;
+  const float* xr = x + (int64_t)m * K;
+  const float* wr = w + (int64_t)n * K;
+  float s = 0.f;
+  for (int k = lane; k < K; k += 64) s += xr[k] * wr[k];
+  s = wave_sum(s);
+  if (lane == 0) {
+    float v = s + (b ? b[n] : 0.f);
+    if (act == MAPA_ACT_RELU) v = fmaxf(v, 0.f);
+    else if (act == MAPA_ACT_GELU) v = gelu_erf(v);
+    y[(int64_t)m * N + n] = v;
+  }
+}
+
+// --------------------------------------------------------------------- pose / scale adaptors (per view)
+// pose_out[v] = { cam_trans*s (3), quat (4), R row-major (9), t (3) } (19 floats); poses44[v] = 4x4 with
+// [:3,:3] = R(q), [:3,3] = cam_trans*s (inference.py:376-390); scale_out[b] = clip(exp(raw), 1e-8).
+__global__ void pose_scale_finalize_kernel(const float* __restrict__ pose_raw, const float* __restrict__ scale_raw,
+                                           int nviews, int batch, float* __restrict__ pose_out,
+                                           float* __restrict__ scale_out, float* __restrict__ poses44) {
+  const int v = blockIdx.x * blockDim.x + threadIdx.x;
+  if (v < batch) scale_out[v] = fmaxf(expf(scale_raw[v]), 1e-8f);
+  if (v >= nviews) return;
+  const float s = fmaxf(expf(scale_raw[v % batch]), 1e-8f);
+  const float* pr = pose_raw + v * 7;
+  float q[4] = {pr[3], pr[4], pr[5], pr[6]};
+  float nq = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  nq = fmaxf(nq, 1e-8f);
+  for (int i = 0; i < 4; ++i) q[i] /= nq;
+  // quaternion_to_rotation_matrix normalises again (geometry.py:619)
+  const float n2 = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const float x = q[0] / n2, y = q[1] / n2, z = q[2] / n2, w = q[3] / n2;
+  const float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+                      2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+                      2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)};
+  float* po = pose_out + v * 19;
+  for (int i = 0; i < 3; ++i) po[i] = pr[i] * s;
+  for (int i = 0; i < 4; ++i) po[3 + i] = q[i];
+  for (int i = 0; i < 9; ++i) po[7 + i] = R[i];
+  for (int i = 0; i < 3; ++i) po[16 + i] = pr[i];
+  if (poses44) {
+    float* P = poses44 + v * 16;
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) P[r * 4 + c] = R[r * 3 + c];
+      P[r * 4 + 3] = pr[r] * s;
+    }
+    P[12] = 0.f; P[13] = 0.f; P[14] = 0.f; P[15] = 1.f;
+  }
+}
+
+// ---------------------------------------------------------------------------- dense head tail (fused)
+template <typename T>
+__global__ void __launch_bounds__(256) dense_head_out_kernel(
+    const T* __restrict__ hidden, int n, int HW, const float* __restrict__ w6, const float* __restrict__ b6,
+    const float* __restrict__ pose_out, const float* __restrict__ scale, int batch, float* __restrict__ pts3d,
+    float* __restrict__ pts3d_cam, float* __restrict__ rays, float* __restrict__ depth, float* __restrict__ conf,
+    float* __restrict__ logits, uint8_t* __restrict__ mask) {
+  __shared__ float sw[6 * 128 + 6];
+  for (int i = threadIdx.x; i < 6 * 128; i += blockDim.x) sw[i] = w6[i];
+  if (threadIdx.x < 6) sw[768 + threadIdx.x] = b6[threadIdx.x];
+  __syncthreads();
+  const int64_t total = (int64_t)n * HW;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const T* h = hidden + p * 128;
+    float acc[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) acc[c] = sw[768 + c];
+#pragma unroll 4
+    for (int k = 0; k < 128; k += 4) {
+      const f32x4 hv = load4(h + k);
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        acc[c] += hv[0] * sw[c * 128 + k] + hv[1] * sw[c * 128 + k + 1] + hv[2] * sw[c * 128 + k + 2] +
+                  hv[3] * sw[c * 128 + k + 3];
+    }
+    const int v = (int)(p / HW);
+    const float* po = pose_out + v * 19;
+    const float sc = scale[v % batch];  // rows are view-major: v = view * batch + b
+    float rx = acc[0], ry = acc[1], rz = acc[2];
+    const float nr = fmaxf(sqrtf(rx * rx + ry * ry + rz * rz), 1e-8f);
+    rx /= nr; ry /= nr; rz /= nr;
+    const float d = expf(acc[3]);
+    const float cx = rx * d, cy = ry * d, cz = rz * d;
+    const float* R = po + 7;
+    const float* t = po + 16;
+    const float wx = R[0] * cx + R[1] * cy + R[2] * cz + t[0];
+    const float wy = R[3] * cx + R[4] * cy + R[5] * cz + t[1];
+    const float wz = R[6] * cx + R[7] * cy + R[8] * cz + t[2];
+    pts3d[p * 3 + 0] = wx * sc; pts3d[p * 3 + 1] = wy * sc; pts3d[p * 3 + 2] = wz * sc;
+    pts3d_cam[p * 3 + 0] = cx * sc; pts3d_cam[p * 3 + 1] = cy * sc; pts3d_cam[p * 3 + 2] = cz * sc;
+    rays[p * 3 + 0] = rx; rays[p * 3 + 1] = ry; rays[p * 3 + 2] = rz;
+    depth[p] = d * sc;
+    conf[p] = 1.f + expf(acc[4]);
+    logits[p] = acc[5];
+    mask[p] = (1.f / (1.f + expf(-acc[5]))) > 0.5f ? 1 : 0;
+  }
+}
+
+__global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, int rows, int cols, void* dst,
+                                    int bf, int64_t ldd) {
+  const int64_t total = (int64_t)rows * cols;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % cols);
+    const int64_t r = e / cols;
+    const float v = src[r * lds + c];
+    if (bf) reinterpret_cast<bf16_t*>(dst)[r * ldd + c] = f32_to_bf16(v);
+    else reinterpret_cast<float*>(dst)[r * ldd + c] = v;
+  }
+}
+
+__global__ void fill_splitmix_kernel(float* __restrict__ out, int64_t n, uint64_t seed, float half, float mid) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t x = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
+    x ^= x >> 30;
+    x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27;
+    x *= 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    const float u = (float)(uint32_t)(x >> 40) * 5.9604644775390625e-08f;  // 2^-24, exact
+    const float t = __fsub_rn(__fmul_rn(u, 2.0f), 1.0f);
+    out[i] = __fadd_rn(__fmul_rn(t, half), mid);
+  }
+}
+
+}  // namespace
+
+extern "C" int mapa_patchify(const float* img, int n, int H, int W, void* out, int dtype, int kpad,
+                             hipStream_t stream) {
+  MAPA_CHECK_ARG(img && out && n > 0 && H % 14 == 0 && W % 14 == 0 && kpad >= 588, "mapa_patchify: bad args");
+  const int64_t total = (int64_t)n * (H / 14) * (W / 14) * kpad;
+  if (dtype == MAPA_BF16)
+    hipLaunchKernelGGL(patchify_kernel<bf16_t>, dim3(grid_for(total)), dim3(TPB), 0, stream, img, n, H, W,
+                       reinterpret_cast<bf16_t*>(out), kpad);
+  else
+    hipLaunchKernelGGL(patchify_kernel<float>, dim3(grid_for(total)), dim3(TPB), 0, stream, img, n, H, W,
+                       reinterpret_cast<float*>(out), kpad);
+  MAPA_CHECK_LAUNCH("mapa_patchify");
+  return 0;
+}
+
+extern "C" int mapa_assemble_tokens(const float* patch, const float* cls, const float* pos, int n, int T, int dim,
+                                    float* x, hipStream_t stream) {
+  MAPA_CHECK_ARG(patch && cls && pos && x && dim % 4 == 0, "mapa_assemble_tokens: bad args");
+  const int64_t total = (int64_t)n * (T + 1) * (dim / 4);
+  hipLaunchKernelGGL(assemble_tokens_kernel, dim3(grid_for(total)), dim3(TPB), 0, stream, patch, cls, pos, n, T, dim,
+                     x);
+  MAPA_CHECK_LAUNCH("mapa_assemble_tokens");
+  return 0;
+}
+
+extern "C" int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, const float* vec, hipStream_t stream) {
+  MAPA_CHECK_ARG(x && vec && r1 >= r0, "mapa_add_rowvec: bad args");
+  if (r1 == r0) return 0;
+  hipLaunchKernelGGL(add_rowvec_kernel, dim3(grid_for((int64_t)(r1 - r0) * dim)), dim3(TPB), 0, stream, x, ldx, r0,
+                     r1, dim, vec);
+  MAPA_CHECK_LAUNCH("mapa_add_rowvec");
+  return 0;
+}
+
+extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
+                                int OW, void* out, int out_dtype, hipStream_t stream) {
+  MAPA_CHECK_ARG(in && out && C % 4 == 0 && OH <= OHf && OW <= OWf, "mapa_bilinear_ac: bad args");
+  const int64_t total = (int64_t)n * OH * OW * (C / 4);
+  const dim3 g(grid_for(total)), b(TPB);
+  if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
+    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
+                       OWf, OH, OW, (bf16_t*)out);
+  else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16)
+    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t>), g, b, 0, stream, (const float*)in, n, IH, IW, C, OHf, OWf,
+                       OH, OW, (bf16_t*)out);
+  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_F32)
+    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, float>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
+                       OWf, OH, OW, (float*)out);
+  else
+    hipLaunchKernelGGL((bilinear_ac_kernel<float, float>), g, b, 0, stream, (const float*)in, n, IH, IW, C, OHf, OWf,
+                       OH, OW, (float*)out);
+  MAPA_CHECK_LAUNCH("mapa_bilinear_ac");
+  return 0;
+}
+
+extern "C" int mapa_mean_tokens(const float* x, int n, int tokens, int C, float* y, hipStream_t stream) {
+  MAPA_CHECK_ARG(x && y && n > 0 && tokens > 0 && C > 0, "mapa_mean_tokens: bad args");
+  hipLaunchKernelGGL(mean_tokens_kernel, dim3(grid_for((int64_t)n * C)), dim3(TPB), 0, stream, x, n, tokens, C, y);
+  MAPA_CHECK_LAUNCH("mapa_mean_tokens");
+  return 0;
+}
+
+extern "C" int mapa_linear_small(const float* x, int M, int K, const float* w, const float* b, int N, int act,
+                                 float* y, hipStream_t stream) {
+  MAPA_CHECK_ARG(x && w && y && M > 0 && N > 0 && K > 0, "mapa_linear_small: bad args");
+  const int64_t waves = (int64_t)M * N;
+  hipLaunchKernelGGL(linear_small_kernel, dim3((unsigned)((waves * 64 + TPB - 1) / TPB)), dim3(TPB), 0, stream, x, M,
+                     K, w, b, N, act, y);
+  MAPA_CHECK_LAUNCH("mapa_linear_small");
+  return 0;
+}
+
+extern "C" int mapa_pose_scale_finalize(const float* pose_raw, const float* scale_raw, int nviews, int batch,
+                                        float* pose_out, float* scale_out, float* poses44, hipStream_t stream) {
+  MAPA_CHECK_ARG(pose_raw && scale_raw && pose_out && scale_out && nviews > 0 && batch > 0,
+                 "mapa_pose_scale_finalize: bad args");
+  const int m = nviews > batch ? nviews : batch;
+  hipLaunchKernelGGL(pose_scale_finalize_kernel, dim3((m + 63) / 64), dim3(64), 0, stream, pose_raw, scale_raw,
+                     nviews, batch, pose_out, scale_out, poses44);
+  MAPA_CHECK_LAUNCH("mapa_pose_scale_finalize");
+  return 0;
+}
+
+extern "C" int mapa_dense_head_out(const void* hidden, int dtype, int n, int HW, const float* w6, const float* b6,
+                                   const float* pose_out, const float* scale, int batch, float* pts3d,
+                                   float* pts3d_cam, float* rays, float* depth, float* conf, float* logits,
+                                   uint8_t* mask, hipStream_t stream) {
+  MAPA_CHECK_ARG(hidden && w6 && b6 && pose_out && scale && pts3d && pts3d_cam && rays && depth && conf && logits &&
+                     mask && n > 0 && HW > 0 && batch > 0 && n % batch == 0,
+                 "mapa_dense_head_out: bad args");
+  const int64_t total = (int64_t)n * HW;
+  const dim3 g(grid_for(total)), b(TPB);
+  if (dtype == MAPA_BF16)
+    hipLaunchKernelGGL(dense_head_out_kernel<bf16_t>, g, b, 0, stream, (const bf16_t*)hidden, n, HW, w6, b6, pose_out,
+                       scale, batch, pts3d, pts3d_cam, rays, depth, conf, logits, mask);
+  else
+    hipLaunchKernelGGL(dense_head_out_kernel<float>, g, b, 0, stream, (const float*)hidden, n, HW, w6, b6, pose_out,
+                       scale, batch, pts3d, pts3d_cam, rays, depth, conf, logits, mask);
+  MAPA_CHECK_LAUNCH("mapa_dense_head_out");
+  return 0;
+}
+
+extern "C" int mapa_convert_rows(const float* src, int64_t lds, int rows, int cols, void* dst, int dst_dtype,
+                                 int64_t ldd, hipStream_t stream) {
+  MAPA_CHECK_ARG(src && dst && rows > 0 && cols > 0, "mapa_convert_rows: bad args");
+  hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(TPB), 0, stream, src, lds, rows,
+                     cols, dst, dst_dtype == MAPA_BF16 ? 1 : 0, ldd);
+  MAPA_CHECK_LAUNCH("mapa_convert_rows");
+  return 0;
+}
+
+extern "C" int mapa_fill_splitmix(float* out, int64_t n, uint64_t seed, float half, float mid, hipStream_t stream) {
+  MAPA_CHECK_ARG(out && n > 0, "mapa_fill_splitmix: bad args");
+  hipLaunchKernelGGL(fill_splitmix_kernel, dim3(grid_for(n)), dim3(TPB), 0, stream, out, n, seed, half, mid);
+  MAPA_CHECK_LAUNCH("mapa_fill_splitmix");
+  return 0;
+}

@@ -1,0 +1,301 @@
+// MFMA GEMM / implicit-GEMM convolution for gfx950.
+//
+//   C[M,N] = A[M,K] * W[N,K]^T   (both operands K-contiguous: nn.Linear / NHWC-conv weight layout)
+//
+// Replaces every nn.Linear / nn.Conv2d / nn.ConvTranspose2d call of the hot path:
+// DINOv2 patch-embed + qkv/proj/fc1/fc2 (vision_transformer.py, layers/block.py), AAT proj_embed/qkv/proj/
+// fc1/fc2 (transformer_blocks.py:65-212), the DPT 1x1/3x3/transposed convs (dpt.py:94-311, dpt_block.py:114-255),
+// the pose-head 1x1 convs (pose_head.py:18-48) and the dense-rep encoder convs (dense_rep_encoder.py).
+//
+// Design (MI355X-first):
+//  * 256 threads = 4 waves (2x2), block tile 128x128, wave tile 64x64 = 4x4 MFMA 16x16 tiles.
+//  * Operands staged HBM -> LDS with global_load_lds (16 B per lane, LDS image lane-linear); the 16-B chunk
+//    XOR swizzle (chunk ^ row&7) is applied on the per-lane SOURCE address so that the ds_read_b128 fragment
+//    reads are bank-conflict free.  Two LDS stages (double buffer), one barrier per K tile.
+//  * Out-of-range rows / K-tail chunks / conv halo taps read a 16-byte zero page instead of branching.
+//  * Two arithmetic variants behind one loader/epilogue: bf16 operands with v_mfma_f32_16x16x32_bf16
+//    (fast path), and fp32 operands with v_mfma_f32_16x16x4_f32 (exact-fp32 "precise" parity mode).
+//    Each LDS row is 128 B in both (64 bf16 or 32 fp32 of K), so the staging code is shared.
+//  * A operand modes: dense rows, or implicit 3x3 convolution (pad 1, stride 1/2) over an NHWC tensor.
+//  * Fused epilogue: out = resid1 + resid2 + gamma * act(acc + bias); optional fp32 output, low-precision
+//    output, ReLU'd low-precision output; row-major or pixel-shuffle (ConvTranspose k=s) addressing.
+//  * XCD-aware tile order (bijective remap: consecutive tiles share an XCD's L2).
+#include "mapa_common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, NTHREADS = 256;
+constexpr int ROW_BYTES = 128;                       // one LDS row of the K tile
+constexpr int TILE_BYTES = BM * ROW_BYTES;           // 16 KiB per operand per stage
+constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;        // 2 stages x (A, W)
+
+struct TraitsBF16 {
+  using T = bf16_t;
+  static constexpr int E = 8;    // elements per 16-B chunk
+  static constexpr int BK = 64;  // K elements per tile
+};
+struct TraitsF32 {
+  using T = float;
+  static constexpr int E = 4;
+  static constexpr int BK = 32;
+};
+
+struct GemmArgs {
+  const void* A;
+  int64_t lda;
+  const void* W;
+  int64_t ldw;
+  int M, N, K;
+  int a_mode;  // 0 dense, 1 conv3x3
+  int cv_C, cv_IH, cv_IW, cv_OH, cv_OW, cv_stride;
+  const float* bias;
+  int bias_mod;
+  const float* gamma;
+  int act;  // 0 none, 1 gelu(erf), 2 relu
+  const float* resid1;
+  const float* resid2;
+  float* out_f32;
+  void* out_lp;
+  void* out_lp_relu;
+  int64_t ldo;
+  int out_mode;  // 0 row-major, 1 pixel shuffle
+  int ps_s, ps_h, ps_w, ps_cout;
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  // blocks b, b+8, ... share an XCD (round-robin dispatch); give each XCD a contiguous tile range.
+  const int q = nblk / 8, r = nblk % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+template <typename Tr>
+__device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int wm, int wn, int lane, int kg,
+                                            f32x4 (&acc)[4][4]) {
+  const int g = lane >> 4, r16 = lane & 15;
+  const int chunk = kg * 4 + g;
+  if constexpr (sizeof(typename Tr::T) == 2) {
+    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+    b8 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ra = wm * 64 + i * 16 + r16;
+      a[i] = *reinterpret_cast<const b8*>(As + ra * ROW_BYTES + ((chunk ^ (ra & 7)) << 4));
+      const int rb = wn * 64 + i * 16 + r16;
+      b[i] = *reinterpret_cast<const b8*>(Bs + rb * ROW_BYTES + ((chunk ^ (rb & 7)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+  } else {
+    f32x4 a[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ra = wm * 64 + i * 16 + r16;
+      a[i] = *reinterpret_cast<const f32x4*>(As + ra * ROW_BYTES + ((chunk ^ (ra & 7)) << 4));
+      const int rb = wn * 64 + i * 16 + r16;
+      b[i] = *reinterpret_cast<const f32x4*>(Bs + rb * ROW_BYTES + ((chunk ^ (rb & 7)) << 4));
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i][s], b[j][s], acc[i][j], 0, 0, 0);
+  }
+}
+
+template <typename Tr>
+__global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
+  using T = typename Tr::T;
+  constexpr int E = Tr::E, BK = Tr::BK;
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int bm = (tile / ntn) * BM, bn = (tile % ntn) * BN;
+
+  // ---- per-thread staging geometry: 4 rows (one per load instruction), one fixed source chunk ----------
+  const int sc = (lane & 7) ^ (lane >> 3);  // source chunk (pre-swizzled)
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  const char* a_row[4];
+  int cv_base[4], cv_iy[4], cv_ix[4];
+  const char* w_row[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (i * 4 + wave) * 8 + (lane >> 3);
+    const int m = bm + r, n = bn + r;
+    w_row[i] = n < p.N ? reinterpret_cast<const char*>(p.W) + (int64_t)n * p.ldw * sizeof(T) : nullptr;
+    if (p.a_mode == 0) {
+      a_row[i] = m < p.M ? reinterpret_cast<const char*>(p.A) + (int64_t)m * p.lda * sizeof(T) : nullptr;
+    } else {
+      a_row[i] = nullptr;
+      if (m < p.M) {
+        const int hw = p.cv_OH * p.cv_OW;
+        const int img = m / hw, rem = m - img * hw;
+        const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
+        cv_base[i] = img * p.cv_IH * p.cv_IW;
+        cv_iy[i] = oy * p.cv_stride - 1;
+        cv_ix[i] = ox * p.cv_stride - 1;
+      } else {
+        cv_base[i] = -1;
+        cv_iy[i] = cv_ix[i] = 0;
+      }
+    }
+  }
+  // conv: (tap, ci) of this thread's chunk, advanced incrementally by BK per tile
+  int cv_tap = 0, cv_ci = sc * E;
+  if (p.a_mode == 1) {
+    while (cv_ci >= p.cv_C) { cv_ci -= p.cv_C; ++cv_tap; }
+  }
+
+  const int nk = (p.K + BK - 1) / BK;
+
+  auto stage = [&](int buf, int kt) {
+    char* As = lds + buf * 2 * TILE_BYTES;
+    char* Bs = As + TILE_BYTES;
+    const int kc = kt * BK + sc * E;
+    const bool kin = kc < p.K;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int base = ((i * 4 + wave) * 64) * 16;
+      const char* src;
+      if (p.a_mode == 0) {
+        src = (a_row[i] && kin) ? a_row[i] + (int64_t)kc * sizeof(T) : zero;
+      } else {
+        const int ky = cv_tap / 3, kx = cv_tap - ky * 3;
+        const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
+        const bool ok = kin && cv_base[i] >= 0 && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+        src = ok ? reinterpret_cast<const char*>(p.A) +
+                       ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + cv_ci) * sizeof(T)
+                 : zero;
+      }
+      __builtin_amdgcn_global_load_lds(src, As + base, 16, 0, 0);
+      const char* wsrc = (w_row[i] && kin) ? w_row[i] + (int64_t)kc * sizeof(T) : zero;
+      __builtin_amdgcn_global_load_lds(wsrc, Bs + base, 16, 0, 0);
+    }
+    if (p.a_mode == 1) {
+      cv_ci += BK;
+      while (cv_ci >= p.cv_C) { cv_ci -= p.cv_C; ++cv_tap; }
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
+    const char* As = lds + cur * 2 * TILE_BYTES;
+    const char* Bs = As + TILE_BYTES;
+    mfma_kgroup<Tr>(As, Bs, wm, wn, lane, 0, acc);
+    mfma_kgroup<Tr>(As, Bs, wm, wn, lane, 1, acc);
+    __syncthreads();
+  }
+
+  // ---- epilogue -----------------------------------------------------------------------------------------
+  const int g = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = bn + wn * 64 + j * 16 + c16;
+    if (n >= p.N) continue;
+    const float bv = p.bias ? p.bias[n % p.bias_mod] : 0.f;
+    const float gv = p.gamma ? p.gamma[n] : 1.f;
+    int64_t col_off = n;
+    int ps_ky = 0, ps_kx = 0;
+    if (p.out_mode == 1) {
+      const int co = n % p.ps_cout, t = n / p.ps_cout;
+      ps_ky = t / p.ps_s;
+      ps_kx = t - ps_ky * p.ps_s;
+      col_off = co;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = bm + wm * 64 + i * 16 + g * 4 + r;
+        if (m >= p.M) continue;
+        int64_t off;
+        if (p.out_mode == 0) {
+          off = (int64_t)m * p.ldo + col_off;
+        } else {
+          const int hw = p.ps_h * p.ps_w;
+          const int img = m / hw, rem = m - img * hw;
+          const int y = rem / p.ps_w, x = rem - y * p.ps_w;
+          const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
+          off = (((int64_t)img * H2 + y * p.ps_s + ps_ky) * W2 + x * p.ps_s + ps_kx) * p.ps_cout + col_off;
+        }
+        float v = acc[i][j][r] + bv;
+        if (p.act == 1) v = gelu_erf(v);
+        else if (p.act == 2) v = fmaxf(v, 0.f);
+        v *= gv;
+        if (p.resid1) v += p.resid1[off];
+        if (p.resid2) v += p.resid2[off];
+        if (p.out_f32) p.out_f32[off] = v;
+        if constexpr (sizeof(T) == 2) {
+          if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[off] = f32_to_bf16(v);
+          if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[off] = f32_to_bf16(fmaxf(v, 0.f));
+        } else {
+          if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[off] = v;
+          if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[off] = fmaxf(v, 0.f);
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
+  MAPA_CHECK_ARG(d != nullptr, "mapa_gemm: null descriptor");
+  MAPA_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "mapa_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
+  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32, "mapa_gemm: dtype must be bf16 or f32");
+  const int E = d->dtype == MAPA_BF16 ? 8 : 4;
+  MAPA_CHECK_ARG(d->K % E == 0, "mapa_gemm: K=%d must be a multiple of %d", d->K, E);
+  MAPA_CHECK_ARG(d->A && d->W, "mapa_gemm: null operand");
+  MAPA_CHECK_ARG(d->out_f32 || d->out_lp || d->out_lp_relu, "mapa_gemm: no output");
+  if (d->a_mode == MAPA_A_CONV3X3) {
+    MAPA_CHECK_ARG(d->conv_C % E == 0 && d->K == 9 * d->conv_C, "mapa_gemm: conv K=%d must be 9*C (C=%d, C%%%d==0)",
+                   d->K, d->conv_C, E);
+    MAPA_CHECK_ARG(d->conv_stride == 1 || d->conv_stride == 2, "mapa_gemm: conv stride must be 1 or 2");
+    const int oh = (d->conv_IH + 2 - 3) / d->conv_stride + 1, ow = (d->conv_IW + 2 - 3) / d->conv_stride + 1;
+    MAPA_CHECK_ARG(oh == d->conv_OH && ow == d->conv_OW, "mapa_gemm: conv out %dx%d != expected %dx%d",
+                   d->conv_OH, d->conv_OW, oh, ow);
+  } else {
+    MAPA_CHECK_ARG(d->a_mode == MAPA_A_DENSE, "mapa_gemm: bad a_mode");
+    MAPA_CHECK_ARG(d->lda >= d->K, "mapa_gemm: lda < K");
+  }
+  MAPA_CHECK_ARG(d->ldw >= d->K, "mapa_gemm: ldw < K");
+  if (d->out_mode == MAPA_OUT_PIXSHUF) {
+    MAPA_CHECK_ARG(d->ps_s > 0 && d->ps_cout > 0 && d->N == d->ps_s * d->ps_s * d->ps_cout &&
+                       d->M % (d->ps_h * d->ps_w) == 0,
+                   "mapa_gemm: bad pixel-shuffle geometry");
+  } else {
+    MAPA_CHECK_ARG(d->ldo >= d->N, "mapa_gemm: ldo < N");
+  }
+  GemmArgs a;
+  a.A = d->A; a.lda = d->lda; a.W = d->W; a.ldw = d->ldw;
+  a.M = d->M; a.N = d->N; a.K = d->K;
+  a.a_mode = d->a_mode;
+  a.cv_C = d->conv_C; a.cv_IH = d->conv_IH; a.cv_IW = d->conv_IW; a.cv_OH = d->conv_OH; a.cv_OW = d->conv_OW;
+  a.cv_stride = d->conv_stride;
+  a.bias = d->bias; a.bias_mod = d->bias_mod > 0 ? d->bias_mod : d->N;
+  a.gamma = d->gamma; a.act = d->act;
+  a.resid1 = d->resid1; a.resid2 = d->resid2;
+  a.out_f32 = d->out_f32; a.out_lp = d->out_lp; a.out_lp_relu = d->out_lp_relu; a.ldo = d->ldo;
+  a.out_mode = d->out_mode; a.ps_s = d->ps_s; a.ps_h = d->ps_h; a.ps_w = d->ps_w; a.ps_cout = d->ps_cout;
+  const int nblk = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
+  if (d->dtype == MAPA_BF16)
+    hipLaunchKernelGGL(gemm_kernel<TraitsBF16>, dim3(nblk), dim3(NTHREADS), 0, stream, a);
+  else
+    hipLaunchKernelGGL(gemm_kernel<TraitsF32>, dim3(nblk), dim3(NTHREADS), 0, stream, a);
+  MAPA_CHECK_LAUNCH("mapa_gemm");
+  return 0;
+}

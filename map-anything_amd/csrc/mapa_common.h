@@ -1,0 +1,73 @@
+// Shared helpers for the gfx950 (CDNA4) MapAnything kernels.  Wave = 64 lanes, LDS = 160 KiB per CU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mapa.h"
+
+#define MAPA_WAVE 64
+
+typedef uint16_t bf16_t;  // raw bf16 bits (row-major tensors in HBM)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------------------------------------
+// error reporting (thread-local last error, mapa_last_error())
+// ---------------------------------------------------------------------------------------------------------
+int mapa_set_error(const char* fmt, ...);
+
+#define MAPA_CHECK_ARG(cond, ...)                 \
+  do {                                            \
+    if (!(cond)) return mapa_set_error(__VA_ARGS__); \
+  } while (0)
+
+#define MAPA_CHECK_LAUNCH(what)                                                         \
+  do {                                                                                  \
+    hipError_t _e = hipGetLastError();                                                  \
+    if (_e != hipSuccess) return mapa_set_error("%s: %s", what, hipGetErrorString(_e)); \
+  } while (0)
+
+// ---------------------------------------------------------------------------------------------------------
+// bf16 <-> f32 (round-to-nearest-even, NaN kept quiet)
+// ---------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+__device__ __forceinline__ bf16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+template <typename T>
+__device__ __forceinline__ T ceil_div(T a, T b) {
+  return (a + b - 1) / b;
+}
+
+// Wave-level reductions (64 lanes).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// 16 zero bytes that out-of-range LDS-DMA lanes read (halo taps, M/N/K tails).
+static __device__ __attribute__((aligned(256))) uint32_t g_mapa_zero_page[64];  // one copy per code object TU

@@ -1,0 +1,253 @@
+// infer() post-processing on the device (the reference does this in CPU numpy at
+// ~230 ms/view): edge-aware output mask (inference.py:407-480 with geometry.py:1788-1853 points_to_normals,
+// :2200-2258 normals_edge, :2102-2145 depth_edge), pinhole intrinsics recovery (geometry.py:304-447) and
+// image de-normalisation (image.py:93-131).
+//
+// The mask is three 3x3-stencil passes over each view (NHWC, one thread per pixel):
+//   K1 normals + normal validity (points_to_normals with mask), K2 per-pixel max angle to the 3x3 window
+//   (NaN-propagating like numpy's .max, edge-replicated padding like np.pad mode="edge"), K3 3x3 nan-max
+//   pool of the angles (max_pool_2d uses np.nanmax with NaN padding) + depth-edge + final combine + zeroing
+//   of the dense geometry outputs.  Float operations follow numpy's order so equal inputs give equal bits.
+#include "mapa_common.h"
+
+namespace {
+
+__device__ __forceinline__ bool ldm(const uint8_t* m, int H, int W, int y, int x) {
+  return (y >= 0 && y < H && x >= 0 && x < W) ? m[y * W + x] != 0 : false;
+}
+
+__device__ __forceinline__ void ldp(const float* p, int H, int W, int y, int x, float v[3]) {
+  if (y >= 0 && y < H && x >= 0 && x < W) {
+    const float* q = p + ((int64_t)y * W + x) * 3;
+    v[0] = q[0]; v[1] = q[1]; v[2] = q[2];
+  } else {
+    v[0] = v[1] = v[2] = 0.f;
+  }
+}
+
+__device__ __forceinline__ void cross3(const float a[3], const float b[3], float c[3]) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ __forceinline__ float norm3(const float a[3]) {
+  return sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+}
+
+// K1: points_to_normals(point, mask) -> normal (H,W,3) and normal_mask (H,W)
+__global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __restrict__ mask, int n, int H, int W,
+                               float* __restrict__ nrm, uint8_t* __restrict__ nmask) {
+  const int64_t total = (int64_t)n * H * W;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int im = (int)(e / ((int64_t)H * W));
+    const int rem = (int)(e - (int64_t)im * H * W);
+    const int y = rem / W, x = rem - y * W;
+    const float* P = pts + (int64_t)im * H * W * 3;
+    const uint8_t* M = mask + (int64_t)im * H * W;
+    float c[3], u[3], l[3], d[3], r[3];
+    ldp(P, H, W, y, x, c);
+    ldp(P, H, W, y - 1, x, u);
+    ldp(P, H, W, y, x - 1, l);
+    ldp(P, H, W, y + 1, x, d);
+    ldp(P, H, W, y, x + 1, r);
+    for (int k = 0; k < 3; ++k) { u[k] -= c[k]; l[k] -= c[k]; d[k] -= c[k]; r[k] -= c[k]; }
+    float nn[4][3];
+    cross3(u, l, nn[0]);
+    cross3(l, d, nn[1]);
+    cross3(d, r, nn[2]);
+    cross3(r, u, nn[3]);
+    const bool mc = ldm(M, H, W, y, x);
+    const bool mu = ldm(M, H, W, y - 1, x), ml = ldm(M, H, W, y, x - 1);
+    const bool md = ldm(M, H, W, y + 1, x), mr = ldm(M, H, W, y, x + 1);
+    const bool valid[4] = {mu && ml && mc, ml && md && mc, md && mr && mc, mr && mu && mc};
+    float s[3] = {0.f, 0.f, 0.f};
+    bool any = false;
+    for (int i = 0; i < 4; ++i) {
+      const float inv = norm3(nn[i]) + 1e-12f;
+      if (valid[i]) {
+        for (int k = 0; k < 3; ++k) s[k] += nn[i][k] / inv;
+        any = true;
+      } else {
+        for (int k = 0; k < 3; ++k) s[k] += (nn[i][k] / inv) * 0.f;
+      }
+    }
+    const float ns = norm3(s) + 1e-12f;
+    float* o = nrm + e * 3;
+    for (int k = 0; k < 3; ++k) o[k] = any ? s[k] / ns : 0.f;
+    nmask[e] = any ? 1 : 0;
+  }
+}
+
+// K2: per-pixel window max of arccos(n_c . n_w) over the 3x3 window (edge padding), where(mask_w, angle, 0)
+__global__ void normal_angle_kernel(const float* __restrict__ nrm, const uint8_t* __restrict__ nmask, int n, int H,
+                                    int W, float* __restrict__ ang) {
+  const int64_t total = (int64_t)n * H * W;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int im = (int)(e / ((int64_t)H * W));
+    const int rem = (int)(e - (int64_t)im * H * W);
+    const int y = rem / W, x = rem - y * W;
+    const float* N = nrm + (int64_t)im * H * W * 3;
+    const uint8_t* Mk = nmask + (int64_t)im * H * W;
+    float c[3];
+    {
+      const float* q = N + ((int64_t)y * W + x) * 3;
+      const float nc = norm3(q) + 1e-12f;
+      for (int k = 0; k < 3; ++k) c[k] = q[k] / nc;
+    }
+    float best = -INFINITY;
+    bool nan = false;
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), W - 1);
+        const float* q = N + ((int64_t)yy * W + xx) * 3;
+        const float nq = norm3(q) + 1e-12f;
+        const float w0 = q[0] / nq, w1 = q[1] / nq, w2 = q[2] / nq;
+        float a = 0.f;
+        if (Mk[yy * W + xx]) a = acosf(c[0] * w0 + c[1] * w1 + c[2] * w2);
+        if (a != a) nan = true;
+        best = fmaxf(best, a);
+      }
+    ang[e] = nan ? __int_as_float(0x7fc00000) : best;
+  }
+}
+
+// K3: nan-max pool of the angles, depth edge, final mask, zero masked geometry
+__global__ void mask_combine_kernel(const float* __restrict__ ang, const float* __restrict__ depth_z, int64_t dz_stride,
+                                    const uint8_t* __restrict__ m_in, int n, int H, int W, float tol_rad,
+                                    float rtol, int use_edges, uint8_t* __restrict__ m_out) {
+  const int64_t total = (int64_t)n * H * W;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const bool mc = m_in[e] != 0;
+    bool keep = mc;
+    if (use_edges && mc) {
+      const int im = (int)(e / ((int64_t)H * W));
+      const int rem = (int)(e - (int64_t)im * H * W);
+      const int y = rem / W, x = rem - y * W;
+      const float* A = ang + (int64_t)im * H * W;
+      const uint8_t* M = m_in + (int64_t)im * H * W;
+      const float* D = depth_z + (int64_t)im * H * W * dz_stride;
+      float amax = -INFINITY, dmax = -INFINITY, ndmax = -INFINITY;
+      bool anyA = false;
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int yy = y + dy, xx = x + dx;
+          if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;  // NaN padding: ignored by nanmax
+          const float a = A[yy * W + xx];
+          if (a == a) { amax = fmaxf(amax, a); anyA = true; }
+          const int64_t k = (int64_t)yy * W + xx;
+          const float d = M[k] ? D[k * dz_stride] : -INFINITY;
+          const float nd = M[k] ? -D[k * dz_stride] : -INFINITY;
+          if (d == d) dmax = fmaxf(dmax, d);
+          if (nd == nd) ndmax = fmaxf(ndmax, nd);
+        }
+      const bool nedge = anyA && (amax > tol_rad);
+      const float diff = dmax + ndmax;
+      const float dc = D[(int64_t)rem * dz_stride];
+      const bool dedge = (diff / dc) > rtol;
+      keep = !(dedge && nedge);
+    }
+    m_out[e] = keep ? 1 : 0;
+  }
+}
+
+// recover_pinhole_intrinsics_from_ray_directions, regression branch (<= 1 MPix): one block per view,
+// normal equations of x = cx + fx * dx/dz (and y) over the strided sample grid, fp64 sums.
+__global__ void recover_intrinsics_kernel(const float* __restrict__ rays, int H, int W, float* __restrict__ K) {
+  const int im = blockIdx.x;
+  const int sh = max(1, H / 50), sw = max(1, W / 50);
+  const int nh = (H + sh - 1) / sh, nw = (W + sw - 1) / sw;
+  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // n, Sx_r, Sx_rr, Sx_b, Sx_rb, Sy_r, Sy_rr, Sy_b ... (+Sy_rb below)
+  double yb = 0.0;
+  const float* R = rays + (int64_t)im * H * W * 3;
+  for (int s = threadIdx.x; s < nh * nw; s += blockDim.x) {
+    const int y = (s / nw) * sh, x = (s % nw) * sw;
+    const float* r = R + ((int64_t)y * W + x) * 3;
+    const double rx = (double)(r[0] / r[2]), ry = (double)(r[1] / r[2]);
+    a[0] += 1.0;
+    a[1] += rx; a[2] += rx * rx; a[3] += x; a[4] += rx * x;
+    a[5] += ry; a[6] += ry * ry; a[7] += y; yb += ry * y;
+  }
+  __shared__ double red[9][256];
+  for (int i = 0; i < 8; ++i) red[i][threadIdx.x] = a[i];
+  red[8][threadIdx.x] = yb;
+  __syncthreads();
+  for (int st = blockDim.x / 2; st > 0; st >>= 1) {
+    if (threadIdx.x < st)
+      for (int i = 0; i < 9; ++i) red[i][threadIdx.x] += red[i][threadIdx.x + st];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double N = red[0][0];
+    const double detx = N * red[2][0] - red[1][0] * red[1][0];
+    const double cx = (red[2][0] * red[3][0] - red[1][0] * red[4][0]) / detx;
+    const double fx = (N * red[4][0] - red[1][0] * red[3][0]) / detx;
+    const double dety = N * red[6][0] - red[5][0] * red[5][0];
+    const double cy = (red[6][0] * red[7][0] - red[5][0] * red[8][0]) / dety;
+    const double fy = (N * red[8][0] - red[5][0] * red[7][0]) / dety;
+    float* k = K + im * 9;
+    k[0] = (float)fx; k[1] = 0.f; k[2] = (float)cx;
+    k[3] = 0.f; k[4] = (float)fy; k[5] = (float)cy;
+    k[6] = 0.f; k[7] = 0.f; k[8] = 1.f;
+  }
+}
+
+__global__ void denorm_image_kernel(const float* __restrict__ img, int n, int H, int W, const float* __restrict__ mean,
+                                    const float* __restrict__ stdv, float* __restrict__ out) {
+  const int64_t total = (int64_t)n * H * W;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int im = (int)(e / ((int64_t)H * W));
+    const int64_t p = e - (int64_t)im * H * W;
+    for (int c = 0; c < 3; ++c) {
+      const float v = img[((int64_t)im * 3 + c) * H * W + p] * stdv[c] + mean[c];
+      out[e * 3 + c] = fminf(fmaxf(v, 0.f), 1.f);
+    }
+  }
+}
+
+inline int grid_for(int64_t n) {
+  int64_t g = (n + 255) / 256;
+  return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+// mask_in: non-ambiguous (& confidence) mask u8 [n][H][W]; pts3d [n][H][W][3]; depth_z = pts3d_cam (z at +2,
+// stride 3); work = scratch of n*H*W*(3 floats + 1 float + 1 byte) bytes is carved from `work`.
+extern "C" int mapa_postprocess_mask(const float* pts3d, const float* pts3d_cam, const uint8_t* mask_in,
+                                     uint8_t* mask_out, int n, int H, int W, float normal_tol_deg, float depth_rtol,
+                                     int use_edges, void* work, hipStream_t stream) {
+  MAPA_CHECK_ARG(pts3d && pts3d_cam && mask_in && mask_out && n > 0 && H > 0 && W > 0,
+                 "mapa_postprocess_mask: bad args");
+  MAPA_CHECK_ARG(!use_edges || work, "mapa_postprocess_mask: edges need a work buffer");
+  const int64_t P = (int64_t)n * H * W;
+  float* nrm = reinterpret_cast<float*>(work);
+  float* ang = nrm + P * 3;
+  uint8_t* nmask = reinterpret_cast<uint8_t*>(ang + P);
+  if (use_edges) {
+    hipLaunchKernelGGL(normals_kernel, dim3(grid_for(P)), dim3(256), 0, stream, pts3d, mask_in, n, H, W, nrm, nmask);
+    hipLaunchKernelGGL(normal_angle_kernel, dim3(grid_for(P)), dim3(256), 0, stream, nrm, nmask, n, H, W, ang);
+  }
+  const float tol = normal_tol_deg * 0.017453292519943295f;
+  hipLaunchKernelGGL(mask_combine_kernel, dim3(grid_for(P)), dim3(256), 0, stream, ang, pts3d_cam + 2, (int64_t)3,
+                     mask_in, n, H, W, tol, depth_rtol, use_edges, mask_out);
+  MAPA_CHECK_LAUNCH("mapa_postprocess_mask");
+  return 0;
+}
+
+extern "C" int mapa_recover_intrinsics(const float* rays, int n, int H, int W, float* K, hipStream_t stream) {
+  MAPA_CHECK_ARG(rays && K && n > 0 && H > 0 && W > 0 && (int64_t)H * W <= 1000000,
+                 "mapa_recover_intrinsics: bad args (high-res geometric branch not implemented)");
+  hipLaunchKernelGGL(recover_intrinsics_kernel, dim3(n), dim3(256), 0, stream, rays, H, W, K);
+  MAPA_CHECK_LAUNCH("mapa_recover_intrinsics");
+  return 0;
+}
+
+extern "C" int mapa_denorm_image(const float* img, int n, int H, int W, const float* mean, const float* stdv,
+                                 float* out, hipStream_t stream) {
+  MAPA_CHECK_ARG(img && mean && stdv && out, "mapa_denorm_image: bad args");
+  hipLaunchKernelGGL(denorm_image_kernel, dim3(grid_for((int64_t)n * H * W)), dim3(256), 0, stream, img, n, H, W,
+                     mean, stdv, out);
+  MAPA_CHECK_LAUNCH("mapa_denorm_image");
+  return 0;
+}

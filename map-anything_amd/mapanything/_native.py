@@ -1,0 +1,293 @@
+"""ctypes binding of libmapa.so (the gfx950 HIP kernels behind include/mapa.h).
+
+There is no fallback: if the library or a gfx950 device is missing, `lib()` raises.  Tensors are passed as
+raw device pointers on torch's current HIP stream (torch is the allocator and stream owner, nothing more).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmapa.so")
+_lib = None
+
+F32, BF16 = 0, 1
+A_DENSE, A_CONV3X3 = 0, 1
+OUT_ROWMAJOR, OUT_PIXSHUF = 0, 1
+ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
+
+# Every extern "C" symbol declared in include/mapa.h (checked by tests/test_capi.py).
+EXPORTED = (
+    "mapa_last_error", "mapa_version", "mapa_device_check", "mapa_gemm", "mapa_attention", "mapa_layernorm",
+    "mapa_patchify", "mapa_assemble_tokens", "mapa_add_rowvec", "mapa_bilinear_ac", "mapa_mean_tokens",
+    "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
+    "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
+)
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int), ("M", ctypes.c_int), ("N", ctypes.c_int), ("K", ctypes.c_int),
+        ("A", ctypes.c_void_p), ("lda", ctypes.c_int64), ("W", ctypes.c_void_p), ("ldw", ctypes.c_int64),
+        ("a_mode", ctypes.c_int), ("conv_C", ctypes.c_int), ("conv_IH", ctypes.c_int), ("conv_IW", ctypes.c_int),
+        ("conv_OH", ctypes.c_int), ("conv_OW", ctypes.c_int), ("conv_stride", ctypes.c_int),
+        ("bias", ctypes.c_void_p), ("bias_mod", ctypes.c_int), ("gamma", ctypes.c_void_p), ("act", ctypes.c_int),
+        ("resid1", ctypes.c_void_p), ("resid2", ctypes.c_void_p), ("out_f32", ctypes.c_void_p),
+        ("out_lp", ctypes.c_void_p), ("out_lp_relu", ctypes.c_void_p), ("ldo", ctypes.c_int64),
+        ("out_mode", ctypes.c_int), ("ps_s", ctypes.c_int), ("ps_h", ctypes.c_int), ("ps_w", ctypes.c_int),
+        ("ps_cout", ctypes.c_int),
+    ]
+
+
+class AttnDesc(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int), ("batch", ctypes.c_int), ("heads", ctypes.c_int), ("seq_q", ctypes.c_int),
+        ("seq_kv", ctypes.c_int), ("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p),
+        ("o", ctypes.c_void_p), ("q_bstride", ctypes.c_int64), ("q_rstride", ctypes.c_int64),
+        ("k_bstride", ctypes.c_int64), ("k_rstride", ctypes.c_int64), ("v_bstride", ctypes.c_int64),
+        ("v_rstride", ctypes.c_int64), ("o_bstride", ctypes.c_int64), ("o_rstride", ctypes.c_int64),
+        ("lse", ctypes.c_void_p),
+    ]
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load_library(path: Optional[str] = None):
+    """dlopen libmapa.so and declare argtypes (no device needed)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or _LIB_PATH
+    if not os.path.exists(p):
+        raise NativeError(f"libmapa.so not found at {p}: build it with `make -C map-anything_amd/csrc` "
+                          f"(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(p)
+    vp, i, i64, f, u64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_uint64
+    L.mapa_last_error.restype = ctypes.c_char_p
+    L.mapa_version.restype = i
+    L.mapa_device_check.argtypes = [i]
+    L.mapa_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
+    L.mapa_attention.argtypes = [ctypes.POINTER(AttnDesc), vp]
+    L.mapa_layernorm.argtypes = [vp, i64, i, i, vp, vp, f, vp, vp, i, i64, i, i64, i, vp]
+    L.mapa_patchify.argtypes = [vp, i, i, i, vp, i, i, vp]
+    L.mapa_assemble_tokens.argtypes = [vp, vp, vp, i, i, i, vp, vp]
+    L.mapa_add_rowvec.argtypes = [vp, i64, i, i, i, vp, vp]
+    L.mapa_bilinear_ac.argtypes = [vp, i, i, i, i, i, i, i, i, i, vp, i, vp]
+    L.mapa_mean_tokens.argtypes = [vp, i, i, i, vp, vp]
+    L.mapa_linear_small.argtypes = [vp, i, i, vp, vp, i, i, vp, vp]
+    L.mapa_pose_scale_finalize.argtypes = [vp, vp, i, i, vp, vp, vp, vp]
+    L.mapa_dense_head_out.argtypes = [vp, i, i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mapa_convert_rows.argtypes = [vp, i64, i, i, vp, i, i64, vp]
+    L.mapa_fill_splitmix.argtypes = [vp, i64, u64, f, f, vp]
+    L.mapa_postprocess_mask.argtypes = [vp, vp, vp, vp, i, i, i, f, f, i, vp, vp]
+    L.mapa_recover_intrinsics.argtypes = [vp, i, i, i, vp, vp]
+    L.mapa_denorm_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
+    _lib = L
+    return L
+
+
+def lib():
+    """The loaded library, after checking that a gfx950 device is present (raises otherwise)."""
+    L = load_library()
+    if not getattr(L, "_device_ok", False):
+        if not torch.cuda.is_available():
+            raise NativeError("no HIP device visible: the MapAnything MI355X engine has no CPU path")
+        dev = torch.cuda.current_device()
+        if L.mapa_device_check(dev) != 1:
+            raise NativeError(L.mapa_last_error().decode())
+        L._device_ok = True
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        raise NativeError(f"{what}: {_lib.mapa_last_error().decode()}")
+
+
+def ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dt_code(dtype: torch.dtype) -> int:
+    if dtype == torch.bfloat16:
+        return BF16
+    if dtype == torch.float32:
+        return F32
+    raise NativeError(f"unsupported dtype {dtype}")
+
+
+# --------------------------------------------------------------------------------------- kernel timing
+# Optional per-launch HIP-event timing (bench.py's roofline numbers): events are recorded on the stream the
+# kernel is launched on, around the launch, and only read after the timed region.
+_timing = None
+
+
+def timing_start():
+    global _timing
+    _timing = {}
+
+
+def timing_stop():
+    """-> {kind: {"ms": total, "count": launches, "flops": total algorithmic flops}} (synchronises)."""
+    global _timing
+    t, _timing = _timing, None
+    if not t:
+        return {}
+    torch.cuda.synchronize()
+    out = {}
+    for kind, recs in t.items():
+        ms = sum(a.elapsed_time(b) for a, b, _ in recs)
+        out[kind] = {"ms": ms, "count": len(recs), "flops": float(sum(f for _, _, f in recs))}
+    return out
+
+
+def _tic():
+    if _timing is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _toc(tok, kind, flops=0.0):
+    if tok is None:
+        return
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    _timing.setdefault(kind, []).append((tok, e, flops))
+
+
+# ------------------------------------------------------------------------------------------------ wrappers
+def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_NONE, resid1=None, resid2=None,
+         out_f32=None, out_lp=None, out_lp_relu=None, ldo=None, conv=None, pixshuf=None):
+    """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout)."""
+    d = GemmDesc()
+    d.dtype = dt_code(A.dtype)
+    assert W.dtype == A.dtype
+    d.M, d.N, d.K = M, N, K
+    d.A = A.data_ptr()
+    d.lda = lda if lda is not None else K
+    d.W = W.data_ptr()
+    d.ldw = W.stride(0)
+    if conv is not None:
+        d.a_mode = A_CONV3X3
+        d.conv_C, d.conv_IH, d.conv_IW, d.conv_OH, d.conv_OW, d.conv_stride = conv
+        d.lda = K
+    d.bias = None if bias is None else bias.data_ptr()
+    d.bias_mod = bias_mod
+    d.gamma = None if gamma is None else gamma.data_ptr()
+    d.act = act
+    d.resid1 = None if resid1 is None else resid1.data_ptr()
+    d.resid2 = None if resid2 is None else resid2.data_ptr()
+    d.out_f32 = None if out_f32 is None else out_f32.data_ptr()
+    d.out_lp = None if out_lp is None else out_lp.data_ptr()
+    d.out_lp_relu = None if out_lp_relu is None else out_lp_relu.data_ptr()
+    d.ldo = ldo if ldo is not None else N
+    if pixshuf is not None:
+        d.out_mode = OUT_PIXSHUF
+        d.ps_s, d.ps_h, d.ps_w, d.ps_cout = pixshuf
+    tok = _tic()
+    check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
+    _toc(tok, "conv3x3" if conv is not None else "gemm", 2.0 * M * N * K)
+
+
+def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, k_bstride, k_rstride,
+              v_bstride, v_rstride, o_bstride, o_rstride, lse=None):
+    """q/k/v/o are tensors whose data_ptr is the (b=0, h=0, i=0, d=0) element."""
+    d = AttnDesc()
+    d.dtype = dt_code(q.dtype)
+    d.batch, d.heads, d.seq_q, d.seq_kv = batch, heads, seq_q, seq_kv
+    d.q, d.k, d.v, d.o = q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr()
+    d.q_bstride, d.q_rstride = q_bstride, q_rstride
+    d.k_bstride, d.k_rstride = k_bstride, k_rstride
+    d.v_bstride, d.v_rstride = v_bstride, v_rstride
+    d.o_bstride, d.o_rstride = o_bstride, o_rstride
+    d.lse = None if lse is None else lse.data_ptr()
+    tok = _tic()
+    check(lib().mapa_attention(ctypes.byref(d), stream()), "mapa_attention")
+    _toc(tok, "attention", 4.0 * batch * heads * seq_q * seq_kv * 64)
+
+
+def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, ldy=None, group=0,
+              group_stride=0, row_off=0):
+    lp_dtype = BF16 if (y_lp is not None and y_lp.dtype == torch.bfloat16) else F32
+    tok = _tic()
+    check(lib().mapa_layernorm(ptr(x), ldx if ldx is not None else dim, rows, dim, ptr(w), ptr(b), eps, ptr(y_f32),
+                               ptr(y_lp), lp_dtype, ldy if ldy is not None else dim, group, group_stride, row_off,
+                               stream()), "mapa_layernorm")
+    _toc(tok, "layernorm")
+
+
+def patchify(img, n, H, W, out, kpad):
+    check(lib().mapa_patchify(ptr(img), n, H, W, ptr(out), dt_code(out.dtype), kpad, stream()), "mapa_patchify")
+
+
+def assemble_tokens(patch, cls, pos, n, T, dim, x):
+    check(lib().mapa_assemble_tokens(ptr(patch), ptr(cls), ptr(pos), n, T, dim, ptr(x), stream()),
+          "mapa_assemble_tokens")
+
+
+def add_rowvec(x, ldx, r0, r1, dim, vec):
+    check(lib().mapa_add_rowvec(ptr(x), ldx, r0, r1, dim, ptr(vec), stream()), "mapa_add_rowvec")
+
+
+def bilinear_ac(inp, n, IH, IW, C, OHf, OWf, OH, OW, out):
+    check(lib().mapa_bilinear_ac(ptr(inp), dt_code(inp.dtype), n, IH, IW, C, OHf, OWf, OH, OW, ptr(out),
+                                 dt_code(out.dtype), stream()), "mapa_bilinear_ac")
+
+
+def mean_tokens(x, n, T, C, y):
+    check(lib().mapa_mean_tokens(ptr(x), n, T, C, ptr(y), stream()), "mapa_mean_tokens")
+
+
+def linear_small(x, M, K, w, b, N, act, y):
+    check(lib().mapa_linear_small(ptr(x), M, K, ptr(w), ptr(b), N, act, ptr(y), stream()), "mapa_linear_small")
+
+
+def pose_scale_finalize(pose_raw, scale_raw, nviews, batch, pose_out, scale_out, poses44=None):
+    check(lib().mapa_pose_scale_finalize(ptr(pose_raw), ptr(scale_raw), nviews, batch, ptr(pose_out),
+                                         ptr(scale_out), ptr(poses44), stream()), "mapa_pose_scale_finalize")
+
+
+def dense_head_out(hidden, n, HW, w6, b6, pose_out, scale, batch, pts3d, pts3d_cam, rays, depth, conf, logits,
+                   mask):
+    check(lib().mapa_dense_head_out(ptr(hidden), dt_code(hidden.dtype), n, HW, ptr(w6), ptr(b6), ptr(pose_out),
+                                    ptr(scale), batch, ptr(pts3d), ptr(pts3d_cam), ptr(rays), ptr(depth), ptr(conf),
+                                    ptr(logits), ptr(mask), stream()), "mapa_dense_head_out")
+
+
+def convert_rows(src, lds, rows, cols, dst, ldd):
+    check(lib().mapa_convert_rows(ptr(src), lds, rows, cols, ptr(dst), dt_code(dst.dtype), ldd, stream()),
+          "mapa_convert_rows")
+
+
+def fill_splitmix(out, seed, half, mid):
+    check(lib().mapa_fill_splitmix(ptr(out), out.numel(), seed, half, mid, stream()), "mapa_fill_splitmix")
+
+
+def postprocess_mask(pts3d, pts3d_cam, mask_in, mask_out, n, H, W, normal_tol_deg, depth_rtol, use_edges, work):
+    check(lib().mapa_postprocess_mask(ptr(pts3d), ptr(pts3d_cam), ptr(mask_in), ptr(mask_out), n, H, W,
+                                      normal_tol_deg, depth_rtol, int(use_edges), ptr(work), stream()),
+          "mapa_postprocess_mask")
+
+
+def recover_intrinsics(rays, n, H, W, K):
+    check(lib().mapa_recover_intrinsics(ptr(rays), n, H, W, ptr(K), stream()), "mapa_recover_intrinsics")
+
+
+def denorm_image(img, n, H, W, mean, std, out):
+    check(lib().mapa_denorm_image(ptr(img), n, H, W, ptr(mean), ptr(std), ptr(out), stream()), "mapa_denorm_image")

@@ -1,0 +1,469 @@
+"""Device executor of the MapAnything feed-forward path on MI355X (every op is a libmapa.so HIP kernel).
+
+`MapaEngine.run(imgs)` is the GPU replacement of `MapAnything.forward` (model.py:1657-2152) for the released
+config (image-only inputs, pred head "dpt+pose", scene rep "raydirs+depth+pose+confidence+mask").  Tensors are
+torch allocations on the current device; torch does nothing else.  Layout in HBM:
+
+  tokens            row-major [rows][C]: encoder rows = view*(T+1) + t (cls first), AAT rows = view*T + t with the
+                    scale token as the last row; residual streams fp32, GEMM operands bf16 (fp32 in precise mode)
+  qkv               one [rows][3*C] buffer straight from the qkv GEMM; attention reads q/k/v in place
+  DPT feature maps  NHWC [view][y][x][C]; 3x3 convs are implicit GEMMs over these, ConvTranspose k=s writes the
+                    pixel-shuffled map directly from the GEMM epilogue
+  outputs           NHWC fp32 [view][H][W][c] (the reference's (B,H,W,c) per view, view-major)
+
+Precision modes: "bf16" (bf16 MFMA operands, fp32 accumulate / LayerNorm / softmax / residuals — the reference's
+own autocast recipe, model.py:2287-2302) and "fp32" (exact-fp32 MFMA everywhere, for parity against the fp32
+reference to ~1e-5).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ... import _native as nat
+
+ENC_DIM, ENC_HEADS, PATCH, KPAD = 1024, 16, 14, 640
+AAT_DIM, AAT_HEADS = 768, 12
+POSE_DIM = 784
+LN_EPS = 1e-6
+DINOV2_MEAN = (0.485, 0.456, 0.406)
+DINOV2_STD = (0.229, 0.224, 0.225)
+
+
+def _np(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().float().cpu().numpy()
+    return np.asarray(x, dtype=np.float32)
+
+
+class PackedWeights:
+    """Canonical state dict -> device buffers in kernel layout (done once at load)."""
+
+    def __init__(self, sd: Dict[str, object], device, lp_dtype: torch.dtype):
+        self.device = device
+        self.lp = lp_dtype
+        self.sd = sd
+        g = self._get
+        dev = device
+
+        def f32(name):
+            return torch.from_numpy(np.ascontiguousarray(_np(g(name)))).to(dev)
+
+        def lin(name):
+            w = _np(g(f"{name}.weight"))
+            return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev, self.lp)
+
+        def conv3(name):  # [co][ci][3][3] -> [co][ky][kx][ci]
+            w = _np(g(f"{name}.weight"))
+            return torch.from_numpy(np.ascontiguousarray(w.transpose(0, 2, 3, 1).reshape(w.shape[0], -1))).to(
+                dev, self.lp)
+
+        def convT(name):  # [ci][co][k][k] -> [(ky*k+kx)*co + c][ci]
+            w = _np(g(f"{name}.weight"))
+            ci, co, k, _ = w.shape
+            return torch.from_numpy(np.ascontiguousarray(w.transpose(2, 3, 1, 0).reshape(k * k * co, ci))).to(
+                dev, self.lp)
+
+        self.f32, self.lin, self.conv3 = f32, lin, conv3
+        # DINOv2
+        pe = _np(g("encoder.model.patch_embed.proj.weight")).reshape(ENC_DIM, 588)
+        pe = np.concatenate([pe, np.zeros((ENC_DIM, KPAD - 588), np.float32)], 1)
+        self.pe_w = torch.from_numpy(np.ascontiguousarray(pe)).to(dev, self.lp)
+        self.pe_b = f32("encoder.model.patch_embed.proj.bias")
+        self.cls = f32("encoder.model.cls_token").reshape(-1)
+        self.pos_embed_param = torch.from_numpy(_np(g("encoder.model.pos_embed")))
+        self.pos_cache: Dict[tuple, torch.Tensor] = {}
+        self.enc = []
+        for b in range(24):
+            p = f"encoder.model.blocks.{b}"
+            self.enc.append(dict(
+                n1w=f32(f"{p}.norm1.weight"), n1b=f32(f"{p}.norm1.bias"),
+                qkv=lin(f"{p}.attn.qkv"), qkv_b=f32(f"{p}.attn.qkv.bias"),
+                proj=lin(f"{p}.attn.proj"), proj_b=f32(f"{p}.attn.proj.bias"), ls1=f32(f"{p}.ls1.gamma"),
+                n2w=f32(f"{p}.norm2.weight"), n2b=f32(f"{p}.norm2.bias"),
+                fc1=lin(f"{p}.mlp.fc1"), fc1_b=f32(f"{p}.mlp.fc1.bias"),
+                fc2=lin(f"{p}.mlp.fc2"), fc2_b=f32(f"{p}.mlp.fc2.bias"), ls2=f32(f"{p}.ls2.gamma")))
+        self.enc_nw, self.enc_nb = f32("encoder.model.norm.weight"), f32("encoder.model.norm.bias")
+        self.fus_w, self.fus_b = f32("fusion_norm_layer.weight"), f32("fusion_norm_layer.bias")
+        self.scale_token = f32("scale_token")
+        # AAT
+        self.pe_proj = lin("info_sharing.proj_embed")
+        self.pe_proj_b = f32("info_sharing.proj_embed.bias")
+        self.view_pe = f32("info_sharing.view_pos_table").reshape(-1)[:AAT_DIM].contiguous()
+        self.aat = []
+        for b in range(24):
+            p = f"info_sharing.self_attention_blocks.{b}"
+            self.aat.append(dict(
+                n1w=f32(f"{p}.norm1.weight"), n1b=f32(f"{p}.norm1.bias"),
+                qkv=lin(f"{p}.attn.qkv"), qkv_b=f32(f"{p}.attn.qkv.bias"),
+                proj=lin(f"{p}.attn.proj"), proj_b=f32(f"{p}.attn.proj.bias"),
+                n2w=f32(f"{p}.norm2.weight"), n2b=f32(f"{p}.norm2.bias"),
+                fc1=lin(f"{p}.mlp.fc1"), fc1_b=f32(f"{p}.mlp.fc1.bias"),
+                fc2=lin(f"{p}.mlp.fc2"), fc2_b=f32(f"{p}.mlp.fc2.bias")))
+        self.aat_nw, self.aat_nb = f32("info_sharing.norm.weight"), f32("info_sharing.norm.bias")
+        # DPT feature head
+        h = "dpt_feature_head"
+        ip = f"{h}.input_process"
+        self.ip = [
+            dict(w=lin(f"{ip}.0.0.0"), b=f32(f"{ip}.0.0.0.bias"), ct=convT(f"{ip}.0.0.1"), ct_b=f32(f"{ip}.0.0.1.bias")),
+            dict(w=lin(f"{ip}.1.0.0"), b=f32(f"{ip}.1.0.0.bias"), ct=convT(f"{ip}.1.0.1"), ct_b=f32(f"{ip}.1.0.1.bias")),
+            dict(w=lin(f"{ip}.2.0.0"), b=f32(f"{ip}.2.0.0.bias")),
+            dict(w=lin(f"{ip}.3.0.0"), b=f32(f"{ip}.3.0.0.bias"), c3=conv3(f"{ip}.3.0.1"), c3_b=f32(f"{ip}.3.0.1.bias")),
+        ]
+        self.layer_rn = [conv3(f"{h}.scratch.layer{i + 1}_rn") for i in range(4)]
+        self.refine = {}
+        for r in (1, 2, 3, 4):
+            n = f"{h}.scratch.refinenet{r}"
+            d = dict(out=lin(f"{n}.out_conv"), out_b=f32(f"{n}.out_conv.bias"))
+            units = ("resConfUnit2",) if r == 4 else ("resConfUnit1", "resConfUnit2")
+            for u in units:
+                d[u] = dict(c1=conv3(f"{n}.{u}.conv1"), b1=f32(f"{n}.{u}.conv1.bias"),
+                            c2=conv3(f"{n}.{u}.conv2"), b2=f32(f"{n}.{u}.conv2.bias"))
+            self.refine[r] = d
+        self.reg_c1, self.reg_b1 = conv3("dpt_regressor_head.conv1"), f32("dpt_regressor_head.conv1.bias")
+        self.reg_c2, self.reg_b2 = conv3("dpt_regressor_head.conv2.0"), f32("dpt_regressor_head.conv2.0.bias")
+        self.reg_w6 = f32("dpt_regressor_head.conv2.2.weight").reshape(6, 128).contiguous()
+        self.reg_b6 = f32("dpt_regressor_head.conv2.2.bias")
+        # pose head (1x1 convs as GEMMs, MLP tail fp32)
+        self.pose_proj, self.pose_proj_b = lin("pose_head.proj"), f32("pose_head.proj.bias")
+        self.pose_res = []
+        for b in range(2):
+            n = f"pose_head.res_conv.{b}"
+            self.pose_res.append([(lin(f"{n}.res_conv{c}"), f32(f"{n}.res_conv{c}.bias")) for c in (1, 2, 3)])
+        self.pose_mlp = [(f32(f"pose_head.more_mlps.{i}.weight"), f32(f"pose_head.more_mlps.{i}.bias")) for i in (0, 2)]
+        # fc_t (3) and fc_rot (4) share their input: one 7-row linear gives cat([t, rot]) (pose_head.py:155-158)
+        self.pose_tr = (torch.cat([f32("pose_head.fc_t.weight"), f32("pose_head.fc_rot.weight")], 0).contiguous(),
+                        torch.cat([f32("pose_head.fc_t.bias"), f32("pose_head.fc_rot.bias")], 0).contiguous())
+        self.scale_mlp = [(f32(f"scale_head.{n}.weight"), f32(f"scale_head.{n}.bias"))
+                          for n in ("proj", "mlp.0.0", "mlp.1.0", "output_proj")]
+        self.norm_mean = torch.tensor(DINOV2_MEAN, device=dev)
+        self.norm_std = torch.tensor(DINOV2_STD, device=dev)
+        self.sd = None  # host copy no longer needed
+
+    def _get(self, name):
+        return self.sd[name]
+
+    def pos_embed(self, H: int, W: int) -> torch.Tensor:
+        """DINOv2 positional embedding for an (H, W) input (vision_transformer.py:208-242).  At 518x518 it is the
+        parameter itself; otherwise the reference's bicubic resample of the 37x37 grid, computed once per
+        resolution on the host and cached on the device (a parameter transform, not per-inference work)."""
+        key = (H, W)
+        if key not in self.pos_cache:
+            pe = self.pos_embed_param.float()
+            h0, w0 = H // PATCH, W // PATCH
+            N = pe.shape[1] - 1
+            if h0 * w0 == N and H == W:
+                out = pe[0]
+            else:
+                M = int(math.sqrt(N))
+                patch = F.interpolate(pe[:, 1:].reshape(1, M, M, ENC_DIM).permute(0, 3, 1, 2), mode="bicubic",
+                                      antialias=False, scale_factor=(float(h0 + 0.1) / M, float(w0 + 0.1) / M))
+                patch = patch.permute(0, 2, 3, 1).reshape(-1, ENC_DIM)
+                out = torch.cat([pe[0, :1], patch], 0)
+            self.pos_cache[key] = out.contiguous().to(self.device)
+        return self.pos_cache[key]
+
+
+class MapaEngine:
+    def __init__(self, sd: Dict[str, object], device=None, precision: str = "bf16"):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision}")
+        nat.lib()  # fail loudly without the HIP library / a gfx950 device
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.precision = precision
+        self.lp = torch.bfloat16 if precision == "bf16" else torch.float32
+        with torch.cuda.device(self.device):
+            self.w = PackedWeights(sd, self.device, self.lp)
+
+    # ---------------------------------------------------------------------------------------- profiling
+    def enable_kernel_timing(self):
+        nat.timing_start()
+
+    def collect_kernel_timing(self):
+        return nat.timing_stop()
+
+    # ----------------------------------------------------------------------------------------------- utils
+    def _empty(self, *shape, dtype=None):
+        return torch.empty(shape, dtype=dtype or self.lp, device=self.device)
+
+    def _ln(self, x, rows, dim, w, b, *, y_f32=None, y_lp=None, group=0, gstride=0, off=0, ldx=None):
+        nat.layernorm(x, rows, dim, w, b, eps=LN_EPS, ldx=ldx, y_f32=y_f32, y_lp=y_lp, group=group,
+                      group_stride=gstride, row_off=off)
+
+    def _conv3(self, x, n, IH, IW, C, wmat, Cout, stride=1, **epi):
+        OH, OW = (IH + 2 - 3) // stride + 1, (IW + 2 - 3) // stride + 1
+        nat.gemm(x, wmat, n * OH * OW, Cout, 9 * C, conv=(C, IH, IW, OH, OW, stride), **epi)
+        return OH, OW
+
+    # ------------------------------------------------------------------------------------ transformer block
+    def _block(self, x, xn, qkv, ao, hbuf, rows, dim, heads, p, *, attn_batch, attn_seq, gamma=True):
+        lp = self.lp
+        self._ln(x, rows, dim, p["n1w"], p["n1b"], y_lp=xn)
+        nat.gemm(xn, p["qkv"], rows, 3 * dim, dim, bias=p["qkv_b"], out_lp=qkv)
+        rs = 3 * dim
+        nat.attention(qkv, qkv[:, dim:], qkv[:, 2 * dim:], ao, batch=attn_batch, heads=heads, seq_q=attn_seq,
+                      seq_kv=attn_seq, q_bstride=attn_seq * rs, q_rstride=rs, k_bstride=attn_seq * rs, k_rstride=rs,
+                      v_bstride=attn_seq * rs, v_rstride=rs, o_bstride=attn_seq * dim, o_rstride=dim)
+        nat.gemm(ao, p["proj"], rows, dim, dim, bias=p["proj_b"], gamma=p.get("ls1") if gamma else None,
+                 resid1=x, out_f32=x)
+        self._ln(x, rows, dim, p["n2w"], p["n2b"], y_lp=xn)
+        nat.gemm(xn, p["fc1"], rows, 4 * dim, dim, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
+        nat.gemm(hbuf, p["fc2"], rows, dim, 4 * dim, bias=p["fc2_b"], gamma=p.get("ls2") if gamma else None,
+                 resid1=x, out_f32=x)
+
+    # ------------------------------------------------------------------------------------------- encoder
+    def encode(self, imgs, taps=None):
+        """DINOv2 ViT-L/14 + final norm + fusion LayerNorm (image-only).  Returns fused_lp [VB*T+1][1024]
+        (last row reserved for the scale token) and fused f32 if taps is not None."""
+        w = self.w
+        VB, _, H, W = imgs.shape
+        hp, wp = H // PATCH, W // PATCH
+        T = hp * wp
+        R = VB * (T + 1)
+        patches = self._empty(VB * T, KPAD)
+        nat.patchify(imgs, VB, H, W, patches, KPAD)
+        pe_out = self._empty(VB * T, ENC_DIM, dtype=torch.float32)
+        nat.gemm(patches, w.pe_w, VB * T, ENC_DIM, KPAD, bias=w.pe_b, out_f32=pe_out)
+        x = self._empty(R, ENC_DIM, dtype=torch.float32)
+        nat.assemble_tokens(pe_out, w.cls, w.pos_embed(H, W), VB, T, ENC_DIM, x)
+        del pe_out, patches
+        xn, qkv, ao = self._empty(R, ENC_DIM), self._empty(R, 3 * ENC_DIM), self._empty(R, ENC_DIM)
+        hbuf = self._empty(R, 4 * ENC_DIM)
+        for p in w.enc:
+            self._block(x, xn, qkv, ao, hbuf, R, ENC_DIM, ENC_HEADS, p, attn_batch=VB, attn_seq=T + 1)
+        del xn, qkv, ao, hbuf
+        enc = self._empty(VB * T, ENC_DIM, dtype=torch.float32)
+        self._ln(x, VB * T, ENC_DIM, w.enc_nw, w.enc_nb, y_f32=enc, group=T, gstride=T + 1, off=1)
+        del x
+        fused_lp = self._empty(VB * T + 1, ENC_DIM)
+        fused_f32 = self._empty(VB * T, ENC_DIM, dtype=torch.float32) if taps is not None else None
+        self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
+        nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
+        if taps is not None:
+            taps["encoder"] = enc
+            taps["fused"] = fused_f32
+        return fused_lp, (hp, wp)
+
+    # ----------------------------------------------------------------------------------------------- AAT
+    def aat(self, fused_lp, VB, T, taps=None):
+        """alternating_attention_transformer.py:530-771 (IFR [11, 17]).  Returns l11, l17, final (lp, VB*T rows)
+        and the final scale-token feature (f32, 768)."""
+        w = self.w
+        L = VB * T + 1
+        y = self._empty(L, AAT_DIM, dtype=torch.float32)
+        nat.gemm(fused_lp, w.pe_proj, L, AAT_DIM, ENC_DIM, bias=w.pe_proj_b, out_f32=y)
+        nat.add_rowvec(y, AAT_DIM, 0, T, AAT_DIM, w.view_pe)
+        yn, qkv, ao = self._empty(L, AAT_DIM), self._empty(L, 3 * AAT_DIM), self._empty(L, AAT_DIM)
+        hbuf = self._empty(L, 4 * AAT_DIM)
+        inter = {}
+        for d, p in enumerate(w.aat):
+            if d % 2 == 0:   # global attention over every view + the scale token
+                self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False)
+            else:            # frame attention inside each view; the scale token bypasses the block
+                self._block(y, yn, qkv, ao, hbuf, VB * T, AAT_DIM, AAT_HEADS, p, attn_batch=VB, attn_seq=T,
+                            gamma=False)
+            if d in (11, 17):
+                t_lp = self._empty(VB * T, AAT_DIM)
+                t_f = self._empty(VB * T, AAT_DIM, dtype=torch.float32) if taps is not None else None
+                self._ln(y, VB * T, AAT_DIM, w.aat_nw, w.aat_nb, y_lp=t_lp, y_f32=t_f)
+                inter[d] = t_lp
+                if taps is not None:
+                    taps[f"aat_l{d}"] = t_f
+        del yn, qkv, ao, hbuf
+        fin_lp = self._empty(L, AAT_DIM)
+        fin_f32 = self._empty(L, AAT_DIM, dtype=torch.float32)
+        self._ln(y, L, AAT_DIM, w.aat_nw, w.aat_nb, y_lp=fin_lp, y_f32=fin_f32)
+        if taps is not None:
+            taps["aat_final"] = fin_f32[:VB * T]
+            taps["scale_token"] = fin_f32[VB * T]
+        return inter[11], inter[17], fin_lp, fin_f32[VB * T:]
+
+    # ----------------------------------------------------------------------------------------------- DPT
+    def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None):
+        """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Returns the ReLU'd 128-ch hidden map at HxW."""
+        w = self.w
+        n, T = VB, hp * wp
+        lp = self.lp
+        # input_process 0: 1x1 1024->96, ConvT k4 s4, layer1_rn 3x3 96->256 (no bias)
+        a = self._empty(n * T, 96)
+        nat.gemm(fused_lp, w.ip[0]["w"], n * T, 96, ENC_DIM, bias=w.ip[0]["b"], out_lp=a)
+        up0 = self._empty(n, 4 * hp, 4 * wp, 96)
+        nat.gemm(a, w.ip[0]["ct"], n * T, 16 * 96, 96, bias=w.ip[0]["ct_b"], bias_mod=96, out_lp=up0,
+                 pixshuf=(4, hp, wp, 96))
+        h0, w0 = 4 * hp, 4 * wp
+        L0f = self._empty(n * h0 * w0, 256, dtype=torch.float32)
+        L0r = self._empty(n * h0 * w0, 256)
+        self._conv3(up0, n, h0, w0, 96, w.layer_rn[0], 256, out_f32=L0f, out_lp_relu=L0r)
+        del a, up0
+        # input_process 1: 1x1 768->192, ConvT k2 s2, layer2_rn
+        a = self._empty(n * T, 192)
+        nat.gemm(l11, w.ip[1]["w"], n * T, 192, AAT_DIM, bias=w.ip[1]["b"], out_lp=a)
+        up1 = self._empty(n, 2 * hp, 2 * wp, 192)
+        nat.gemm(a, w.ip[1]["ct"], n * T, 4 * 192, 192, bias=w.ip[1]["ct_b"], bias_mod=192, out_lp=up1,
+                 pixshuf=(2, hp, wp, 192))
+        h1, w1 = 2 * hp, 2 * wp
+        L1f = self._empty(n * h1 * w1, 256, dtype=torch.float32)
+        L1r = self._empty(n * h1 * w1, 256)
+        self._conv3(up1, n, h1, w1, 192, w.layer_rn[1], 256, out_f32=L1f, out_lp_relu=L1r)
+        del a, up1
+        # input_process 2: 1x1 768->384, layer3_rn
+        a = self._empty(n * T, 384)
+        nat.gemm(l17, w.ip[2]["w"], n * T, 384, AAT_DIM, bias=w.ip[2]["b"], out_lp=a)
+        L2f = self._empty(n * T, 256, dtype=torch.float32)
+        L2r = self._empty(n * T, 256)
+        self._conv3(a, n, hp, wp, 384, w.layer_rn[2], 256, out_f32=L2f, out_lp_relu=L2r)
+        del a
+        # input_process 3: 1x1 768->768, 3x3 s2 768->768, layer4_rn
+        a = self._empty(n * T, 768)
+        nat.gemm(fin_lp, w.ip[3]["w"], n * T, 768, AAT_DIM, bias=w.ip[3]["b"], out_lp=a)
+        h3, w3 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1
+        b3 = self._empty(n * h3 * w3, 768)
+        self._conv3(a, n, hp, wp, 768, w.ip[3]["c3"], 768, stride=2, bias=w.ip[3]["c3_b"], out_lp=b3)
+        L3f = self._empty(n * h3 * w3, 256, dtype=torch.float32)
+        L3r = self._empty(n * h3 * w3, 256)
+        self._conv3(b3, n, h3, w3, 768, w.layer_rn[3], 256, out_f32=L3f, out_lp_relu=L3r)
+        del a, b3
+        # refinenet4 (RCU2 only) -> x2 -> crop to (hp, wp) -> out_conv
+        o = self._fusion_single(n, h3, w3, 4, L3f, L3r)
+        path = self._upsample_outconv(o, n, h3, w3, 4, crop=(hp, wp))
+        # refinenet3/2/1
+        o = self._fusion_two(n, hp, wp, 3, path, L2f, L2r)
+        path = self._upsample_outconv(o, n, hp, wp, 3)
+        o = self._fusion_two(n, h1, w1, 2, path, L1f, L1r)
+        path = self._upsample_outconv(o, n, h1, w1, 2)
+        o = self._fusion_two(n, h0, w0, 1, path, L0f, L0r)
+        feat_lp = self._upsample_outconv(o, n, h0, w0, 1, lowp=True, taps=taps)
+        hf, wf = 2 * h0, 2 * w0
+        # regressor: conv3x3 256->128 @8x, bilinear(ac) -> HxW, conv3x3 128->128 + ReLU
+        r1 = self._empty(n * hf * wf, 128)
+        self._conv3(feat_lp, n, hf, wf, 256, w.reg_c1, 128, bias=w.reg_b1, out_lp=r1)
+        del feat_lp
+        r1u = self._empty(n * H * W, 128)
+        nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u)
+        del r1
+        hid = self._empty(n * H * W, 128)
+        self._conv3(r1u, n, H, W, 128, w.reg_c2, 128, bias=w.reg_b2, act=nat.ACT_RELU, out_lp=hid)
+        return hid
+
+    def _fusion_single(self, n, h, w_, r, x_f, x_r):
+        u = self.w.refine[r]["resConfUnit2"]
+        c1 = self._empty(n * h * w_, 256)
+        self._conv3(x_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, out_lp=c1)
+        o = self._empty(n * h * w_, 256)
+        self._conv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=x_f, out_lp=o)
+        return o
+
+    def _fusion_two(self, n, h, w_, r, path_f, skip_f, skip_r):
+        d = self.w.refine[r]
+        u = d["resConfUnit1"]
+        c1 = self._empty(n * h * w_, 256)
+        self._conv3(skip_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, out_lp=c1)
+        s_f = self._empty(n * h * w_, 256, dtype=torch.float32)
+        s_r = self._empty(n * h * w_, 256)
+        self._conv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=skip_f, resid2=path_f, out_f32=s_f,
+                    out_lp_relu=s_r)
+        u = d["resConfUnit2"]
+        self._conv3(s_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, out_lp=c1)
+        o = self._empty(n * h * w_, 256)
+        self._conv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=s_f, out_lp=o)
+        return o
+
+    def _upsample_outconv(self, o, n, h, w_, r, crop=None, lowp=False, taps=None):
+        """bilinear x2 (align_corners) [+ crop] then the 1x1 out_conv (dpt_block.py:241-254, dpt.py:213)."""
+        d = self.w.refine[r]
+        Hf, Wf = 2 * h, 2 * w_
+        oh, ow = crop if crop is not None else (Hf, Wf)
+        up = self._empty(n * oh * ow, 256)
+        nat.bilinear_ac(o, n, h, w_, 256, Hf, Wf, oh, ow, up)
+        if lowp:
+            out = self._empty(n * oh * ow, 256)
+            f = self._empty(n * oh * ow, 256, dtype=torch.float32) if taps is not None else None
+            nat.gemm(up, d["out"], n * oh * ow, 256, 256, bias=d["out_b"], out_lp=out, out_f32=f)
+            if taps is not None:
+                taps["dpt_feature"] = f.view(n, oh, ow, 256)
+            return out
+        out = self._empty(n * oh * ow, 256, dtype=torch.float32)
+        nat.gemm(up, d["out"], n * oh * ow, 256, 256, bias=d["out_b"], out_f32=out)
+        return out
+
+    # ------------------------------------------------------------------------------------- pose / scale
+    def pose(self, fin_lp, VB, T, taps=None):
+        """PoseHead (pose_head.py:50-159) -> raw (VB, 7)."""
+        w = self.w
+        M = VB * T
+        pf = self._empty(M, POSE_DIM, dtype=torch.float32)
+        pl = self._empty(M, POSE_DIM)
+        nat.gemm(fin_lp, w.pose_proj, M, POSE_DIM, AAT_DIM, bias=w.pose_proj_b, out_f32=pf, out_lp=pl)
+        t1, t2 = self._empty(M, POSE_DIM), self._empty(M, POSE_DIM)
+        for blk in w.pose_res:
+            (w1, b1), (w2, b2), (w3, b3) = blk
+            nat.gemm(pl, w1, M, POSE_DIM, POSE_DIM, bias=b1, act=nat.ACT_RELU, out_lp=t1)
+            nat.gemm(t1, w2, M, POSE_DIM, POSE_DIM, bias=b2, act=nat.ACT_RELU, out_lp=t2)
+            nat.gemm(t2, w3, M, POSE_DIM, POSE_DIM, bias=b3, act=nat.ACT_RELU, resid1=pf, out_f32=pf, out_lp=pl)
+        pooled = self._empty(VB, POSE_DIM, dtype=torch.float32)
+        nat.mean_tokens(pf, VB, T, POSE_DIM, pooled)
+        h1 = self._empty(VB, POSE_DIM, dtype=torch.float32)
+        h2 = self._empty(VB, POSE_DIM, dtype=torch.float32)
+        nat.linear_small(pooled, VB, POSE_DIM, w.pose_mlp[0][0], w.pose_mlp[0][1], POSE_DIM, nat.ACT_RELU, h1)
+        nat.linear_small(h1, VB, POSE_DIM, w.pose_mlp[1][0], w.pose_mlp[1][1], POSE_DIM, nat.ACT_RELU, h2)
+        raw = self._empty(VB, 7, dtype=torch.float32)
+        nat.linear_small(h2, VB, POSE_DIM, w.pose_tr[0], w.pose_tr[1], 7, nat.ACT_NONE, raw)
+        if taps is not None:
+            taps["pose_raw"] = raw
+        return raw
+
+    def scale(self, tok, taps=None):
+        """MLPHead (mlp_head.py:13-92) on the scale-token feature -> raw (1,)."""
+        w = self.w.scale_mlp
+        a = self._empty(1, 196, dtype=torch.float32)
+        b = self._empty(1, 196, dtype=torch.float32)
+        nat.linear_small(tok, 1, AAT_DIM, w[0][0], w[0][1], 196, nat.ACT_NONE, a)
+        nat.linear_small(a, 1, 196, w[1][0], w[1][1], 196, nat.ACT_RELU, b)
+        nat.linear_small(b, 1, 196, w[2][0], w[2][1], 196, nat.ACT_RELU, a)
+        raw = self._empty(1, dtype=torch.float32)
+        nat.linear_small(a, 1, 196, w[3][0], w[3][1], 1, nat.ACT_NONE, raw)
+        if taps is not None:
+            taps["scale_raw"] = raw
+        return raw
+
+    # ----------------------------------------------------------------------------------------------- run
+    @torch.no_grad()
+    def run(self, imgs: torch.Tensor, taps: Optional[dict] = None) -> Dict[str, torch.Tensor]:
+        """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
+        per-pixel / per-view outputs of MapAnything.forward, view-major."""
+        if imgs.dim() != 4 or imgs.shape[1] != 3:
+            raise AssertionError("images must be (V, 3, H, W)")
+        VB, _, H, W = imgs.shape
+        if H % PATCH or W % PATCH:
+            raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
+        imgs = imgs.to(self.device, torch.float32).contiguous()
+        with torch.cuda.device(self.device):
+            fused_lp, (hp, wp) = self.encode(imgs, taps)
+            T = hp * wp
+            l11, l17, fin_lp, tok = self.aat(fused_lp, VB, T, taps)
+            pose_raw = self.pose(fin_lp, VB, T, taps)
+            scale_raw = self.scale(tok, taps)
+            pose_out = self._empty(VB, 19, dtype=torch.float32)
+            scale = self._empty(1, dtype=torch.float32)
+            poses44 = self._empty(VB, 4, 4, dtype=torch.float32)
+            nat.pose_scale_finalize(pose_raw, scale_raw, VB, 1, pose_out, scale, poses44)
+            hid = self.dpt(fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps)
+            f = torch.float32
+            out = dict(
+                pts3d=self._empty(VB, H, W, 3, dtype=f), pts3d_cam=self._empty(VB, H, W, 3, dtype=f),
+                ray_directions=self._empty(VB, H, W, 3, dtype=f), depth_along_ray=self._empty(VB, H, W, 1, dtype=f),
+                conf=self._empty(VB, H, W, dtype=f), non_ambiguous_mask_logits=self._empty(VB, H, W, dtype=f),
+                non_ambiguous_mask=self._empty(VB, H, W, dtype=torch.uint8))
+            nat.dense_head_out(hid, VB, H * W, self.w.reg_w6, self.w.reg_b6, pose_out, scale, 1, out["pts3d"],
+                               out["pts3d_cam"], out["ray_directions"], out["depth_along_ray"], out["conf"],
+                               out["non_ambiguous_mask_logits"], out["non_ambiguous_mask"])
+            out["cam_trans"] = pose_out[:, 0:3]
+            out["cam_quats"] = pose_out[:, 3:7]
+            out["metric_scaling_factor"] = scale.view(1, 1)
+            out["camera_poses"] = poses44
+        return out

@@ -1,0 +1,284 @@
+"""`MapAnything` — drop-in for `mapanything.models.MapAnything` (reference model.py:96-2355) on MI355X.
+
+Same constructor config (configs/inference.json schema), same `from_pretrained(local_dir)`, `infer(views, ...)`
+keyword arguments and output dictionaries (model.py:2206-2355), same `forward(views)` raw outputs
+(model.py:1657-2152), same `ValueError`s for invalid views (inference.py:146-217).  Every arithmetic step runs in
+the gfx950 HIP library (`MapaEngine`); this class is host glue: validation, device placement, bookkeeping.
+
+Differences that are by design:
+  * weights come from a LOCAL directory (config.json + model.safetensors) or the synthetic named-PRNG
+    checkpoint; there is no hub download (no network on this box),
+  * `precision="bf16"` (default) mirrors `infer(use_amp=True, amp_dtype="bf16")`; `use_amp=False` (or
+    precision="fp32") runs the exact-fp32 MFMA path,
+  * multi-view batches are processed B = 1 per view (the reference's configs all use B = 1).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import warnings
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ... import _native as nat
+from ...utils.inference import (postprocess_outputs, preprocess_input_views_for_inference,
+                                validate_input_views_for_inference)
+from .spec import aliases, canonical_spec
+
+SUPPORTED = dict(
+    encoder="dinov2", size="large", info_sharing="alternating_attention", return_type="intermediate_features",
+    pred_head="dpt+pose", adaptor="raydirs+depth+pose+confidence+mask",
+)
+
+
+def _check_config(encoder_config, info_sharing_config, pred_head_config):
+    problems = []
+    if encoder_config.get("encoder_str") != "dinov2" or encoder_config.get("size", "large") != "large":
+        problems.append(f"encoder {encoder_config.get('encoder_str')}/{encoder_config.get('size')}")
+    if encoder_config.get("with_registers", False):
+        problems.append("dinov2 with registers")
+    if info_sharing_config.get("model_type") != SUPPORTED["info_sharing"]:
+        problems.append(f"info_sharing {info_sharing_config.get('model_type')}")
+    if info_sharing_config.get("model_return_type") != SUPPORTED["return_type"]:
+        problems.append(f"return type {info_sharing_config.get('model_return_type')}")
+    args = info_sharing_config.get("module_args", {})
+    if list(args.get("indices", [11, 17])) != [11, 17] or args.get("depth", 24) != 24:
+        problems.append("AAT depth/indices")
+    if pred_head_config.get("type") != SUPPORTED["pred_head"]:
+        problems.append(f"pred head {pred_head_config.get('type')}")
+    if pred_head_config.get("adaptor_type") != SUPPORTED["adaptor"]:
+        problems.append(f"adaptor {pred_head_config.get('adaptor_type')}")
+    if problems:
+        raise ValueError("MapAnything (MI355X engine) implements the released architecture "
+                         f"(configs/inference.json); unsupported: {', '.join(problems)}")
+
+
+class MapAnything:
+    """Modular MapAnything model (reference model.py:96) — MI355X-native inference engine."""
+
+    def __init__(self, name: str, encoder_config: Dict, info_sharing_config: Dict, pred_head_config: Dict,
+                 geometric_input_config: Dict, fusion_norm_layer=None, pretrained_checkpoint_path: str = None,
+                 load_specific_pretrained_submodules: bool = False, specific_pretrained_submodules: list = None,
+                 torch_hub_force_reload: bool = False, precision: str = "bf16"):
+        _check_config(encoder_config, info_sharing_config, pred_head_config)
+        self.name = name
+        self.encoder_config = encoder_config
+        self.info_sharing_config = info_sharing_config
+        self.pred_head_config = pred_head_config
+        self.geometric_input_config = dict(geometric_input_config)
+        self.class_init_args = dict(name=name, encoder_config=encoder_config, info_sharing_config=info_sharing_config,
+                                    pred_head_config=pred_head_config, geometric_input_config=geometric_input_config,
+                                    pretrained_checkpoint_path=pretrained_checkpoint_path,
+                                    load_specific_pretrained_submodules=load_specific_pretrained_submodules,
+                                    specific_pretrained_submodules=specific_pretrained_submodules,
+                                    torch_hub_force_reload=torch_hub_force_reload)
+        self.precision = precision
+        self._sd: Optional[Dict[str, np.ndarray]] = None
+        self._engines: Dict[tuple, Any] = {}
+        self._device = torch.device("cpu")
+        self.training = False
+        if pretrained_checkpoint_path is not None:
+            self.load_checkpoint(pretrained_checkpoint_path)
+
+    # ------------------------------------------------------------------------------------------ weights
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path: str, local_files_only: bool = True, **kwargs):
+        """Local-directory version of PyTorchModelHubMixin.from_pretrained (config.json + model.safetensors)."""
+        path = pretrained_model_name_or_path
+        if not os.path.isdir(path):
+            raise FileNotFoundError(
+                f"{path!r} is not a local directory: this engine loads config.json + model.safetensors from disk "
+                "(no hub access); download the checkpoint elsewhere and pass its directory")
+        with open(os.path.join(path, "config.json")) as f:
+            cfg = json.loads(_strip_comments(f.read()))
+        cfg.update({k: v for k, v in kwargs.items() if k in ("precision",)})
+        model = cls(**cfg)
+        st = os.path.join(path, "model.safetensors")
+        if os.path.exists(st):
+            from safetensors.numpy import load_file
+            model.load_state_dict(load_file(st))
+        else:
+            raise FileNotFoundError(f"{st} not found")
+        return model
+
+    @classmethod
+    def from_config_file(cls, path: str, **kwargs):
+        with open(path) as f:
+            cfg = json.loads(_strip_comments(f.read()))
+        cfg.update(kwargs)
+        return cls(**cfg)
+
+    def load_checkpoint(self, path: str):
+        """`_load_pretrained_weights` (model.py:636-666): a torch checkpoint with a 'model' state dict."""
+        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+        self.load_state_dict(ckpt["model"] if "model" in ckpt else ckpt)
+
+    def load_state_dict(self, state_dict: Dict[str, Any], strict: bool = True):
+        canon = dict(canonical_spec())
+        al = aliases()
+        sd: Dict[str, np.ndarray] = {}
+        for k, v in state_dict.items():
+            arr = v.detach().float().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v, np.float32)
+            key = al.get(k, k)
+            if key not in canon:
+                if strict:
+                    raise KeyError(f"unexpected key in state_dict: {k}")
+                continue
+            if tuple(arr.shape) != tuple(canon[key]):
+                raise ValueError(f"shape mismatch for {k}: {arr.shape} vs {canon[key]}")
+            sd[key] = arr
+        missing = [k for k in canon if k not in sd]
+        if missing and strict:
+            raise KeyError(f"missing keys in state_dict: {missing[:5]} ... ({len(missing)})")
+        self._sd = sd
+        self._engines.clear()
+        return self
+
+    def load_synthetic_weights(self):
+        """Named-PRNG synthetic checkpoint (mapanything/utils/synthetic.py) — bench/tests only."""
+        from ...utils.synthetic import synthetic_state_dict
+
+        self._sd = synthetic_state_dict(canonical_spec())
+        self._engines.clear()
+        return self
+
+    # ------------------------------------------------------------------------------------ nn.Module-ish
+    def to(self, device=None, *args, **kwargs):
+        if device is not None:
+            self._device = torch.device(device)
+            if self._device.type == "cuda" and self._device.index is None:
+                self._device = torch.device("cuda", torch.cuda.current_device())
+        return self
+
+    def cuda(self, device=None):
+        return self.to(torch.device("cuda", device) if device is not None else "cuda")
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise NotImplementedError("training is out of scope for the MI355X inference engine")
+        return self.eval()
+
+    @property
+    def device(self) -> torch.device:
+        return self._device
+
+    def engine(self, precision: Optional[str] = None):
+        prec = precision or self.precision
+        if self._sd is None:
+            raise RuntimeError("no weights loaded: use from_pretrained(local_dir), load_state_dict() or "
+                               "load_synthetic_weights()")
+        if self._device.type != "cuda":
+            raise nat.NativeError("MapAnything (MI355X engine) runs on a gfx950 device only: call .to('cuda')")
+        key = (str(self._device), prec)
+        if key not in self._engines:
+            from .engine import MapaEngine
+            self._engines[key] = MapaEngine(self._sd, self._device, prec)
+        return self._engines[key]
+
+    def enable_view_sharding(self, group):
+        """Shard the views over the ranks of `group` (one process per GPU); global-attention K/V all-gathered."""
+        self._shard_group = group
+        self._engines.clear()
+        return self
+
+    # ------------------------------------------------------------------------------------------ forward
+    def _check_image_only(self, views):
+        for i, v in enumerate(views):
+            extra = [k for k in ("ray_directions_cam", "depth_along_ray", "camera_pose_quats") if k in v]
+            if extra:
+                raise NotImplementedError(
+                    f"view {i}: geometric inputs {extra} are not yet supported by the MI355X engine "
+                    "(image-only inference; pass ignore_*_inputs=True to drop them)")
+            if "img" not in v:
+                raise NotImplementedError(f"view {i}: views without images are not supported yet")
+            if v["img"].shape[0] != 1:
+                raise NotImplementedError("batch size per view must be 1")
+
+    def forward(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False,
+                precision: Optional[str] = None) -> List[Dict[str, torch.Tensor]]:
+        """Raw per-view outputs of model.py:1657-2152 (pts3d, pts3d_cam, ray_directions, depth_along_ray,
+        cam_trans, cam_quats, metric_scaling_factor, conf, non_ambiguous_mask, non_ambiguous_mask_logits)."""
+        self._check_image_only(views)
+        dnt = views[0].get("data_norm_type", ["dinov2"])
+        if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
+            raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
+        imgs = torch.cat([v["img"] for v in views], 0).to(self._device, torch.float32)
+        raw = self.engine(precision).run(imgs)
+        return split_views(raw, len(views), with_post=False)
+
+    @torch.inference_mode()
+    def infer(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False, use_amp: bool = True,
+              amp_dtype: str = "bf16", apply_mask: bool = True, mask_edges: bool = True,
+              edge_normal_threshold: float = 5.0, edge_depth_threshold: float = 0.03,
+              apply_confidence_mask: bool = False, confidence_percentile: float = 10,
+              ignore_calibration_inputs: bool = False, ignore_depth_inputs: bool = False,
+              ignore_pose_inputs: bool = False, ignore_depth_scale_inputs: bool = False,
+              ignore_pose_scale_inputs: bool = False) -> List[Dict[str, torch.Tensor]]:
+        """model.py:2206-2355."""
+        if use_amp and amp_dtype in ("bf16", "fp16"):
+            if amp_dtype == "fp16":
+                warnings.warn("fp16 autocast is served by the bf16 MFMA path on MI355X")
+            precision = "bf16"
+        else:
+            precision = "fp32"
+        validated = validate_input_views_for_inference(views)
+        for v in validated:
+            for k in list(v.keys()):
+                if k in ("instance", "idx", "true_shape", "data_norm_type"):
+                    continue
+                if isinstance(v[k], torch.Tensor):
+                    v[k] = v[k].to(self._device, non_blocking=True)
+        processed = preprocess_input_views_for_inference(validated)
+        for v in processed:
+            if ignore_calibration_inputs:
+                v.pop("ray_directions_cam", None)
+            if ignore_depth_inputs:
+                v.pop("depth_along_ray", None)
+            if ignore_pose_inputs:
+                v.pop("camera_pose_quats", None)
+                v.pop("camera_pose_trans", None)
+        self._check_image_only(processed)
+        imgs = torch.cat([v["img"] for v in processed], 0).to(self._device, torch.float32)
+        eng = self.engine(precision)
+        raw = eng.run(imgs)
+        post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
+                                   mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
+                                   edge_depth_threshold=edge_depth_threshold,
+                                   apply_confidence_mask=apply_confidence_mask,
+                                   confidence_percentile=confidence_percentile)
+        return split_views(post, len(views), with_post=True)
+
+    __call__ = forward
+
+
+def split_views(out: Dict[str, torch.Tensor], V: int, with_post: bool) -> List[Dict[str, torch.Tensor]]:
+    """Batched view-major outputs -> the reference's list of per-view dicts (B = 1), as views (no copies)."""
+    res = []
+    for i in range(V):
+        d = {}
+        for k, t in out.items():
+            if k == "metric_scaling_factor":
+                d[k] = t
+            elif k == "non_ambiguous_mask":
+                d[k] = t[i:i + 1].bool()
+            elif k == "mask":
+                d[k] = t[i:i + 1].bool().unsqueeze(-1)
+            else:
+                d[k] = t[i:i + 1]
+        if "pts3d_cam" in d:
+            d["depth_z"] = d["pts3d_cam"][..., 2:3]
+        res.append(d)
+    return res
+
+
+def _strip_comments(txt: str) -> str:
+    import re
+
+    return re.sub(r"//[^\n]*", "", txt)

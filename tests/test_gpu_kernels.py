@@ -1,0 +1,200 @@
+"""Per-kernel parity of libmapa.so against PyTorch fp32 references of the same op (needs an MI355X)."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def nat():
+    from mapanything import _native
+
+    _native.lib()
+    return _native
+
+
+def _rand(*shape, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).cuda()
+
+
+# ------------------------------------------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 200, 264), (129, 130, 72), (1370, 1024, 1024),
+                                   (37, 784, 784), (5, 7, 16)])
+def test_gemm_plain(nat, dtype, M, N, K):
+    A = _rand(M, K, seed=1).to(dtype)
+    W = _rand(N, K, scale=K ** -0.5, seed=2).to(dtype)
+    b = _rand(N, seed=3)
+    out = torch.empty(M, N, device="cuda")
+    nat.gemm(A, W, M, N, K, bias=b, out_f32=out)
+    ref = A.float() @ W.float().t() + b
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    assert rel_l2(out.cpu(), ref.cpu()) < tol
+
+
+def test_gemm_epilogues(nat):
+    M, N, K = 333, 384, 192
+    A = _rand(M, K, seed=4).to(torch.bfloat16)
+    W = _rand(N, K, scale=K ** -0.5, seed=5).to(torch.bfloat16)
+    b, g = _rand(N, seed=6), _rand(N, seed=7)
+    r1, r2 = _rand(M, N, seed=8), _rand(M, N, seed=9)
+    acc = A.float() @ W.float().t() + b
+    # gelu -> bf16
+    o = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=o)
+    assert rel_l2(o.float().cpu(), F.gelu(acc).cpu()) < 5e-3
+    # resid1 + resid2 + gamma * relu(acc) -> f32 + relu copy
+    of = torch.empty(M, N, device="cuda")
+    orl = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    nat.gemm(A, W, M, N, K, bias=b, gamma=g, act=nat.ACT_RELU, resid1=r1, resid2=r2, out_f32=of, out_lp_relu=orl)
+    ref = r1 + r2 + g * torch.relu(acc)
+    assert rel_l2(of.cpu(), ref.cpu()) < 1e-4
+    assert rel_l2(orl.float().cpu(), torch.relu(ref).cpu()) < 5e-3
+    # in-place residual (x = x + gamma * acc), the transformer-block pattern
+    x = r1.clone()
+    nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=x, out_f32=x)
+    assert rel_l2(x.cpu(), (r1 + g * acc).cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("n,H,W,C,Co,stride", [(2, 19, 19, 96, 256, 1), (1, 37, 37, 768, 768, 2),
+                                              (3, 16, 20, 128, 128, 1), (1, 8, 8, 256, 6, 1)])
+def test_conv3x3_implicit_gemm(nat, dtype, n, H, W, C, Co, stride):
+    x = _rand(n, C, H, W, seed=10)
+    w = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=11)
+    b = _rand(Co, seed=12)
+    xl, wl = x.to(dtype), w.to(dtype)
+    ref = F.conv2d(xl.float(), wl.float(), b, stride=stride, padding=1)
+    OH, OW = ref.shape[-2:]
+    x_nhwc = xl.permute(0, 2, 3, 1).contiguous()
+    wmat = wl.permute(0, 2, 3, 1).reshape(Co, -1).contiguous()
+    out = torch.empty(n * OH * OW, Co, device="cuda")
+    nat.gemm(x_nhwc, wmat, n * OH * OW, Co, 9 * C, bias=b, out_f32=out, conv=(C, H, W, OH, OW, stride))
+    got = out.view(n, OH, OW, Co).permute(0, 3, 1, 2)
+    tol = 1e-5 if dtype == torch.float32 else 1e-4
+    assert rel_l2(got.cpu(), ref.cpu()) < tol
+
+
+@pytest.mark.parametrize("s,ci,co", [(4, 96, 96), (2, 192, 192)])
+def test_convtranspose_pixel_shuffle(nat, s, ci, co):
+    n, h, w = 2, 7, 9
+    x = _rand(n, ci, h, w, seed=13).to(torch.bfloat16)
+    wt = _rand(ci, co, s, s, scale=ci ** -0.5, seed=14).to(torch.bfloat16)
+    b = _rand(co, seed=15)
+    ref = F.conv_transpose2d(x.float(), wt.float(), b, stride=s)
+    A = x.permute(0, 2, 3, 1).reshape(n * h * w, ci).contiguous()
+    Wm = wt.permute(2, 3, 1, 0).reshape(s * s * co, ci).contiguous()
+    out = torch.empty(n, h * s, w * s, co, device="cuda")
+    nat.gemm(A, Wm, n * h * w, s * s * co, ci, bias=b, bias_mod=co, out_f32=out, pixshuf=(s, h, w, co))
+    assert rel_l2(out.permute(0, 3, 1, 2).cpu(), ref.cpu()) < 1e-4
+
+
+# ------------------------------------------------------------------------------------------------- attention
+def _sdpa_ref(q, k, v):
+    return F.scaled_dot_product_attention(q.float(), k.float(), v.float())
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 8e-3), (torch.float32, 2e-5)])
+@pytest.mark.parametrize("B,Hh,S", [(2, 16, 1370), (3, 12, 1369), (1, 12, 200), (1, 2, 64), (1, 1, 1), (2, 3, 65)])
+def test_attention_packed_qkv(nat, dtype, tol, B, Hh, S):
+    C = Hh * 64
+    qkv = _rand(B * S, 3 * C, seed=16).to(dtype)
+    o = torch.empty(B * S, C, device="cuda", dtype=dtype)
+    rs = 3 * C
+    nat.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B, heads=Hh, seq_q=S, seq_kv=S, q_bstride=S * rs,
+                  q_rstride=rs, k_bstride=S * rs, k_rstride=rs, v_bstride=S * rs, v_rstride=rs, o_bstride=S * C,
+                  o_rstride=C)
+    t = qkv.view(B, S, 3, Hh, 64).permute(2, 0, 3, 1, 4)
+    ref = _sdpa_ref(t[0], t[1], t[2]).transpose(1, 2).reshape(B * S, C)
+    assert rel_l2(o.float().cpu(), ref.cpu()) < tol
+
+
+def test_attention_cross_lengths_and_lse(nat):
+    """Q rows attend to a different-length K/V set (the sharded global layer) + LSE output."""
+    Hh, Sq, Skv = 12, 300, 1111
+    q = _rand(Sq, Hh * 64, seed=17).to(torch.bfloat16)
+    kv = _rand(Skv, 2 * Hh * 64, seed=18).to(torch.bfloat16)
+    o = torch.empty(Sq, Hh * 64, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(1, Hh, Sq, device="cuda")
+    C = Hh * 64
+    nat.attention(q, kv, kv[:, C:], o, batch=1, heads=Hh, seq_q=Sq, seq_kv=Skv, q_bstride=0, q_rstride=C,
+                  k_bstride=0, k_rstride=2 * C, v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C, lse=lse)
+    qh = q.view(Sq, Hh, 64).transpose(0, 1)[None]
+    kh = kv[:, :C].reshape(Skv, Hh, 64).transpose(0, 1)[None]
+    vh = kv[:, C:].reshape(Skv, Hh, 64).transpose(0, 1)[None]
+    ref = _sdpa_ref(qh, kh, vh)[0].transpose(0, 1).reshape(Sq, C)
+    assert rel_l2(o.float().cpu(), ref.cpu()) < 8e-3
+    s = (qh.float() @ kh.float().transpose(-1, -2)) / 8.0
+    assert rel_l2(lse.cpu(), torch.logsumexp(s, -1).cpu()) < 1e-4
+
+
+def test_attention_softmax_rescale_branch(nat):
+    """A key block late in the sweep carries a spiked score so the running max jumps (rule 26)."""
+    Hh, S = 1, 1024
+    qkv = _rand(S, 3 * 64, scale=0.5, seed=19)
+    qkv[:, 64:128][900] *= 40.0
+    qkv = qkv.to(torch.bfloat16)
+    o = torch.empty(S, 64, device="cuda", dtype=torch.bfloat16)
+    nat.attention(qkv, qkv[:, 64:], qkv[:, 128:], o, batch=1, heads=1, seq_q=S, seq_kv=S, q_bstride=0, q_rstride=192,
+                  k_bstride=0, k_rstride=192, v_bstride=0, v_rstride=192, o_bstride=0, o_rstride=64)
+    t = qkv.view(1, S, 3, 1, 64).permute(2, 0, 3, 1, 4)
+    ref = _sdpa_ref(t[0], t[1], t[2])[0, 0]
+    assert rel_l2(o.float().cpu(), ref.cpu()) < 8e-3
+
+
+# ----------------------------------------------------------------------------------------------- others
+@pytest.mark.parametrize("dim", [768, 1024])
+def test_layernorm(nat, dim):
+    rows = 517
+    x = _rand(rows + 7, dim, scale=3.0, seed=20) + 1.5
+    w, b = _rand(dim, seed=21), _rand(dim, seed=22)
+    yf = torch.empty(rows, dim, device="cuda")
+    yl = torch.empty(rows, dim, device="cuda", dtype=torch.bfloat16)
+    nat.layernorm(x, rows, dim, w, b, y_f32=yf, y_lp=yl)
+    ref = F.layer_norm(x[:rows], (dim,), w, b, 1e-6)
+    assert rel_l2(yf.cpu(), ref.cpu()) < 1e-6
+    assert rel_l2(yl.float().cpu(), ref.cpu()) < 5e-3
+    # grouped rows: drop the first row of every group of T+1 (DINOv2 cls)
+    T = 10
+    yg = torch.empty(30, dim, device="cuda")
+    nat.layernorm(x, 30, dim, w, b, y_f32=yg, group=T, group_stride=T + 1, row_off=1)
+    idx = torch.tensor([g * (T + 1) + 1 + t for g in range(3) for t in range(T)])
+    assert rel_l2(yg.cpu(), F.layer_norm(x[idx], (dim,), w, b, 1e-6).cpu()) < 1e-6
+
+
+@pytest.mark.parametrize("IH,IW,OHf,OWf,OH,OW", [(19, 19, 38, 38, 37, 37), (37, 37, 74, 74, 74, 74),
+                                                 (296, 296, 518, 518, 518, 518), (16, 16, 224, 224, 224, 224)])
+def test_bilinear_align_corners(nat, IH, IW, OHf, OWf, OH, OW):
+    n, C = 2, 128
+    x = _rand(n, C, IH, IW, seed=23)
+    ref = F.interpolate(x, size=(OHf, OWf), mode="bilinear", align_corners=True)[:, :, :OH, :OW]
+    out = torch.empty(n, OH, OW, C, device="cuda")
+    nat.bilinear_ac(x.permute(0, 2, 3, 1).contiguous(), n, IH, IW, C, OHf, OWf, OH, OW, out)
+    assert rel_l2(out.permute(0, 3, 1, 2).cpu(), ref.cpu()) < 3e-5  # fp32 op-order vs ATen GPU kernel
+
+
+def test_splitmix_fill_matches_numpy(nat):
+    from mapanything.utils.synthetic import GLOBAL_SEED, fnv1a64, named_uniform
+
+    name = "encoder.model.blocks.3.mlp.fc1.weight"
+    ref = named_uniform(name, (4096, 1024), -0.054, 0.054)
+    out = torch.empty(4096 * 1024, device="cuda")
+    half = np.float32(0.054)
+    nat.fill_splitmix(out, fnv1a64(name) ^ GLOBAL_SEED, float(half), 0.0)
+    assert np.array_equal(out.cpu().numpy().reshape(4096, 1024), ref)
+
+
+def test_patchify_and_tokens(nat):
+    n, H, W = 2, 56, 70
+    img = _rand(n, 3, H, W, seed=24)
+    out = torch.empty(n * (H // 14) * (W // 14), 640, device="cuda")
+    nat.patchify(img, n, H, W, out, 640)
+    ref = F.unfold(img, 14, stride=14).transpose(1, 2).reshape(-1, 588)
+    assert torch.equal(out[:, :588].cpu(), ref.cpu())
+    assert torch.count_nonzero(out[:, 588:]).item() == 0

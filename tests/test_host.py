@@ -1,0 +1,86 @@
+"""Host-side logic: state-dict layout vs the reference, synthetic checkpoint determinism, input validation."""
+
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+
+def test_state_dict_layout_matches_reference():
+    from mapanything.models.mapanything.spec import canonical_spec, full_spec
+
+    ref = json.load(open(os.path.join(GOLDEN, "ref_state_dict_spec.json")))
+    mine = dict(full_spec())
+    assert len(ref) == len(mine) == 880
+    for k, shape in ref:
+        assert tuple(mine[k]) == tuple(shape), k
+    assert sum(int(np.prod(s)) for _, s in canonical_spec()) == 563336150
+
+
+def test_synthetic_generator_is_deterministic_and_scaled():
+    from mapanything.utils.synthetic import named_uniform, splitmix_uniform, tensor_init
+
+    a = named_uniform("x.weight", (64, 32), -1, 1)
+    b = named_uniform("x.weight", (64, 32), -1, 1)
+    assert np.array_equal(a, b)
+    assert not np.array_equal(a, named_uniform("y.weight", (64, 32), -1, 1))
+    u = splitmix_uniform(12345, 100000)
+    assert u.min() >= 0 and u.max() < 1 and abs(u.mean() - 0.5) < 0.01
+    w = tensor_init("info_sharing.self_attention_blocks.0.mlp.fc1.weight", (3072, 768))
+    assert abs(np.abs(w).max() - np.sqrt(3 / 768)) < 1e-3
+    pe = tensor_init("info_sharing.view_pos_table", (1, 768))
+    assert np.array_equal(pe[0, 0::2], np.zeros(384, np.float32)) and np.array_equal(pe[0, 1::2], np.ones(384))
+
+
+def test_validation_errors_match_reference_rules():
+    from mapanything.utils.inference import validate_input_views_for_inference as val
+
+    img = torch.zeros(1, 3, 28, 28)
+    with pytest.raises(ValueError, match="At least one view"):
+        val([])
+    with pytest.raises(ValueError, match="missing required keys"):
+        val([{"img": img}])
+    with pytest.raises(ValueError, match="conflicting keys"):
+        val([{"img": img, "data_norm_type": ["dinov2"], "intrinsics": 1, "ray_directions": 2}])
+    with pytest.raises(ValueError, match="depth constraint"):
+        val([{"img": img, "data_norm_type": ["dinov2"], "depth_z": 1}])
+    with pytest.raises(ValueError, match="Camera pose constraint"):
+        val([{"img": img, "data_norm_type": ["dinov2"]},
+             {"img": img, "data_norm_type": ["dinov2"], "camera_poses": 1}])
+    with pytest.raises(ValueError, match="First View"):
+        val([{"data_norm_type": ["dinov2"], "intrinsics": 1, "camera_poses": 1}])
+    ok = [{"img": img, "data_norm_type": ["dinov2"]}]
+    assert val(ok) is ok
+
+
+def test_preprocess_matches_oracle_restatement():
+    from mapanything.utils.inference import preprocess_input_views_for_inference
+    from oracle.mapa_oracle import preprocess_views
+
+    K = torch.tensor([[[30.0, 0, 14.0], [0, 31.0, 13.5], [0, 0, 1]]])
+    d = torch.rand(1, 28, 28, generator=torch.Generator().manual_seed(0)) * 5
+    q = torch.tensor([[0.1, 0.2, 0.3, 0.9]])
+    q = q / q.norm()
+    views = [{"img": torch.zeros(1, 3, 28, 28), "data_norm_type": ["dinov2"], "intrinsics": K, "depth_z": d,
+              "camera_poses": (q, torch.tensor([[1.0, 2.0, 3.0]]))}]
+    a = preprocess_input_views_for_inference([dict(v) for v in views])[0]
+    b = preprocess_views([dict(v) for v in views])[0]
+    for k in ("ray_directions_cam", "depth_along_ray", "camera_pose_quats", "camera_pose_trans"):
+        assert torch.allclose(a[k], b[k], atol=1e-6), k
+    assert bool(a["is_metric_scale"].all())
+
+
+def test_config_guard_rejects_other_architectures():
+    from mapanything.models import MapAnything
+    from tests_helpers import released_config
+
+    cfg = released_config()
+    m = MapAnything(**cfg)
+    assert m.class_init_args["name"] == "mapanything"
+    cfg["pred_head_config"] = dict(cfg["pred_head_config"], type="linear")
+    with pytest.raises(ValueError, match="unsupported"):
+        MapAnything(**cfg)
