@@ -17,6 +17,7 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "map-anything_amd"))
 sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

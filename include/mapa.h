@@ -113,8 +113,9 @@ int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, const float*
 int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH, int OW,
                      void* out, int out_dtype, mapa_stream_t stream);
 
-/* mean over `tokens` rows per image: x [n][tokens][C] f32 -> y [n][C] (AdaptiveAvgPool2d(1), pose_head.py:150) */
-int mapa_mean_tokens(const float* x, int n, int tokens, int C, float* y, mapa_stream_t stream);
+/* mean over `tokens` rows per image: x [n][tokens][C] f32 -> y [n][C] (AdaptiveAvgPool2d(1), pose_head.py:150).
+ * work: n*32*C floats of scratch (deterministic two-pass reduction). */
+int mapa_mean_tokens(const float* x, int n, int tokens, int C, float* y, void* work, mapa_stream_t stream);
 
 /* small fp32 linear for M <= 64 rows: y[m][n] = act(sum_k x[m][k] w[n][k] + b[n])  (pose/scale MLPs) */
 int mapa_linear_small(const float* x, int M, int K, const float* w, const float* b, int N, int act, float* y,

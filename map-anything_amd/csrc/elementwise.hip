@@ -115,16 +115,27 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
 }
 
 // ------------------------------------------------------------------------------------------ mean over T
-__global__ void mean_tokens_kernel(const float* __restrict__ x, int n, int T, int C, float* __restrict__ y) {
-  const int64_t total = (int64_t)n * C;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(e % C);
-    const int im = (int)(e / C);
-    const float* p = x + (int64_t)im * T * C + c;
-    float s = 0.f;
-    for (int t = 0; t < T; ++t) s += p[(int64_t)t * C];
-    y[e] = s / (float)T;
-  }
+// Two deterministic passes: partial sums over token chunks (coalesced rows), then the chunk sum in fixed order.
+constexpr int MEAN_CHUNKS = 32;
+__global__ void mean_tokens_partial_kernel(const float* __restrict__ x, int n, int T, int C,
+                                           float* __restrict__ part) {
+  const int cblk = blockIdx.x, chunk = blockIdx.y, im = blockIdx.z;
+  const int c = cblk * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const int t0 = (int)((int64_t)T * chunk / MEAN_CHUNKS), t1 = (int)((int64_t)T * (chunk + 1) / MEAN_CHUNKS);
+  const float* p = x + (int64_t)im * T * C + c;
+  float s = 0.f;
+  for (int t = t0; t < t1; ++t) s += p[(int64_t)t * C];
+  part[((int64_t)im * MEAN_CHUNKS + chunk) * C + c] = s;
+}
+
+__global__ void mean_tokens_final_kernel(const float* __restrict__ part, int n, int T, int C, float* __restrict__ y) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= (int64_t)n * C) return;
+  const int c = (int)(e % C), im = (int)(e / C);
+  float s = 0.f;
+  for (int k = 0; k < MEAN_CHUNKS; ++k) s += part[((int64_t)im * MEAN_CHUNKS + k) * C + c];
+  y[e] = s / (float)T;
 }
 
 // -------------------------------------------------------------------------------------- small linear
@@ -313,9 +324,13 @@ extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int
   return 0;
 }
 
-extern "C" int mapa_mean_tokens(const float* x, int n, int tokens, int C, float* y, hipStream_t stream) {
-  MAPA_CHECK_ARG(x && y && n > 0 && tokens > 0 && C > 0, "mapa_mean_tokens: bad args");
-  hipLaunchKernelGGL(mean_tokens_kernel, dim3(grid_for((int64_t)n * C)), dim3(TPB), 0, stream, x, n, tokens, C, y);
+extern "C" int mapa_mean_tokens(const float* x, int n, int tokens, int C, float* y, void* work, hipStream_t stream) {
+  MAPA_CHECK_ARG(x && y && work && n > 0 && tokens > 0 && C > 0, "mapa_mean_tokens: bad args");
+  float* part = reinterpret_cast<float*>(work);
+  hipLaunchKernelGGL(mean_tokens_partial_kernel, dim3((C + 255) / 256, MEAN_CHUNKS, n), dim3(256), 0, stream, x, n,
+                     tokens, C, part);
+  hipLaunchKernelGGL(mean_tokens_final_kernel, dim3((unsigned)(((int64_t)n * C + 255) / 256)), dim3(256), 0, stream,
+                     part, n, tokens, C, y);
   MAPA_CHECK_LAUNCH("mapa_mean_tokens");
   return 0;
 }

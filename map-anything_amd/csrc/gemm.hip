@@ -11,14 +11,18 @@
 //  * 256 threads = 4 waves (2x2), block tile 128x128, wave tile 64x64 = 4x4 MFMA 16x16 tiles.
 //  * Operands staged HBM -> LDS with global_load_lds (16 B per lane, LDS image lane-linear); the 16-B chunk
 //    XOR swizzle (chunk ^ row&7) is applied on the per-lane SOURCE address so that the ds_read_b128 fragment
-//    reads are bank-conflict free.  Two LDS stages (double buffer), one barrier per K tile.
-//  * Out-of-range rows / K-tail chunks / conv halo taps read a 16-byte zero page instead of branching.
+//    reads are bank-conflict free.  Two LDS stages (double buffer), one barrier per K tile.  The wave index is
+//    made provably uniform (readfirstlane) so the LDS-DMA destination (M0) never needs a waterfall loop, and
+//    every per-lane source address is precomputed once: the K loop adds a byte offset and issues the DMA.
+//  * Rows past M / N are clamped to the last row (their results are never stored); K-tail chunks and conv
+//    halo taps read a 16-byte zero page.
 //  * Two arithmetic variants behind one loader/epilogue: bf16 operands with v_mfma_f32_16x16x32_bf16
 //    (fast path), and fp32 operands with v_mfma_f32_16x16x4_f32 (exact-fp32 "precise" parity mode).
 //    Each LDS row is 128 B in both (64 bf16 or 32 fp32 of K), so the staging code is shared.
-//  * A operand modes: dense rows, or implicit 3x3 convolution (pad 1, stride 1/2) over an NHWC tensor.
-//  * Fused epilogue: out = resid1 + resid2 + gamma * act(acc + bias); optional fp32 output, low-precision
-//    output, ReLU'd low-precision output; row-major or pixel-shuffle (ConvTranspose k=s) addressing.
+//  * A operand modes (template): dense rows, or implicit 3x3 convolution (pad 1, stride 1/2) over NHWC.
+//  * Epilogue staged through LDS so every lane stores 16 contiguous output bytes: out = resid1 + resid2 +
+//    gamma * act(acc + bias); fp32 and/or low-precision and/or ReLU'd low-precision outputs; row-major or
+//    pixel-shuffle (ConvTranspose k=s) addressing.
 //  * XCD-aware tile order (bijective remap: consecutive tiles share an XCD's L2).
 #include "mapa_common.h"
 
@@ -27,7 +31,10 @@ namespace {
 constexpr int BM = 128, BN = 128, NTHREADS = 256;
 constexpr int ROW_BYTES = 128;                       // one LDS row of the K tile
 constexpr int TILE_BYTES = BM * ROW_BYTES;           // 16 KiB per operand per stage
-constexpr int LDS_BYTES = 2 * 2 * TILE_BYTES;        // 2 stages x (A, W)
+constexpr int MAIN_LDS = 2 * 2 * TILE_BYTES;         // 2 stages x (A, W)
+constexpr int EPI_LD = 68;                           // fp32 row stride of the epilogue staging tile
+constexpr int EPI_LDS = 4 * 64 * EPI_LD * 4;         // 4 waves x 64 rows
+constexpr int LDS_BYTES = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
 
 struct TraitsBF16 {
   using T = bf16_t;
@@ -46,7 +53,6 @@ struct GemmArgs {
   const void* W;
   int64_t ldw;
   int M, N, K;
-  int a_mode;  // 0 dense, 1 conv3x3
   int cv_C, cv_IH, cv_IW, cv_OH, cv_OW, cv_stride;
   const float* bias;
   int bias_mod;
@@ -60,6 +66,7 @@ struct GemmArgs {
   int64_t ldo;
   int out_mode;  // 0 row-major, 1 pixel shuffle
   int ps_s, ps_h, ps_w, ps_cout;
+  int vec_ok;    // N % 4 == 0, ldo % 4 == 0, ps_cout % 4 == 0: 4-wide epilogue
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblk) {
@@ -105,13 +112,20 @@ __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int 
   }
 }
 
-template <typename Tr>
+__device__ __forceinline__ float epi_act(float v, int act) {
+  if (act == 1) return gelu_erf(v);
+  if (act == 2) return fmaxf(v, 0.f);
+  return v;
+}
+
+template <typename Tr, int AMODE>
 __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
   using T = typename Tr::T;
   constexpr int E = Tr::E, BK = Tr::BK;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: no M0 waterfall
   const int wm = wave >> 1, wn = wave & 1;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
@@ -120,65 +134,56 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
   // ---- per-thread staging geometry: 4 rows (one per load instruction), one fixed source chunk ----------
   const int sc = (lane & 7) ^ (lane >> 3);  // source chunk (pre-swizzled)
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
-  const char* a_row[4];
+  const char* a_src[4];
+  const char* w_src[4];
   int cv_base[4], cv_iy[4], cv_ix[4];
-  const char* w_row[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = (i * 4 + wave) * 8 + (lane >> 3);
-    const int m = bm + r, n = bn + r;
-    w_row[i] = n < p.N ? reinterpret_cast<const char*>(p.W) + (int64_t)n * p.ldw * sizeof(T) : nullptr;
-    if (p.a_mode == 0) {
-      a_row[i] = m < p.M ? reinterpret_cast<const char*>(p.A) + (int64_t)m * p.lda * sizeof(T) : nullptr;
+    const int m = min(bm + r, p.M - 1), n = min(bn + r, p.N - 1);
+    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + sc * E) * sizeof(T);
+    if constexpr (AMODE == 0) {
+      a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + sc * E) * sizeof(T);
     } else {
-      a_row[i] = nullptr;
-      if (m < p.M) {
-        const int hw = p.cv_OH * p.cv_OW;
-        const int img = m / hw, rem = m - img * hw;
-        const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
-        cv_base[i] = img * p.cv_IH * p.cv_IW;
-        cv_iy[i] = oy * p.cv_stride - 1;
-        cv_ix[i] = ox * p.cv_stride - 1;
-      } else {
-        cv_base[i] = -1;
-        cv_iy[i] = cv_ix[i] = 0;
-      }
+      const int hw = p.cv_OH * p.cv_OW;
+      const int img = m / hw, rem = m - img * hw;
+      const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
+      cv_base[i] = img * p.cv_IH * p.cv_IW;
+      cv_iy[i] = oy * p.cv_stride - 1;
+      cv_ix[i] = ox * p.cv_stride - 1;
     }
   }
-  // conv: (tap, ci) of this thread's chunk, advanced incrementally by BK per tile
-  int cv_tap = 0, cv_ci = sc * E;
-  if (p.a_mode == 1) {
-    while (cv_ci >= p.cv_C) { cv_ci -= p.cv_C; ++cv_tap; }
-  }
-
   const int nk = (p.K + BK - 1) / BK;
+  const bool k_exact = (p.K % BK) == 0;
+  const int lds_base = wave * 64 * 16;
 
   auto stage = [&](int buf, int kt) {
     char* As = lds + buf * 2 * TILE_BYTES;
     char* Bs = As + TILE_BYTES;
     const int kc = kt * BK + sc * E;
-    const bool kin = kc < p.K;
+    const bool kin = k_exact || kc < p.K;
+    const int64_t koff = (int64_t)kt * BK * sizeof(T);
+    int tap = 0, ci = 0;
+    if constexpr (AMODE == 1) {
+      tap = kc / p.cv_C;
+      ci = kc - tap * p.cv_C;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int base = ((i * 4 + wave) * 64) * 16;
+      const int off = lds_base + i * 4 * 64 * 16;
       const char* src;
-      if (p.a_mode == 0) {
-        src = (a_row[i] && kin) ? a_row[i] + (int64_t)kc * sizeof(T) : zero;
+      if constexpr (AMODE == 0) {
+        src = kin ? a_src[i] + koff : zero;
       } else {
-        const int ky = cv_tap / 3, kx = cv_tap - ky * 3;
+        const int ky = tap / 3, kx = tap - ky * 3;
         const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
-        const bool ok = kin && cv_base[i] >= 0 && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+        const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
         src = ok ? reinterpret_cast<const char*>(p.A) +
-                       ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + cv_ci) * sizeof(T)
+                       ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * sizeof(T)
                  : zero;
       }
-      __builtin_amdgcn_global_load_lds(src, As + base, 16, 0, 0);
-      const char* wsrc = (w_row[i] && kin) ? w_row[i] + (int64_t)kc * sizeof(T) : zero;
-      __builtin_amdgcn_global_load_lds(wsrc, Bs + base, 16, 0, 0);
-    }
-    if (p.a_mode == 1) {
-      cv_ci += BK;
-      while (cv_ci >= p.cv_C) { cv_ci -= p.cv_C; ++cv_tap; }
+      __builtin_amdgcn_global_load_lds(src, As + off, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(kin ? w_src[i] + koff : zero, Bs + off, 16, 0, 0);
     }
   };
 
@@ -200,51 +205,96 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
     __syncthreads();
   }
 
-  // ---- epilogue -----------------------------------------------------------------------------------------
-  const int g = lane >> 4, c16 = lane & 15;
+  // ---- epilogue: accumulators -> LDS (per-wave 64 x 64 fp32 tile) -> 16-B row segments -----------------
+  float* ep = reinterpret_cast<float*>(lds) + wave * 64 * EPI_LD;
+  {
+    const int g = lane >> 4, c16 = lane & 15;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n = bn + wn * 64 + j * 16 + c16;
-    if (n >= p.N) continue;
-    const float bv = p.bias ? p.bias[n % p.bias_mod] : 0.f;
-    const float gv = p.gamma ? p.gamma[n] : 1.f;
-    int64_t col_off = n;
-    int ps_ky = 0, ps_kx = 0;
-    if (p.out_mode == 1) {
-      const int co = n % p.ps_cout, t = n / p.ps_cout;
-      ps_ky = t / p.ps_s;
-      ps_kx = t - ps_ky * p.ps_s;
-      col_off = co;
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * EPI_LD + j * 16 + c16] = acc[i][j][r];
+  }
+  __syncthreads();
+  const int c4 = (lane & 15) * 4;
+  const int n0 = bn + wn * 64 + c4;
+  if (n0 >= p.N) return;
+  float bv[4], gv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int n = min(n0 + e, p.N - 1);
+    bv[e] = p.bias ? p.bias[n % p.bias_mod] : 0.f;
+    gv[e] = p.gamma ? p.gamma[n] : 1.f;
+  }
+  int64_t col_off = n0;
+  int ps_ky = 0, ps_kx = 0;
+  if (p.out_mode == 1) {
+    const int co = n0 % p.ps_cout, t = n0 / p.ps_cout;
+    ps_ky = t / p.ps_s;
+    ps_kx = t - ps_ky * p.ps_s;
+    col_off = co;
+  }
+  const bool vec = p.vec_ok && (n0 + 3 < p.N);
+#pragma unroll 4
+  for (int pass = 0; pass < 16; ++pass) {
+    const int rloc = pass * 4 + (lane >> 4);
+    const int m = bm + wm * 64 + rloc;
+    if (m >= p.M) break;
+    const f32x4 a = *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c4);
+    int64_t off;
+    if (p.out_mode == 0) {
+      off = (int64_t)m * p.ldo + col_off;
+    } else {
+      const int hw = p.ps_h * p.ps_w;
+      const int img = m / hw, rem = m - img * hw;
+      const int y = rem / p.ps_w, x = rem - y * p.ps_w;
+      const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
+      off = (((int64_t)img * H2 + y * p.ps_s + ps_ky) * W2 + x * p.ps_s + ps_kx) * p.ps_cout + col_off;
     }
+    f32x4 v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = bm + wm * 64 + i * 16 + g * 4 + r;
-        if (m >= p.M) continue;
-        int64_t off;
-        if (p.out_mode == 0) {
-          off = (int64_t)m * p.ldo + col_off;
-        } else {
-          const int hw = p.ps_h * p.ps_w;
-          const int img = m / hw, rem = m - img * hw;
-          const int y = rem / p.ps_w, x = rem - y * p.ps_w;
-          const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
-          off = (((int64_t)img * H2 + y * p.ps_s + ps_ky) * W2 + x * p.ps_s + ps_kx) * p.ps_cout + col_off;
+    for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + bv[e], p.act) * gv[e];
+    if (vec) {
+      if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
+      if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
+      if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
+      if constexpr (sizeof(T) == 2) {
+        if (p.out_lp) {
+          uint2 u;
+          u.x = pack_bf16x2(v[0], v[1]);
+          u.y = pack_bf16x2(v[2], v[3]);
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
         }
-        float v = acc[i][j][r] + bv;
-        if (p.act == 1) v = gelu_erf(v);
-        else if (p.act == 2) v = fmaxf(v, 0.f);
-        v *= gv;
-        if (p.resid1) v += p.resid1[off];
-        if (p.resid2) v += p.resid2[off];
-        if (p.out_f32) p.out_f32[off] = v;
+        if (p.out_lp_relu) {
+          uint2 u;
+          u.x = pack_bf16x2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
+          u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
+        }
+      } else {
+        if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
+        if (p.out_lp_relu) {
+          f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off) = rr;
+        }
+      }
+    } else {
+      // scalar tail (N % 4 != 0 or the last partial column group); row-major only
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (n0 + e >= p.N) break;
+        const int64_t o = off + e;
+        float x = v[e];
+        if (p.resid1) x += p.resid1[o];
+        if (p.resid2) x += p.resid2[o];
+        if (p.out_f32) p.out_f32[o] = x;
         if constexpr (sizeof(T) == 2) {
-          if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[off] = f32_to_bf16(v);
-          if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[off] = f32_to_bf16(fmaxf(v, 0.f));
+          if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
+          if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
         } else {
-          if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[off] = v;
-          if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[off] = fmaxf(v, 0.f);
+          if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
+          if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);
         }
       }
     }
@@ -268,14 +318,16 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
     const int oh = (d->conv_IH + 2 - 3) / d->conv_stride + 1, ow = (d->conv_IW + 2 - 3) / d->conv_stride + 1;
     MAPA_CHECK_ARG(oh == d->conv_OH && ow == d->conv_OW, "mapa_gemm: conv out %dx%d != expected %dx%d",
                    d->conv_OH, d->conv_OW, oh, ow);
+    MAPA_CHECK_ARG((int64_t)d->conv_OH * d->conv_OW > 0 && d->M % (d->conv_OH * d->conv_OW) == 0,
+                   "mapa_gemm: conv M must be images * OH * OW");
   } else {
     MAPA_CHECK_ARG(d->a_mode == MAPA_A_DENSE, "mapa_gemm: bad a_mode");
-    MAPA_CHECK_ARG(d->lda >= d->K, "mapa_gemm: lda < K");
+    MAPA_CHECK_ARG(d->lda >= d->K && d->lda % E == 0, "mapa_gemm: lda must be >= K and keep 16-B rows");
   }
-  MAPA_CHECK_ARG(d->ldw >= d->K, "mapa_gemm: ldw < K");
+  MAPA_CHECK_ARG(d->ldw >= d->K && d->ldw % E == 0, "mapa_gemm: ldw must be >= K and keep 16-B rows");
   if (d->out_mode == MAPA_OUT_PIXSHUF) {
     MAPA_CHECK_ARG(d->ps_s > 0 && d->ps_cout > 0 && d->N == d->ps_s * d->ps_s * d->ps_cout &&
-                       d->M % (d->ps_h * d->ps_w) == 0,
+                       d->M % (d->ps_h * d->ps_w) == 0 && d->ps_cout % 4 == 0,
                    "mapa_gemm: bad pixel-shuffle geometry");
   } else {
     MAPA_CHECK_ARG(d->ldo >= d->N, "mapa_gemm: ldo < N");
@@ -283,7 +335,6 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   GemmArgs a;
   a.A = d->A; a.lda = d->lda; a.W = d->W; a.ldw = d->ldw;
   a.M = d->M; a.N = d->N; a.K = d->K;
-  a.a_mode = d->a_mode;
   a.cv_C = d->conv_C; a.cv_IH = d->conv_IH; a.cv_IW = d->conv_IW; a.cv_OH = d->conv_OH; a.cv_OW = d->conv_OW;
   a.cv_stride = d->conv_stride;
   a.bias = d->bias; a.bias_mod = d->bias_mod > 0 ? d->bias_mod : d->N;
@@ -291,11 +342,17 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   a.resid1 = d->resid1; a.resid2 = d->resid2;
   a.out_f32 = d->out_f32; a.out_lp = d->out_lp; a.out_lp_relu = d->out_lp_relu; a.ldo = d->ldo;
   a.out_mode = d->out_mode; a.ps_s = d->ps_s; a.ps_h = d->ps_h; a.ps_w = d->ps_w; a.ps_cout = d->ps_cout;
+  a.vec_ok = (d->N % 4 == 0) && (d->out_mode == MAPA_OUT_PIXSHUF || d->ldo % 4 == 0);
+  MAPA_CHECK_ARG(a.vec_ok || d->out_mode == MAPA_OUT_ROWMAJOR, "mapa_gemm: pixel shuffle needs N %% 4 == 0");
   const int nblk = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
-  if (d->dtype == MAPA_BF16)
-    hipLaunchKernelGGL(gemm_kernel<TraitsBF16>, dim3(nblk), dim3(NTHREADS), 0, stream, a);
-  else
-    hipLaunchKernelGGL(gemm_kernel<TraitsF32>, dim3(nblk), dim3(NTHREADS), 0, stream, a);
+  const bool conv = d->a_mode == MAPA_A_CONV3X3;
+  if (d->dtype == MAPA_BF16) {
+    if (conv) hipLaunchKernelGGL((gemm_kernel<TraitsBF16, 1>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
+    else hipLaunchKernelGGL((gemm_kernel<TraitsBF16, 0>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
+  } else {
+    if (conv) hipLaunchKernelGGL((gemm_kernel<TraitsF32, 1>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
+    else hipLaunchKernelGGL((gemm_kernel<TraitsF32, 0>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
+  }
   MAPA_CHECK_LAUNCH("mapa_gemm");
   return 0;
 }

@@ -83,7 +83,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_assemble_tokens.argtypes = [vp, vp, vp, i, i, i, vp, vp]
     L.mapa_add_rowvec.argtypes = [vp, i64, i, i, i, vp, vp]
     L.mapa_bilinear_ac.argtypes = [vp, i, i, i, i, i, i, i, i, i, vp, i, vp]
-    L.mapa_mean_tokens.argtypes = [vp, i, i, i, vp, vp]
+    L.mapa_mean_tokens.argtypes = [vp, i, i, i, vp, vp, vp]
     L.mapa_linear_small.argtypes = [vp, i, i, vp, vp, i, i, vp, vp]
     L.mapa_pose_scale_finalize.argtypes = [vp, vp, i, i, vp, vp, vp, vp]
     L.mapa_dense_head_out.argtypes = [vp, i, i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -251,7 +251,8 @@ def bilinear_ac(inp, n, IH, IW, C, OHf, OWf, OH, OW, out):
 
 
 def mean_tokens(x, n, T, C, y):
-    check(lib().mapa_mean_tokens(ptr(x), n, T, C, ptr(y), stream()), "mapa_mean_tokens")
+    work = torch.empty(n * 32 * C, device=x.device, dtype=torch.float32)
+    check(lib().mapa_mean_tokens(ptr(x), n, T, C, ptr(y), ptr(work), stream()), "mapa_mean_tokens")
 
 
 def linear_small(x, M, K, w, b, N, act, y):

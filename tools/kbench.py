@@ -1,0 +1,78 @@
+"""Kernel micro-benchmark: TFLOP/s of the hot GEMM / conv / attention shapes of the 8-view 518x518 workload
+(HIP-event timing, random data).  Usage: python tools/kbench.py [gemm|attn|conv|all] [reps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "map-anything_amd"))
+import torch  # noqa: E402
+
+from mapanything import _native as nat  # noqa: E402
+
+nat.lib()
+V, T = 8, 1369
+R, L = V * (T + 1), V * T + 1
+GEMMS = [("enc.qkv", R, 3072, 1024), ("enc.proj", R, 1024, 1024), ("enc.fc1", R, 4096, 1024),
+         ("enc.fc2", R, 1024, 4096), ("aat.qkv", L, 2304, 768), ("aat.proj", L, 768, 768),
+         ("aat.fc1", L, 3072, 768), ("aat.fc2", L, 768, 3072), ("pose.res", V * T, 784, 784)]
+CONVS = [("rn1.c@148", V, 148, 148, 256, 256), ("reg.c2@518", V, 518, 518, 128, 128),
+         ("reg.c1@296", V, 296, 296, 256, 128), ("rn2.c@74", V, 74, 74, 256, 256)]
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    dt = torch.bfloat16
+    if what in ("gemm", "all"):
+        for name, M, N, K in GEMMS:
+            A = (torch.randn(M, K, device="cuda") * 0.5).to(dt)
+            W = (torch.randn(N, K, device="cuda") * K ** -0.5).to(dt)
+            b = torch.randn(N, device="cuda")
+            o = torch.empty(M, N, device="cuda", dtype=dt)
+            ms = timeit(lambda: nat.gemm(A, W, M, N, K, bias=b, out_lp=o), reps)
+            ms_t = timeit(lambda: torch.nn.functional.linear(A, W, b.to(dt)), reps) if "torch" in sys.argv else 0
+            print(f"gemm {name:10s} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s"
+                  + (f"   [hipBLASLt via torch: {2*M*N*K/ms_t/1e9:7.1f} TF/s]" if ms_t else ""), flush=True)
+    if what in ("conv", "all"):
+        for name, n, H, W_, C, Co in CONVS:
+            x = (torch.randn(n, H, W_, C, device="cuda") * 0.5).to(dt)
+            w = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(dt)
+            b = torch.randn(Co, device="cuda")
+            o = torch.empty(n * H * W_, Co, device="cuda", dtype=dt)
+            M = n * H * W_
+            ms = timeit(lambda: nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1)), reps)
+            print(f"conv {name:10s} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  {2*M*Co*9*C/ms/1e9:7.1f} TF/s",
+                  flush=True)
+    if what in ("attn", "all"):
+        for name, B, Hh, S in [("enc", V, 16, T + 1), ("frame", V, 12, T), ("global", 1, 12, L)]:
+            C = Hh * 64
+            qkv = torch.randn(B * S, 3 * C, device="cuda").to(dt)
+            o = torch.empty(B * S, C, device="cuda", dtype=dt)
+            rs = 3 * C
+            f = lambda: nat.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B, heads=Hh, seq_q=S, seq_kv=S,
+                                      q_bstride=S * rs, q_rstride=rs, k_bstride=S * rs, k_rstride=rs,
+                                      v_bstride=S * rs, v_rstride=rs, o_bstride=S * C, o_rstride=C)
+            ms = timeit(f, reps)
+            if "torch" in sys.argv:
+                t = qkv.view(B, S, 3, Hh, 64).permute(2, 0, 3, 1, 4)
+                q, k, v = t[0].contiguous(), t[1].contiguous(), t[2].contiguous()
+                ms_t = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), reps)
+                print(f"  torch SDPA {name}: {4*B*Hh*S*S*64/ms_t/1e9:7.1f} TF/s", flush=True)
+            print(f"attn {name:10s} B={B} H={Hh} S={S}: {ms*1e3:8.1f} us  {4*B*Hh*S*S*64/ms/1e9:7.1f} TF/s",
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
