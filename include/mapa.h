@@ -72,7 +72,11 @@ int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
  *   q + b*q_bstride + i*q_rstride + h*64 + d   (same for k, v, o), so the packed qkv GEMM output is read in place.
  * Q rows [0, seq_q) attend to K/V rows [0, seq_kv) of the same batch; o receives the per-head outputs.
  * lse (optional, f32 [batch][heads][seq_q]) receives log-sum-exp of the scaled scores for chunk merging.
+ * kv_nseg > 0: the seq_kv logical keys live in kv_nseg row segments of K/V (physical rows
+ * [kv_seg_start[s], kv_seg_start[s] + kv_seg_len[s])), e.g. the padded per-rank slots of an RCCL all-gather;
+ * seq_kv must equal the sum of the lengths.
  * ------------------------------------------------------------------------------------------------------- */
+#define MAPA_MAX_KV_SEGMENTS 16
 typedef struct {
   int dtype;
   int batch, heads, seq_q, seq_kv;
@@ -82,6 +86,9 @@ typedef struct {
   void* o;
   int64_t q_bstride, q_rstride, k_bstride, k_rstride, v_bstride, v_rstride, o_bstride, o_rstride;
   float* lse;
+  int kv_nseg;
+  int kv_seg_start[MAPA_MAX_KV_SEGMENTS];
+  int kv_seg_len[MAPA_MAX_KV_SEGMENTS];
 } mapa_attn_desc;
 
 int mapa_attention(const mapa_attn_desc* d, mapa_stream_t stream);

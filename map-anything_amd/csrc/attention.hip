@@ -33,7 +33,22 @@ struct AttnArgs {
   float* lse;
   int64_t qb, qr, kb, kr, vb, vr, ob, orr;
   int batch, heads, seq_q, seq_kv;
+  int nseg;
+  int seg_start[MAPA_MAX_KV_SEGMENTS];
+  int seg_len[MAPA_MAX_KV_SEGMENTS];
 };
+
+// logical key -> physical K/V row (identity unless the keys are split into segments)
+__device__ __forceinline__ int kv_row(const AttnArgs& p, int key) {
+  if (p.nseg == 0) return key;
+  int acc = 0;
+#pragma unroll 1
+  for (int s = 0; s < p.nseg; ++s) {
+    if (key < acc + p.seg_len[s]) return p.seg_start[s] + (key - acc);
+    acc += p.seg_len[s];
+  }
+  return 0;
+}
 
 __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   const int q = nblk / 8, r = nblk % 8, x = b % 8;
@@ -52,7 +67,7 @@ __device__ __forceinline__ s4v tr_read(const char* p) {
 __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
   constexpr int TILE = KT * 128;  // 64 rows x 128 B
   __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5, l32 = lane & 31;
   const int nqt = (p.seq_q + QBLK - 1) / QBLK;
   const int nblk = nqt * p.heads * p.batch;
@@ -88,8 +103,9 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
       const int key = kt * KT + row;
       const int kc = pos ^ ((row >> 1) & 7);
       const int vc = pos ^ (((row >> 1) & 1) << 2);
-      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)key * p.kr + kc * 8) : zero;
-      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)key * p.vr + vc * 8) : zero;
+      const int pr = kv_row(p, key);
+      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)pr * p.kr + kc * 8) : zero;
+      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)pr * p.vr + vc * 8) : zero;
       const int base = (i * 4 + wave) * 64 * 16;
       __builtin_amdgcn_global_load_lds(ks, Ks + base, 16, 0, 0);
       __builtin_amdgcn_global_load_lds(vs, Vs + base, 16, 0, 0);
@@ -212,7 +228,7 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
 __global__ void __launch_bounds__(NT, 1) attn_fwd_f32(AttnArgs p) {
   constexpr int TILE = KT * 256;  // 64 rows x 256 B
   __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TILE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5, l32 = lane & 31;
   const int nqt = (p.seq_q + QBLK - 1) / QBLK;
   const int nblk = nqt * p.heads * p.batch;
@@ -243,8 +259,9 @@ __global__ void __launch_bounds__(NT, 1) attn_fwd_f32(AttnArgs p) {
       const int row = (i * 4 + wave) * 4 + (lane >> 4), pos = lane & 15;
       const int key = kt * KT + row;
       const int kc = pos ^ (row & 15);
-      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)key * p.kr + kc * 4) : zero;
-      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)key * p.vr + pos * 4) : zero;
+      const int pr = kv_row(p, key);
+      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)pr * p.kr + kc * 4) : zero;
+      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)pr * p.vr + pos * 4) : zero;
       const int base = (i * 4 + wave) * 64 * 16;
       __builtin_amdgcn_global_load_lds(ks, Ks + base, 16, 0, 0);
       __builtin_amdgcn_global_load_lds(vs, Vs + base, 16, 0, 0);
@@ -358,6 +375,17 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   a.qb = d->q_bstride; a.qr = d->q_rstride; a.kb = d->k_bstride; a.kr = d->k_rstride;
   a.vb = d->v_bstride; a.vr = d->v_rstride; a.ob = d->o_bstride; a.orr = d->o_rstride;
   a.batch = d->batch; a.heads = d->heads; a.seq_q = d->seq_q; a.seq_kv = d->seq_kv;
+  MAPA_CHECK_ARG(d->kv_nseg >= 0 && d->kv_nseg <= MAPA_MAX_KV_SEGMENTS, "mapa_attention: kv_nseg out of range");
+  a.nseg = d->kv_nseg;
+  int64_t tot = 0;
+  for (int s = 0; s < d->kv_nseg; ++s) {
+    a.seg_start[s] = d->kv_seg_start[s];
+    a.seg_len[s] = d->kv_seg_len[s];
+    MAPA_CHECK_ARG(d->kv_seg_len[s] >= 0 && d->kv_seg_start[s] >= 0, "mapa_attention: bad kv segment");
+    tot += d->kv_seg_len[s];
+  }
+  MAPA_CHECK_ARG(d->kv_nseg == 0 || tot == d->seq_kv, "mapa_attention: kv segments sum %lld != seq_kv %d",
+                 (long long)tot, d->seq_kv);
   const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
   if (d->dtype == MAPA_BF16)
     hipLaunchKernelGGL(attn_fwd_bf16, dim3(nblk), dim3(NT), 0, stream, a);

@@ -50,7 +50,8 @@ class AttnDesc(ctypes.Structure):
         ("o", ctypes.c_void_p), ("q_bstride", ctypes.c_int64), ("q_rstride", ctypes.c_int64),
         ("k_bstride", ctypes.c_int64), ("k_rstride", ctypes.c_int64), ("v_bstride", ctypes.c_int64),
         ("v_rstride", ctypes.c_int64), ("o_bstride", ctypes.c_int64), ("o_rstride", ctypes.c_int64),
-        ("lse", ctypes.c_void_p),
+        ("lse", ctypes.c_void_p), ("kv_nseg", ctypes.c_int), ("kv_seg_start", ctypes.c_int * 16),
+        ("kv_seg_len", ctypes.c_int * 16),
     ]
 
 
@@ -206,7 +207,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
 
 
 def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, k_bstride, k_rstride,
-              v_bstride, v_rstride, o_bstride, o_rstride, lse=None):
+              v_bstride, v_rstride, o_bstride, o_rstride, lse=None, kv_segments=None):
     """q/k/v/o are tensors whose data_ptr is the (b=0, h=0, i=0, d=0) element."""
     d = AttnDesc()
     d.dtype = dt_code(q.dtype)
@@ -217,6 +218,12 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
     d.v_bstride, d.v_rstride = v_bstride, v_rstride
     d.o_bstride, d.o_rstride = o_bstride, o_rstride
     d.lse = None if lse is None else lse.data_ptr()
+    if kv_segments:
+        if len(kv_segments) > 16:
+            raise NativeError("at most 16 K/V segments")
+        d.kv_nseg = len(kv_segments)
+        for i, (st, ln) in enumerate(kv_segments):
+            d.kv_seg_start[i], d.kv_seg_len[i] = st, ln
     tok = _tic()
     check(lib().mapa_attention(ctypes.byref(d), stream()), "mapa_attention")
     _toc(tok, "attention", 4.0 * batch * heads * seq_q * seq_kv * 64)

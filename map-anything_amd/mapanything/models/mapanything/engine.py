@@ -250,20 +250,28 @@ class MapaEngine:
         return fused_lp, (hp, wp)
 
     # ----------------------------------------------------------------------------------------------- AAT
-    def aat(self, fused_lp, VB, T, taps=None):
+    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None):
         """alternating_attention_transformer.py:530-771 (IFR [11, 17]).  Returns l11, l17, final (lp, VB*T rows)
-        and the final scale-token feature (f32, 768)."""
+        and the final scale-token feature (f32, 768).  With `shard` (parallel.ShardPlan) this rank holds only its
+        views (+ the scale-token replica) and the global layers all-gather K/V through `comm`."""
         w = self.w
         L = VB * T + 1
         y = self._empty(L, AAT_DIM, dtype=torch.float32)
         nat.gemm(fused_lp, w.pe_proj, L, AAT_DIM, ENC_DIM, bias=w.pe_proj_b, out_f32=y)
-        nat.add_rowvec(y, AAT_DIM, 0, T, AAT_DIM, w.view_pe)
+        if shard is None or shard.rank == 0:  # reference-view PE on view 0 only
+            nat.add_rowvec(y, AAT_DIM, 0, T, AAT_DIM, w.view_pe)
         yn, qkv, ao = self._empty(L, AAT_DIM), self._empty(L, 3 * AAT_DIM), self._empty(L, AAT_DIM)
         hbuf = self._empty(L, 4 * AAT_DIM)
+        if shard is not None:
+            kv_full = self._empty(shard.world * shard.max_rows, 2 * AAT_DIM)
+            q_loc = self._empty(L, AAT_DIM)
         inter = {}
         for d, p in enumerate(w.aat):
             if d % 2 == 0:   # global attention over every view + the scale token
-                self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False)
+                if shard is None:
+                    self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False)
+                else:
+                    self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm)
             else:            # frame attention inside each view; the scale token bypasses the block
                 self._block(y, yn, qkv, ao, hbuf, VB * T, AAT_DIM, AAT_HEADS, p, attn_batch=VB, attn_seq=T,
                             gamma=False)
@@ -282,6 +290,22 @@ class MapaEngine:
             taps["aat_final"] = fin_f32[:VB * T]
             taps["scale_token"] = fin_f32[VB * T]
         return inter[11], inter[17], fin_lp, fin_f32[VB * T:]
+
+    def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm):
+        """Global SelfAttentionBlock on a view shard: Q for the local rows, K/V of all ranks (one all-gather)."""
+        C = AAT_DIM
+        self._ln(y, L, C, p["n1w"], p["n1b"], y_lp=yn)
+        nat.gemm(yn, p["qkv"][:C], L, C, C, bias=p["qkv_b"][:C], out_lp=q_loc)
+        slot = kv_full[shard.rank * shard.max_rows:]
+        nat.gemm(yn, p["qkv"][C:], L, 2 * C, C, bias=p["qkv_b"][C:], out_lp=slot, ldo=2 * C)
+        comm.allgather_slots(kv_full, shard.max_rows)
+        nat.attention(q_loc, kv_full, kv_full[:, C:], ao, batch=1, heads=AAT_HEADS, seq_q=L, seq_kv=shard.total_kv,
+                      q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C, v_bstride=0, v_rstride=2 * C,
+                      o_bstride=0, o_rstride=C, kv_segments=shard.kv_segments())
+        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
+        self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)
+        nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
+        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y)
 
     # ----------------------------------------------------------------------------------------------- DPT
     def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None):
@@ -433,9 +457,10 @@ class MapaEngine:
 
     # ----------------------------------------------------------------------------------------------- run
     @torch.no_grad()
-    def run(self, imgs: torch.Tensor, taps: Optional[dict] = None) -> Dict[str, torch.Tensor]:
+    def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None) -> Dict[str, torch.Tensor]:
         """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
-        per-pixel / per-view outputs of MapAnything.forward, view-major."""
+        per-pixel / per-view outputs of MapAnything.forward, view-major.  With `shard`/`comm`, imgs are this
+        rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'."""
         if imgs.dim() != 4 or imgs.shape[1] != 3:
             raise AssertionError("images must be (V, 3, H, W)")
         VB, _, H, W = imgs.shape
@@ -445,7 +470,9 @@ class MapaEngine:
         with torch.cuda.device(self.device):
             fused_lp, (hp, wp) = self.encode(imgs, taps)
             T = hp * wp
-            l11, l17, fin_lp, tok = self.aat(fused_lp, VB, T, taps)
+            if shard is not None and (shard.counts[shard.rank] != VB or shard.tokens_per_view != T):
+                raise AssertionError("shard plan does not match the local views")
+            l11, l17, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm)
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)

@@ -79,6 +79,7 @@ class MapAnything:
         self._sd: Optional[Dict[str, np.ndarray]] = None
         self._engines: Dict[tuple, Any] = {}
         self._device = torch.device("cpu")
+        self._comm = None
         self.training = False
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)
@@ -182,10 +183,13 @@ class MapAnything:
             self._engines[key] = MapaEngine(self._sd, self._device, prec)
         return self._engines[key]
 
-    def enable_view_sharding(self, group):
-        """Shard the views over the ranks of `group` (one process per GPU); global-attention K/V all-gathered."""
-        self._shard_group = group
-        self._engines.clear()
+    def enable_view_sharding(self, group=None, comm=None):
+        """Shard the views over the ranks of `group` (one process per GPU, torch.distributed over RCCL) or of an
+        explicit communicator (parallel.ThreadComm in tests).  infer()/forward() then run only this rank's
+        views; the returned list holds this rank's views' outputs and None for the others."""
+        from ...parallel import DistComm
+
+        self._comm = comm if comm is not None else DistComm(group)
         return self
 
     # ------------------------------------------------------------------------------------------ forward
@@ -209,9 +213,10 @@ class MapAnything:
         dnt = views[0].get("data_norm_type", ["dinov2"])
         if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
-        imgs = torch.cat([v["img"] for v in views], 0).to(self._device, torch.float32)
-        raw = self.engine(precision).run(imgs)
-        return split_views(raw, len(views), with_post=False)
+        local, plan = self._local_views(views)
+        imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
+        raw = self.engine(precision).run(imgs, shard=plan, comm=self._comm)
+        return self._assemble(split_views(raw, len(local), with_post=False), plan, len(views))
 
     @torch.inference_mode()
     def infer(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False, use_amp: bool = True,
@@ -245,15 +250,34 @@ class MapAnything:
                 v.pop("camera_pose_quats", None)
                 v.pop("camera_pose_trans", None)
         self._check_image_only(processed)
-        imgs = torch.cat([v["img"] for v in processed], 0).to(self._device, torch.float32)
+        local, plan = self._local_views(processed)
+        imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
         eng = self.engine(precision)
-        raw = eng.run(imgs)
+        raw = eng.run(imgs, shard=plan, comm=self._comm)
         post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
                                    mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
                                    edge_depth_threshold=edge_depth_threshold,
                                    apply_confidence_mask=apply_confidence_mask,
                                    confidence_percentile=confidence_percentile)
-        return split_views(post, len(views), with_post=True)
+        return self._assemble(split_views(post, len(local), with_post=True), plan, len(views))
+
+    def _local_views(self, views):
+        if self._comm is None:
+            return views, None
+        from ...parallel import ShardPlan
+
+        H, W = views[0]["img"].shape[-2:]
+        plan = ShardPlan(len(views), self._comm.world, self._comm.rank, (H // 14) * (W // 14))
+        return [views[i] for i in plan.local_views], plan
+
+    @staticmethod
+    def _assemble(local_out, plan, V):
+        if plan is None:
+            return local_out
+        out = [None] * V
+        for i, v in enumerate(plan.local_views):
+            out[v] = local_out[i]
+        return out
 
     __call__ = forward
 

@@ -1,0 +1,111 @@
+"""View-sharded multi-GPU execution.
+
+One process per GPU.  The V input views are split into contiguous blocks (view 0 -> rank 0, sizes differ by at
+most one: 100 views on 8 ranks -> 13,13,13,13,12,12,12,12).  Every stage of the path is per-view except the
+12 global layers of the alternating-attention transformer (alternating_attention_transformer.py:658-661): there
+each rank computes Q for its own tokens and attends to the K/V of ALL tokens, so K/V are all-gathered once per
+global layer (RCCL over xGMI; backend "nccl" of torch.distributed IS RCCL on ROCm).  The scale token is carried
+by every rank as a bit-identical replica (identical inputs in identical order), and its K/V are contributed once,
+by rank 0.  Nothing else crosses GPUs; outputs stay on the rank that owns the view.
+
+Gathered K/V layout: [world][max_rows][2*C] with rank r's block in slot r (its valid rows first, padding after);
+the attention kernel reads the valid rows through its K/V segment table, so no compaction copy is needed.
+"""
+
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass, field
+from typing import List, Optional, Tuple
+
+import torch
+
+
+@dataclass
+class ShardPlan:
+    num_views: int
+    world: int
+    rank: int
+    tokens_per_view: int
+    counts: List[int] = field(init=False)
+    starts: List[int] = field(init=False)
+
+    def __post_init__(self):
+        V, P = self.num_views, self.world
+        if V < P:
+            raise ValueError(f"{V} views cannot be sharded over {P} ranks (need at least one view per rank)")
+        self.counts = [V // P + (1 if r < V % P else 0) for r in range(P)]
+        self.starts = [sum(self.counts[:r]) for r in range(P)]
+
+    @property
+    def local_views(self) -> range:
+        return range(self.starts[self.rank], self.starts[self.rank] + self.counts[self.rank])
+
+    def local_rows(self, r: Optional[int] = None) -> int:
+        """AAT rows held by rank r: its views' tokens + the scale-token replica."""
+        r = self.rank if r is None else r
+        return self.counts[r] * self.tokens_per_view + 1
+
+    def kv_valid_rows(self, r: int) -> int:
+        """K/V rows rank r contributes to the global set (scale token only from rank 0)."""
+        return self.counts[r] * self.tokens_per_view + (1 if r == 0 else 0)
+
+    @property
+    def max_rows(self) -> int:
+        return max(self.local_rows(r) for r in range(self.world))
+
+    @property
+    def total_kv(self) -> int:
+        return self.num_views * self.tokens_per_view + 1
+
+    def kv_segments(self) -> List[Tuple[int, int]]:
+        return [(r * self.max_rows, self.kv_valid_rows(r)) for r in range(self.world)]
+
+
+class DistComm:
+    """K/V exchange over a torch.distributed process group (RCCL on MI355X, gloo on CPU tests)."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def allgather_slots(self, full: torch.Tensor, rows_per_slot: int):
+        """full: [world * rows_per_slot, C]; this rank's slot already written in place."""
+        mine = full.narrow(0, self.rank * rows_per_slot, rows_per_slot)
+        self.dist.all_gather_into_tensor(full, mine, group=self.group)
+
+
+class ThreadComm:
+    """In-process communicator for tests: P threads (one engine each, same device) exchange slots through a
+    barrier; the exchanged bytes are identical to what all_gather_into_tensor delivers."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self._barrier = threading.Barrier(world)
+        self._bufs = [None] * world
+        self._local = threading.local()
+
+    def bind(self, rank: int):
+        self._local.rank = rank
+        return self
+
+    @property
+    def rank(self):
+        return self._local.rank
+
+    def allgather_slots(self, full: torch.Tensor, rows_per_slot: int):
+        r = self.rank
+        torch.cuda.current_stream().synchronize() if full.is_cuda else None
+        self._bufs[r] = full
+        self._barrier.wait()
+        for s in range(self.world):
+            if s != r:
+                src = self._bufs[s].narrow(0, s * rows_per_slot, rows_per_slot)
+                full.narrow(0, s * rows_per_slot, rows_per_slot).copy_(src)
+        if full.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        self._barrier.wait()
