@@ -18,7 +18,7 @@ def _views(n, h, w, seed):
     return [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]} for i in synthetic.synthetic_images(n, h, w, seed)]
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 3e-3)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 2.4e-2)])  # bf16: 3x reference bf16 yardstick
 @pytest.mark.parametrize("world,V", [(2, 3), (3, 3)])
 def test_sharded_equals_single(precision, tol, world, V):
     from mapanything.models import MapAnything
