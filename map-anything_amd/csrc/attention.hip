@@ -80,15 +80,16 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
   const int qrow = qt * QBLK + wave * 32 + l32;
   const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
 
-  // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 (exact).
+  // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 * log2(e) so the
+  // scores come out of the MFMA already in the log2 domain (one bf16 rounding of the scaled Q).
   b8 qf[4];
 #pragma unroll
   for (int kk = 0; kk < 4; ++kk) {
     const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
-    s8v sc;
+    b8 sc;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sc[j] = (short)f32_to_bf16(bf16_to_f32((bf16_t)raw[j]) * 0.125f);
-    qf[kk] = __builtin_bit_cast(b8, sc);
+    for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E));
+    qf[kk] = sc;
   }
 
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
@@ -141,24 +142,31 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
         st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], st[kb], 0, 0, 0);
       }
     }
-    // mask the tail tile, go to the log2 domain, running max
-    const bool tail = (kt + 1) * KT > p.seq_kv;
+    // mask the tail tile (scores are already in the log2 domain), running max
+    if ((kt + 1) * KT > p.seq_kv) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (key >= p.seq_kv) st[kb][r] = -INFINITY;
+        }
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float s = st[kb][r] * LOG2E;
-        if (tail) {
-          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= p.seq_kv) s = -INFINITY;
-        }
-        st[kb][r] = s;
-        mx = fmaxf(mx, s);
-      }
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb][r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float m_new = fmaxf(m_run, mx);
-    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    if (__any(m_new > m_run)) {  // rescale only when some row max moved (exact: alpha == 1 otherwise)
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      l_run *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    }
     m_run = m_new;
     float ls = 0.f;
 #pragma unroll
@@ -169,11 +177,7 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
         st[kb][r] = e;
         ls += e;
       }
-    l_run = l_run * alpha + ls;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    l_run += ls;
 
     // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T via transposed LDS reads
     b8 pf[2][2];
@@ -181,10 +185,10 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        s8v t;
+        b8 t;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = (short)f32_to_bf16(st[kb][8 * s + j]);
-        pf[kb][s] = __builtin_bit_cast(b8, t);
+        for (int j = 0; j < 8; ++j) t[j] = (__bf16)st[kb][8 * s + j];
+        pf[kb][s] = t;
       }
     const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
 #pragma unroll
