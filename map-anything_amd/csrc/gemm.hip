@@ -24,27 +24,32 @@
 //    gamma * act(acc + bias); fp32 and/or low-precision and/or ReLU'd low-precision outputs; row-major or
 //    pixel-shuffle (ConvTranspose k=s) addressing.
 //  * XCD-aware tile order (bijective remap: consecutive tiles share an XCD's L2).
+#include <stdlib.h>
+
 #include "mapa_common.h"
 
-namespace {
+namespace mapa_gemm_impl {
 
 constexpr int BM = 128, BN = 128, NTHREADS = 256;
-constexpr int ROW_BYTES = 128;                       // one LDS row of the K tile
-constexpr int TILE_BYTES = BM * ROW_BYTES;           // 16 KiB per operand per stage
-constexpr int MAIN_LDS = 2 * 2 * TILE_BYTES;         // 2 stages x (A, W)
 constexpr int EPI_LD = 68;                           // fp32 row stride of the epilogue staging tile
-constexpr int EPI_LDS = 4 * 64 * EPI_LD * 4;         // 4 waves x 64 rows
-constexpr int LDS_BYTES = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
+constexpr int EPI_LDS = 4 * 32 * EPI_LD * 4;         // 4 waves x 32 rows (the wave tile in two halves)
+
+// LDS image of one K tile: BM rows of RB bytes (RB = 128: 64 bf16 / 32 fp32 of K; RB = 64: half that).
+// 16-B chunk position = chunk ^ swz(row) (applied on the LDS-DMA source address, read with the same XOR):
+// conflict-free ds_read_b128 for the 16x16 fragment pattern at both row sizes.
+template <int RB>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (RB == 128) return row & 7;
+  else return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;  // [0, 2, 3, 1][(row >> 2) & 3]
+}
 
 struct TraitsBF16 {
   using T = bf16_t;
   static constexpr int E = 8;    // elements per 16-B chunk
-  static constexpr int BK = 64;  // K elements per tile
 };
 struct TraitsF32 {
   using T = float;
   static constexpr int E = 4;
-  static constexpr int BK = 32;
 };
 
 struct GemmArgs {
@@ -75,9 +80,10 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 
-template <typename Tr>
+template <typename Tr, int RB>
 __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int wm, int wn, int lane, int kg,
                                             f32x4 (&acc)[4][4]) {
+  constexpr int ROW_BYTES = RB;
   const int g = lane >> 4, r16 = lane & 15;
   const int chunk = kg * 4 + g;
   if constexpr (sizeof(typename Tr::T) == 2) {
@@ -86,9 +92,9 @@ __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ra = wm * 64 + i * 16 + r16;
-      a[i] = *reinterpret_cast<const b8*>(As + ra * ROW_BYTES + ((chunk ^ (ra & 7)) << 4));
+      a[i] = *reinterpret_cast<const b8*>(As + ra * ROW_BYTES + ((chunk ^ swz<RB>(ra)) << 4));
       const int rb = wn * 64 + i * 16 + r16;
-      b[i] = *reinterpret_cast<const b8*>(Bs + rb * ROW_BYTES + ((chunk ^ (rb & 7)) << 4));
+      b[i] = *reinterpret_cast<const b8*>(Bs + rb * ROW_BYTES + ((chunk ^ swz<RB>(rb)) << 4));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -99,9 +105,9 @@ __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int 
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ra = wm * 64 + i * 16 + r16;
-      a[i] = *reinterpret_cast<const f32x4*>(As + ra * ROW_BYTES + ((chunk ^ (ra & 7)) << 4));
+      a[i] = *reinterpret_cast<const f32x4*>(As + ra * ROW_BYTES + ((chunk ^ swz<RB>(ra)) << 4));
       const int rb = wn * 64 + i * 16 + r16;
-      b[i] = *reinterpret_cast<const f32x4*>(Bs + rb * ROW_BYTES + ((chunk ^ (rb & 7)) << 4));
+      b[i] = *reinterpret_cast<const f32x4*>(Bs + rb * ROW_BYTES + ((chunk ^ swz<RB>(rb)) << 4));
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s)
@@ -118,10 +124,55 @@ __device__ __forceinline__ float epi_act(float v, int act) {
   return v;
 }
 
-template <typename Tr, int AMODE>
-__global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
+// LDS-DMA of K tile kt into ring slot buf: NLD 16-B chunks of A and of W per thread (lane-linear LDS image).
+template <typename Tr, int AMODE, int RB>
+__device__ __forceinline__ void stage_tile(const GemmArgs& p, char* lds, int buf, int kt, int lds_base, bool k_exact,
+                                           const char* const* a_src, const char* const* w_src, const int* sc,
+                                           const int* cv_base, const int* cv_iy, const int* cv_ix) {
   using T = typename Tr::T;
-  constexpr int E = Tr::E, BK = Tr::BK;
+  constexpr int E = Tr::E;
+  constexpr int BK = (RB / 16) * E;
+  constexpr int NLD = BM / (4 * (1024 / RB));
+  constexpr int TILE_BYTES = BM * RB;
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  char* As = lds + buf * 2 * TILE_BYTES;
+  char* Bs = As + TILE_BYTES;
+  const int64_t koff = (int64_t)kt * BK * sizeof(T);
+#pragma unroll
+  for (int i = 0; i < NLD; ++i) {
+    const int off = lds_base + i * 4 * 1024;
+    const int kc = kt * BK + sc[i] * E;
+    const bool kin = k_exact || kc < p.K;
+    const char* src;
+    if constexpr (AMODE == 0) {
+      src = kin ? a_src[i] + koff : zero;
+    } else {
+      const int tap = kc / p.cv_C, ci = kc - tap * p.cv_C;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
+      const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+      src = ok ? reinterpret_cast<const char*>(p.A) +
+                     ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * sizeof(T)
+               : zero;
+    }
+    __builtin_amdgcn_global_load_lds(src, As + off, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(kin ? w_src[i] + koff : zero, Bs + off, 16, 0, 0);
+  }
+}
+
+// RB: LDS row bytes of a K tile (128 or 64); STAGES: LDS ring depth.  With STAGES > 2 the LDS-DMA for tile
+// t+STAGES-1 stays in flight across the barrier of tile t (counted vmcnt + raw s_barrier, no vmcnt(0) drain).
+template <typename Tr, int AMODE, int RB, int STAGES>
+__global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
+  using T = typename Tr::T;
+  constexpr int E = Tr::E;
+  constexpr int CPR = RB / 16;                     // 16-B chunks per LDS row
+  constexpr int BK = CPR * E;                      // K elements per tile
+  constexpr int RPI = 1024 / RB;                   // rows per 1-KiB wave instruction
+  constexpr int NLD = BM / (4 * RPI);              // load instructions per operand per thread
+  constexpr int TILE_BYTES = BM * RB;
+  constexpr int MAIN_LDS = STAGES * 2 * TILE_BYTES;
+  constexpr int LDS_BYTES = MAIN_LDS > EPI_LDS ? MAIN_LDS : EPI_LDS;
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -131,19 +182,21 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
   const int tile = xcd_remap(blockIdx.x, ntm * ntn);
   const int bm = (tile / ntn) * BM, bn = (tile % ntn) * BN;
 
-  // ---- per-thread staging geometry: 4 rows (one per load instruction), one fixed source chunk ----------
-  const int sc = (lane & 7) ^ (lane >> 3);  // source chunk (pre-swizzled)
+  // ---- per-thread staging geometry: NLD rows (one per load instruction), one fixed source chunk ---------
+  const int lrow = lane / CPR, pos = lane % CPR;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
-  const char* a_src[4];
-  const char* w_src[4];
-  int cv_base[4], cv_iy[4], cv_ix[4];
+  const char* a_src[NLD];
+  const char* w_src[NLD];
+  int sc[NLD];
+  int cv_base[NLD], cv_iy[NLD], cv_ix[NLD];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (i * 4 + wave) * 8 + (lane >> 3);
+  for (int i = 0; i < NLD; ++i) {
+    const int r = (i * 4 + wave) * RPI + lrow;
+    sc[i] = pos ^ swz<RB>(r);  // pre-swizzled source chunk
     const int m = min(bm + r, p.M - 1), n = min(bn + r, p.N - 1);
-    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + sc * E) * sizeof(T);
+    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + sc[i] * E) * sizeof(T);
     if constexpr (AMODE == 0) {
-      a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + sc * E) * sizeof(T);
+      a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + sc[i] * E) * sizeof(T);
     } else {
       const int hw = p.cv_OH * p.cv_OW;
       const int img = m / hw, rem = m - img * hw;
@@ -155,37 +208,8 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
   }
   const int nk = (p.K + BK - 1) / BK;
   const bool k_exact = (p.K % BK) == 0;
-  const int lds_base = wave * 64 * 16;
+  const int lds_base = wave * 1024;
 
-  auto stage = [&](int buf, int kt) {
-    char* As = lds + buf * 2 * TILE_BYTES;
-    char* Bs = As + TILE_BYTES;
-    const int kc = kt * BK + sc * E;
-    const bool kin = k_exact || kc < p.K;
-    const int64_t koff = (int64_t)kt * BK * sizeof(T);
-    int tap = 0, ci = 0;
-    if constexpr (AMODE == 1) {
-      tap = kc / p.cv_C;
-      ci = kc - tap * p.cv_C;
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int off = lds_base + i * 4 * 64 * 16;
-      const char* src;
-      if constexpr (AMODE == 0) {
-        src = kin ? a_src[i] + koff : zero;
-      } else {
-        const int ky = tap / 3, kx = tap - ky * 3;
-        const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
-        const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-        src = ok ? reinterpret_cast<const char*>(p.A) +
-                       ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * sizeof(T)
-                 : zero;
-      }
-      __builtin_amdgcn_global_load_lds(src, As + off, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(kin ? w_src[i] + koff : zero, Bs + off, 16, 0, 0);
-    }
-  };
 
   f32x4 acc[4][4];
 #pragma unroll
@@ -193,33 +217,47 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, kt + 1);
-    const char* As = lds + cur * 2 * TILE_BYTES;
-    const char* Bs = As + TILE_BYTES;
-    mfma_kgroup<Tr>(As, Bs, wm, wn, lane, 0, acc);
-    mfma_kgroup<Tr>(As, Bs, wm, wn, lane, 1, acc);
+  if constexpr (STAGES == 2) {
+    stage_tile<Tr, AMODE, RB>(p, lds, 0, 0, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) stage_tile<Tr, AMODE, RB>(p, lds, cur ^ 1, kt + 1, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+      const char* As = lds + cur * 2 * TILE_BYTES;
+      const char* Bs = As + TILE_BYTES;
+#pragma unroll
+      for (int kg = 0; kg < CPR / 4; ++kg) mfma_kgroup<Tr, RB>(As, Bs, wm, wn, lane, kg, acc);
+      __syncthreads();
+    }
+  } else {
+    // prologue: tiles 0 .. STAGES-2 in flight
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+      if (s0 < nk) stage_tile<Tr, AMODE, RB>(p, lds, s0, s0, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+    for (int kt = 0; kt < nk; ++kt) {
+      // tile kt landed (this thread's DMAs): later tiles may stay in flight
+      if (kt + STAGES - 2 < nk) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NLD * (STAGES - 2)) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's DMA for tile kt landed; every wave done with tile kt-1
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + STAGES - 1 < nk) stage_tile<Tr, AMODE, RB>(p, lds, (kt + STAGES - 1) % STAGES, kt + STAGES - 1, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+      const char* As = lds + (kt % STAGES) * 2 * TILE_BYTES;
+      const char* Bs = As + TILE_BYTES;
+#pragma unroll
+      for (int kg = 0; kg < CPR / 4; ++kg) mfma_kgroup<Tr, RB>(As, Bs, wm, wn, lane, kg, acc);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
 
-  // ---- epilogue: accumulators -> LDS (per-wave 64 x 64 fp32 tile) -> 16-B row segments -----------------
-  float* ep = reinterpret_cast<float*>(lds) + wave * 64 * EPI_LD;
-  {
-    const int g = lane >> 4, c16 = lane & 15;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * EPI_LD + j * 16 + c16] = acc[i][j][r];
-  }
-  __syncthreads();
+  // ---- epilogue: accumulators -> LDS (per-wave 32 x 64 fp32 half tile) -> 16-B row segments ------------
+  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * EPI_LD;
   const int c4 = (lane & 15) * 4;
   const int n0 = bn + wn * 64 + c4;
-  if (n0 >= p.N) return;
   float bv[4], gv[4];
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -236,72 +274,104 @@ __global__ void __launch_bounds__(NTHREADS, 2) gemm_kernel(GemmArgs p) {
     col_off = co;
   }
   const bool vec = p.vec_ok && (n0 + 3 < p.N);
-#pragma unroll 4
-  for (int pass = 0; pass < 16; ++pass) {
-    const int rloc = pass * 4 + (lane >> 4);
-    const int m = bm + wm * 64 + rloc;
-    if (m >= p.M) break;
-    const f32x4 a = *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c4);
-    int64_t off;
-    if (p.out_mode == 0) {
-      off = (int64_t)m * p.ldo + col_off;
-    } else {
-      const int hw = p.ps_h * p.ps_w;
-      const int img = m / hw, rem = m - img * hw;
-      const int y = rem / p.ps_w, x = rem - y * p.ps_w;
-      const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
-      off = (((int64_t)img * H2 + y * p.ps_s + ps_ky) * W2 + x * p.ps_s + ps_kx) * p.ps_cout + col_off;
-    }
-    f32x4 v;
+  const int g = lane >> 4, c16 = lane & 15;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + bv[e], p.act) * gv[e];
-    if (vec) {
-      if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
-      if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
-      if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
-      if constexpr (sizeof(T) == 2) {
-        if (p.out_lp) {
-          uint2 u;
-          u.x = pack_bf16x2(v[0], v[1]);
-          u.y = pack_bf16x2(v[2], v[3]);
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
-        }
-        if (p.out_lp_relu) {
-          uint2 u;
-          u.x = pack_bf16x2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
-          u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
-          *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
-        }
-      } else {
-        if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
-        if (p.out_lp_relu) {
-          f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
-          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off) = rr;
-        }
-      }
-    } else {
-      // scalar tail (N % 4 != 0 or the last partial column group); row-major only
+  for (int half = 0; half < 2; ++half) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (n0 + e >= p.N) break;
-        const int64_t o = off + e;
-        float x = v[e];
-        if (p.resid1) x += p.resid1[o];
-        if (p.resid2) x += p.resid2[o];
-        if (p.out_f32) p.out_f32[o] = x;
-        if constexpr (sizeof(T) == 2) {
-          if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
-          if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * EPI_LD + j * 16 + c16] = acc[half * 2 + i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (n0 < p.N) {
+#pragma unroll 2
+      for (int pass = 0; pass < 8; ++pass) {
+        const int rloc = pass * 4 + (lane >> 4);
+        const int m = bm + wm * 64 + half * 32 + rloc;
+        if (m >= p.M) break;
+        const f32x4 a = *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c4);
+        int64_t off;
+        if (p.out_mode == 0) {
+          off = (int64_t)m * p.ldo + col_off;
         } else {
-          if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
-          if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);
+          const int hw = p.ps_h * p.ps_w;
+          const int img = m / hw, rem = m - img * hw;
+          const int y = rem / p.ps_w, x = rem - y * p.ps_w;
+          const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
+          off = (((int64_t)img * H2 + y * p.ps_s + ps_ky) * W2 + x * p.ps_s + ps_kx) * p.ps_cout + col_off;
+        }
+        f32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + bv[e], p.act) * gv[e];
+        if (vec) {
+          if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
+          if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
+          if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
+          if constexpr (sizeof(T) == 2) {
+            if (p.out_lp) {
+              uint2 u;
+              u.x = pack_bf16x2(v[0], v[1]);
+              u.y = pack_bf16x2(v[2], v[3]);
+              *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
+            }
+            if (p.out_lp_relu) {
+              uint2 u;
+              u.x = pack_bf16x2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
+              u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+              *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
+            }
+          } else {
+            if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
+            if (p.out_lp_relu) {
+              f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+              *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off) = rr;
+            }
+          }
+        } else {
+          // scalar tail (N % 4 != 0 or the last partial column group); row-major only
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (n0 + e >= p.N) break;
+            const int64_t o = off + e;
+            float x = v[e];
+            if (p.resid1) x += p.resid1[o];
+            if (p.resid2) x += p.resid2[o];
+            if (p.out_f32) p.out_f32[o] = x;
+            if constexpr (sizeof(T) == 2) {
+              if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
+              if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
+            } else {
+              if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
+              if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);
+            }
+          }
         }
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
-}  // namespace
+// variant = RB * 10 + STAGES (runtime-selectable for tuning: MAPA_GEMM_VARIANT)
+template <typename Tr, int AMODE>
+void launch_variant(int variant, int nblk, hipStream_t stream, const GemmArgs& a) {
+  void (*k)(GemmArgs);
+  switch (variant) {
+    case 643: k = gemm_kernel<Tr, AMODE, 64, 3>; break;
+    case 644: k = gemm_kernel<Tr, AMODE, 64, 4>; break;
+    case 1283: k = gemm_kernel<Tr, AMODE, 128, 3>; break;
+    default: k = gemm_kernel<Tr, AMODE, 128, 2>; break;
+  }
+  hipLaunchKernelGGL(k, dim3(nblk), dim3(NTHREADS), 0, stream, a);
+}
+
+}  // namespace mapa_gemm_impl
+using namespace mapa_gemm_impl;
 
 extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d != nullptr, "mapa_gemm: null descriptor");
@@ -346,12 +416,20 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(a.vec_ok || d->out_mode == MAPA_OUT_ROWMAJOR, "mapa_gemm: pixel shuffle needs N %% 4 == 0");
   const int nblk = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const bool conv = d->a_mode == MAPA_A_CONV3X3;
+  // Tile-pipeline variant (RB*10 + STAGES).  Measured on MI355X (tools/kbench.py): 64-B rows x 3 stages (occupancy
+  // 3) wins for the implicit convs and K < 1024; 128-B rows x 2 stages for the K >= 1024 linears.
+  static int forced = -1;
+  if (forced < 0) {
+    const char* ev = getenv("MAPA_GEMM_VARIANT");
+    forced = ev ? atoi(ev) : 0;
+  }
+  const int variant = forced ? forced : ((conv || d->K < 1024) ? 643 : 1282);
   if (d->dtype == MAPA_BF16) {
-    if (conv) hipLaunchKernelGGL((gemm_kernel<TraitsBF16, 1>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
-    else hipLaunchKernelGGL((gemm_kernel<TraitsBF16, 0>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
+    if (conv) launch_variant<TraitsBF16, 1>(variant, nblk, stream, a);
+    else launch_variant<TraitsBF16, 0>(variant, nblk, stream, a);
   } else {
-    if (conv) hipLaunchKernelGGL((gemm_kernel<TraitsF32, 1>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
-    else hipLaunchKernelGGL((gemm_kernel<TraitsF32, 0>), dim3(nblk), dim3(NTHREADS), 0, stream, a);
+    if (conv) launch_variant<TraitsF32, 1>(variant, nblk, stream, a);
+    else launch_variant<TraitsF32, 0>(variant, nblk, stream, a);
   }
   MAPA_CHECK_LAUNCH("mapa_gemm");
   return 0;
