@@ -25,7 +25,7 @@ typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
 enum { MAPA_F32 = 0, MAPA_BF16 = 1 };
 enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
 enum { MAPA_OUT_ROWMAJOR = 0, MAPA_OUT_PIXSHUF = 1 };
-enum { MAPA_ACT_NONE = 0, MAPA_ACT_GELU = 1, MAPA_ACT_RELU = 2 };
+enum { MAPA_ACT_NONE = 0, MAPA_ACT_GELU = 1, MAPA_ACT_RELU = 2, MAPA_ACT_GELU_POST = 3 };
 
 const char* mapa_last_error(void);
 int mapa_version(void);
@@ -35,6 +35,8 @@ int mapa_device_check(int device);
 /* ---------------------------------------------------------------------------------------------------------
  * GEMM / implicit-GEMM convolution: C[M,N] = A[M,K] * W[N,K]^T, fused epilogue
  *   v = acc + bias[n % bias_mod]; v = act(v); v *= gamma[n]; v += resid1[o] + resid2[o];
+ *   (act MAPA_ACT_GELU_POST: v = gelu(acc + bias + resid1 + resid2), gamma must be NULL — ResidualBlock,
+ *   dense_rep_encoder.py:44-52)
  *   out_f32[o] = v; out_lp[o] = lowp(v); out_lp_relu[o] = lowp(max(v,0))
  * Replaces nn.Linear (transformer_blocks.py:65-212, dinov2 layers/block.py:93-118, mlp_head.py, pose_head.py),
  * nn.Conv2d 1x1/3x3 (dpt.py:94-311, dpt_block.py:114-177, pose_head.py:18-48, dense_rep_encoder.py:31-287),
@@ -165,6 +167,34 @@ int mapa_convert_rows(const float* src, int64_t lds, int rows, int cols, void* d
 /* Deterministic synthetic weights on device: out[i] = (2*u_i - 1)*half + mid, u_i = splitmix64 stream of
  * `seed` (bit-identical to mapanything/utils/synthetic.py). */
 int mapa_fill_splitmix(float* out, int64_t n, uint64_t seed, float half, float mid, mapa_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Optional geometric inputs (model.py:792-1289; dense_rep_encoder.py:234-287; global_rep_encoder.py:85-104).
+ * The encoders' convolutions / linears run through mapa_gemm (fp32, as the reference's autocast-disabled block).
+ * ------------------------------------------------------------------------------------------------------- */
+/* nn.PixelUnshuffle(r) from NHWC f32 [n][H][W][C] to token rows out[(v*h+py)*w+px][c*r*r+i*r+j] (ldo), f32/bf16.
+ * lognorm != 0 applies the depth-encoder input transform first: x /= view_div[v]; x = x/max(|x|,1e-8)*log1p(|x|)
+ * (normalize_depth_using_non_zero_pixels + apply_log_to_norm, geometry.py:1594-1626, 1737-1750). */
+int mapa_pixel_unshuffle(const float* in, int n, int H, int W, int C, int r, const float* view_div, int lognorm,
+                         void* out, int out_dtype, int64_t ldo, mapa_stream_t stream);
+
+/* Per view: nf = clip(sum(d[d>0]) / (count(d>0) + 1e-8), 1e-8); log_nf (optional) = log(nf + 1e-8).
+ * depth [n][HW] f32; work: n*128 floats of scratch (deterministic two-pass reduction). */
+int mapa_depth_norm_factors(const float* depth, int n, int HW, float* nf, float* log_nf, void* work,
+                            mapa_stream_t stream);
+
+/* Camera inputs of all V views in view 0's frame (model.py:792-896, geometry.py:745-852), identity where
+ * cam_mask[v] == 0, translations normalised by their mean non-zero norm (geometry.py:1629-1666).
+ * quats [V][4] (x,y,z,w), trans [V][3] -> out_q [V][4], out_t [V][3], out_log_nf [V] = log(nf + 1e-8). */
+int mapa_pose_inputs(const float* quats, const float* trans, const uint8_t* cam_mask, int V, float* out_q,
+                     float* out_t, float* out_log_nf, mapa_stream_t stream);
+
+/* x[v*T+t][c] += sum_j scales[j*nviews+v] * vecs[(j*nviews+v)*C + c]  (per-view global features, C % 4 == 0) */
+int mapa_add_view_vectors(float* x, int T, int C, int nviews, const float* vecs, const float* scales, int nvec,
+                          mapa_stream_t stream);
+
+/* dst[i] += src[i] (n % 4 == 0) */
+int mapa_add_f32(float* dst, const float* src, int64_t n, mapa_stream_t stream);
 
 #ifdef __cplusplus
 }

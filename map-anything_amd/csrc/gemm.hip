@@ -309,6 +309,10 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
         if (vec) {
           if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
           if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
+          if (p.act == MAPA_ACT_GELU_POST) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+          }
           if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
           if constexpr (sizeof(T) == 2) {
             if (p.out_lp) {
@@ -339,6 +343,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
             float x = v[e];
             if (p.resid1) x += p.resid1[o];
             if (p.resid2) x += p.resid2[o];
+            if (p.act == MAPA_ACT_GELU_POST) x = gelu_erf(x);
             if (p.out_f32) p.out_f32[o] = x;
             if constexpr (sizeof(T) == 2) {
               if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
@@ -381,6 +386,8 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d->K % E == 0, "mapa_gemm: K=%d must be a multiple of %d", d->K, E);
   MAPA_CHECK_ARG(d->A && d->W, "mapa_gemm: null operand");
   MAPA_CHECK_ARG(d->out_f32 || d->out_lp || d->out_lp_relu, "mapa_gemm: no output");
+  MAPA_CHECK_ARG(d->act >= MAPA_ACT_NONE && d->act <= MAPA_ACT_GELU_POST, "mapa_gemm: bad act %d", d->act);
+  MAPA_CHECK_ARG(d->act != MAPA_ACT_GELU_POST || !d->gamma, "mapa_gemm: GELU_POST takes no gamma");
   if (d->a_mode == MAPA_A_CONV3X3) {
     MAPA_CHECK_ARG(d->conv_C % E == 0 && d->K == 9 * d->conv_C, "mapa_gemm: conv K=%d must be 9*C (C=%d, C%%%d==0)",
                    d->K, d->conv_C, E);

@@ -18,7 +18,7 @@ _lib = None
 F32, BF16 = 0, 1
 A_DENSE, A_CONV3X3 = 0, 1
 OUT_ROWMAJOR, OUT_PIXSHUF = 0, 1
-ACT_NONE, ACT_GELU, ACT_RELU = 0, 1, 2
+ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_POST = 0, 1, 2, 3
 
 # Every extern "C" symbol declared in include/mapa.h (checked by tests/test_capi.py).
 EXPORTED = (
@@ -26,6 +26,7 @@ EXPORTED = (
     "mapa_patchify", "mapa_assemble_tokens", "mapa_add_rowvec", "mapa_bilinear_ac", "mapa_mean_tokens",
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
+    "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
 )
 
 
@@ -93,6 +94,11 @@ def load_library(path: Optional[str] = None):
     L.mapa_postprocess_mask.argtypes = [vp, vp, vp, vp, i, i, i, f, f, i, vp, vp]
     L.mapa_recover_intrinsics.argtypes = [vp, i, i, i, vp, vp]
     L.mapa_denorm_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
+    L.mapa_pixel_unshuffle.argtypes = [vp, i, i, i, i, i, vp, i, vp, i, i64, vp]
+    L.mapa_depth_norm_factors.argtypes = [vp, i, i, vp, vp, vp, vp]
+    L.mapa_pose_inputs.argtypes = [vp, vp, vp, i, vp, vp, vp, vp]
+    L.mapa_add_view_vectors.argtypes = [vp, i, i, i, vp, vp, i, vp]
+    L.mapa_add_f32.argtypes = [vp, vp, i64, vp]
     _lib = L
     return L
 
@@ -299,3 +305,30 @@ def recover_intrinsics(rays, n, H, W, K):
 
 def denorm_image(img, n, H, W, mean, std, out):
     check(lib().mapa_denorm_image(ptr(img), n, H, W, ptr(mean), ptr(std), ptr(out), stream()), "mapa_denorm_image")
+
+
+def pixel_unshuffle(inp, n, H, W, C, r, out, *, ldo=None, view_div=None):
+    """NHWC f32 [n][H][W][C] -> token rows [n*(H/r)*(W/r)][C*r*r]; view_div given: depth log-normalisation."""
+    check(lib().mapa_pixel_unshuffle(ptr(inp), n, H, W, C, r, ptr(view_div), 1 if view_div is not None else 0,
+                                     ptr(out), dt_code(out.dtype), ldo if ldo is not None else C * r * r,
+                                     stream()), "mapa_pixel_unshuffle")
+
+
+def depth_norm_factors(depth, n, HW, nf, log_nf=None):
+    work = torch.empty(n * 128, device=depth.device, dtype=torch.float32)
+    check(lib().mapa_depth_norm_factors(ptr(depth), n, HW, ptr(nf), ptr(log_nf), ptr(work), stream()),
+          "mapa_depth_norm_factors")
+
+
+def pose_inputs(quats, trans, cam_mask, V, out_q, out_t, out_log_nf):
+    check(lib().mapa_pose_inputs(ptr(quats), ptr(trans), ptr(cam_mask), V, ptr(out_q), ptr(out_t), ptr(out_log_nf),
+                                 stream()), "mapa_pose_inputs")
+
+
+def add_view_vectors(x, T, C, nviews, vecs, scales, nvec):
+    check(lib().mapa_add_view_vectors(ptr(x), T, C, nviews, ptr(vecs), ptr(scales), nvec, stream()),
+          "mapa_add_view_vectors")
+
+
+def add_f32(dst, src, n):
+    check(lib().mapa_add_f32(ptr(dst), ptr(src), n, stream()), "mapa_add_f32")

@@ -19,6 +19,7 @@ reference to ~1e-5).
 from __future__ import annotations
 
 import math
+from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -39,6 +40,27 @@ def _np(x):
     if isinstance(x, torch.Tensor):
         return x.detach().float().cpu().numpy()
     return np.asarray(x, dtype=np.float32)
+
+
+@dataclass
+class GeoInputs:
+    """Optional geometric inputs of this rank's views, prepared by MapAnything (model.py:1292-1438 with the
+    deterministic masks of infer(), model.py:2154-2197).  Dense inputs hold every local view (zeros where the
+    view has no such input, as the reference builds them); the *_views lists are the views whose mask is set.
+    Camera arrays cover ALL views (translation normalisation is across views), local views start at local_start."""
+    rays: Optional[torch.Tensor] = None          # (n_local, H, W, 3) f32
+    ray_views: List[int] = field(default_factory=list)
+    depth: Optional[torch.Tensor] = None         # (n_local, H, W) f32 depth along ray
+    depth_views: List[int] = field(default_factory=list)
+    depth_metric: List[bool] = field(default_factory=list)   # per local view (is_metric_scale & use_depth_scale)
+    cam_quats: Optional[torch.Tensor] = None     # (V, 4) f32, (x, y, z, w)
+    cam_trans: Optional[torch.Tensor] = None     # (V, 3) f32
+    cam_mask: List[bool] = field(default_factory=list)       # (V,)
+    pose_metric: List[bool] = field(default_factory=list)    # (V,) is_metric_scale & use_pose_scale
+    local_start: int = 0
+
+    def empty(self) -> bool:
+        return not self.ray_views and not self.depth_views and not any(self.cam_mask)
 
 
 class PackedWeights:
@@ -143,10 +165,45 @@ class PackedWeights:
                           for n in ("proj", "mlp.0.0", "mlp.1.0", "output_proj")]
         self.norm_mean = torch.tensor(DINOV2_MEAN, device=dev)
         self.norm_std = torch.tensor(DINOV2_STD, device=dev)
-        self.sd = None  # host copy no longer needed
+        self._geo = None
 
     def _get(self, name):
         return self.sd[name]
+
+    def geometric(self, sd: Dict[str, object]) -> Dict[str, object]:
+        """fp32 kernel-layout weights of the dense (ray, depth) and global (depth-scale, camera) encoders, packed on
+        first use (the reference runs them with autocast disabled, model.py:1377)."""
+        if getattr(self, "_geo", None) is not None:
+            return self._geo
+        dev = self.device
+
+        def t(name):
+            return torch.from_numpy(np.ascontiguousarray(_np(sd[name]))).to(dev)
+
+        def c3(name):
+            w = _np(sd[f"{name}.weight"])
+            return torch.from_numpy(np.ascontiguousarray(w.transpose(0, 2, 3, 1).reshape(w.shape[0], -1))).to(dev)
+
+        def l1(name):
+            w = _np(sd[f"{name}.weight"])
+            return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev)
+
+        geo = {}
+        for enc in ("ray_dirs_encoder", "depth_encoder"):
+            d = dict(conv_in=c3(f"{enc}.conv_in"), conv_in_b=t(f"{enc}.conv_in.bias"), blocks=[],
+                     out=l1(f"{enc}.encoder.2"), out_b=t(f"{enc}.encoder.2.bias"),
+                     nw=t(f"{enc}.norm_layer.weight"), nb=t(f"{enc}.norm_layer.bias"))
+            for i in range(2):
+                n = f"{enc}.encoder.{i}"
+                d["blocks"].append(dict(c1=c3(f"{n}.conv1"), b1=t(f"{n}.conv1.bias"), c2=c3(f"{n}.conv2"),
+                                        b2=t(f"{n}.conv2.bias"), sc=l1(f"{n}.shortcut"), sc_b=t(f"{n}.shortcut.bias")))
+            geo[enc] = d
+        for enc in ("depth_scale_encoder", "cam_rot_encoder", "cam_trans_encoder", "cam_trans_scale_encoder"):
+            names = ("encoder.0.0.0.0", "encoder.0.0.1", "encoder.0.1", "encoder.1")
+            geo[enc] = dict(lin=[(t(f"{enc}.{n}.weight"), t(f"{enc}.{n}.bias")) for n in names],
+                            nw=t(f"{enc}.norm_layer.weight"), nb=t(f"{enc}.norm_layer.bias"))
+        self._geo = geo
+        return geo
 
     def pos_embed(self, H: int, W: int) -> torch.Tensor:
         """DINOv2 positional embedding for an (H, W) input (vision_transformer.py:208-242).  At 518x518 it is the
@@ -177,6 +234,7 @@ class MapaEngine:
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.precision = precision
         self.lp = torch.bfloat16 if precision == "bf16" else torch.float32
+        self._sd = sd  # host state dict: the geometric encoders are packed on first use
         with torch.cuda.device(self.device):
             self.w = PackedWeights(sd, self.device, self.lp)
 
@@ -217,9 +275,9 @@ class MapaEngine:
                  resid1=x, out_f32=x)
 
     # ------------------------------------------------------------------------------------------- encoder
-    def encode(self, imgs, taps=None):
-        """DINOv2 ViT-L/14 + final norm + fusion LayerNorm (image-only).  Returns fused_lp [VB*T+1][1024]
-        (last row reserved for the scale token) and fused f32 if taps is not None."""
+    def encode(self, imgs, taps=None, geo: Optional[GeoInputs] = None):
+        """DINOv2 ViT-L/14 + final norm [+ geometric-input features] + fusion LayerNorm.  Returns fused_lp
+        [VB*T+1][1024] (last row reserved for the scale token) and fused f32 if taps is not None."""
         w = self.w
         VB, _, H, W = imgs.shape
         hp, wp = H // PATCH, W // PATCH
@@ -240,14 +298,129 @@ class MapaEngine:
         enc = self._empty(VB * T, ENC_DIM, dtype=torch.float32)
         self._ln(x, VB * T, ENC_DIM, w.enc_nw, w.enc_nb, y_f32=enc, group=T, gstride=T + 1, off=1)
         del x
+        if taps is not None:
+            taps["encoder"] = enc.clone()
+        if geo is not None and not geo.empty():
+            self.geometric(enc, geo, VB, H, W)
         fused_lp = self._empty(VB * T + 1, ENC_DIM)
         fused_f32 = self._empty(VB * T, ENC_DIM, dtype=torch.float32) if taps is not None else None
         self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
         nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
         if taps is not None:
-            taps["encoder"] = enc
             taps["fused"] = fused_f32
         return fused_lp, (hp, wp)
+
+    # ------------------------------------------------------------------------------ geometric inputs
+    def geometric(self, enc, geo: GeoInputs, VB, H, W):
+        """enc [VB*T][1024] f32 += ray / depth dense features and the per-view global features, in the reference's
+        order (model.py:1392-1420): rays, depth (+ depth scale), camera rotation, translation, translation scale.
+        fp32 kernels throughout (autocast disabled in the reference, model.py:1377)."""
+        g = self.w.geometric(self._sd)
+        T = (H // PATCH) * (W // PATCH)
+        f32 = torch.float32
+        dev = self.device
+        if geo.ray_views:
+            self._dense_into(enc, geo.rays, geo.ray_views, VB, H, W, 3, g["ray_dirs_encoder"])
+        vecs, scales = [], []
+        if geo.depth_views:
+            nf = self._empty(VB, dtype=f32)
+            log_nf = self._empty(VB, dtype=f32)
+            nat.depth_norm_factors(geo.depth, VB, H * W, nf, log_nf)
+            self._dense_into(enc, geo.depth, geo.depth_views, VB, H, W, 1, g["depth_encoder"], view_div=nf)
+            sel = set(geo.depth_views)
+            sc = [1.0 if (v in sel and geo.depth_metric[v]) else 0.0 for v in range(VB)]
+            if any(sc):
+                vecs.append(self._global_rep(log_nf.view(VB, 1), VB, 1, g["depth_scale_encoder"]))
+                scales.append(sc)
+        if any(geo.cam_mask):
+            V = len(geo.cam_mask)
+            mask = torch.tensor([1 if m else 0 for m in geo.cam_mask], dtype=torch.uint8).to(dev, non_blocking=True)
+            q = self._empty(V, 4, dtype=f32)
+            t = self._empty(V, 3, dtype=f32)
+            lnf = self._empty(V, dtype=f32)
+            nat.pose_inputs(geo.cam_quats.contiguous(), geo.cam_trans.contiguous(), mask, V, q, t, lnf)
+            s0 = geo.local_start
+            cm = [1.0 if geo.cam_mask[s0 + v] else 0.0 for v in range(VB)]
+            pm = [cm[v] if geo.pose_metric[s0 + v] else 0.0 for v in range(VB)]
+            vecs.append(self._global_rep(q[s0:s0 + VB], VB, 4, g["cam_rot_encoder"]))
+            scales.append(cm)
+            vecs.append(self._global_rep(t[s0:s0 + VB], VB, 3, g["cam_trans_encoder"]))
+            scales.append(cm)
+            if any(pm):
+                vecs.append(self._global_rep(lnf[s0:s0 + VB].view(VB, 1), VB, 1, g["cam_trans_scale_encoder"]))
+                scales.append(pm)
+        if vecs:
+            vb = torch.stack(vecs, 0).contiguous()
+            sb = torch.tensor(scales, dtype=f32).to(dev, non_blocking=True)
+            nat.add_view_vectors(enc, T, ENC_DIM, VB, vb, sb, len(vecs))
+
+    def _dense_into(self, enc, data, views, VB, H, W, C, g, view_div=None):
+        """DenseRepresentationEncoder (dense_rep_encoder.py:234-287, apply_pe=False) on the selected local views,
+        added into their encoder rows (features * mask, model.py:960-968 / 1136-1140)."""
+        hp, wp = H // PATCH, W // PATCH
+        T = hp * wp
+        n = len(views)
+        if n != VB:
+            idx = torch.tensor(views, dtype=torch.long).to(self.device, non_blocking=True)
+            data = data.index_select(0, idx)
+            if view_div is not None:
+                view_div = view_div.index_select(0, idx)
+        data = data.contiguous()
+        f = self._dense_rep(data, n, H, W, C, g, view_div)
+        runs = []
+        for i, v in enumerate(views):
+            if runs and runs[-1][1] + runs[-1][2] == v:
+                runs[-1][2] += 1
+            else:
+                runs.append([i, v, 1])
+        for i, v, k in runs:
+            nat.add_f32(enc[v * T:(v + k) * T], f[i * T:(i + k) * T], k * T * ENC_DIM)
+
+    def _dense_rep(self, data, n, H, W, C, g, view_div=None):
+        f32 = torch.float32
+        hp, wp = H // PATCH, W // PATCH
+        M = n * hp * wp
+        cin = C * PATCH * PATCH
+        u = self._empty(M, cin, dtype=f32)
+        nat.pixel_unshuffle(data, n, H, W, C, PATCH, u, view_div=view_div)
+        c0 = g["conv_in"].shape[0]
+        x = self._empty(M, c0, dtype=f32)
+        nat.gemm(u, g["conv_in"], M, c0, 9 * cin, bias=g["conv_in_b"], out_f32=x, conv=(cin, hp, wp, hp, wp, 1))
+        del u
+        cin = c0
+        for blk in g["blocks"]:
+            co = blk["c1"].shape[0]
+            idt = self._empty(M, co, dtype=f32)
+            nat.gemm(x, blk["sc"], M, co, cin, bias=blk["sc_b"], out_f32=idt)
+            o = self._empty(M, co, dtype=f32)
+            nat.gemm(x, blk["c1"], M, co, 9 * cin, bias=blk["b1"], act=nat.ACT_GELU, out_f32=o,
+                     conv=(cin, hp, wp, hp, wp, 1))
+            x = self._empty(M, co, dtype=f32)
+            nat.gemm(o, blk["c2"], M, co, 9 * co, bias=blk["b2"], resid1=idt, act=nat.ACT_GELU_POST, out_f32=x,
+                     conv=(co, hp, wp, hp, wp, 1))
+            del idt, o
+            cin = co
+        y = self._empty(M, ENC_DIM, dtype=f32)
+        nat.gemm(x, g["out"], M, ENC_DIM, cin, bias=g["out_b"], out_f32=y)
+        del x
+        f = self._empty(M, ENC_DIM, dtype=f32)
+        nat.layernorm(y, M, ENC_DIM, g["nw"], g["nb"], eps=LN_EPS, y_f32=f)
+        return f
+
+    def _global_rep(self, inp, m, cin, g):
+        """GlobalRepresentationEncoder (global_rep_encoder.py:85-104): 3x (Linear + GELU), Linear, LayerNorm."""
+        f32 = torch.float32
+        inp = inp.contiguous()
+        h = inp
+        k = cin
+        for i, (w_, b_) in enumerate(g["lin"]):
+            n_out = w_.shape[0]
+            o = self._empty(m, n_out, dtype=f32)
+            nat.linear_small(h, m, k, w_, b_, n_out, nat.ACT_GELU if i < 3 else nat.ACT_NONE, o)
+            h, k = o, n_out
+        y = self._empty(m, ENC_DIM, dtype=f32)
+        nat.layernorm(h, m, ENC_DIM, g["nw"], g["nb"], eps=LN_EPS, y_f32=y)
+        return y
 
     # ----------------------------------------------------------------------------------------------- AAT
     def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None):
@@ -457,10 +630,12 @@ class MapaEngine:
 
     # ----------------------------------------------------------------------------------------------- run
     @torch.no_grad()
-    def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None) -> Dict[str, torch.Tensor]:
+    def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None,
+            geo: Optional[GeoInputs] = None) -> Dict[str, torch.Tensor]:
         """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
         per-pixel / per-view outputs of MapAnything.forward, view-major.  With `shard`/`comm`, imgs are this
-        rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'."""
+        rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'.  `geo` carries the
+        optional geometric inputs of these views (GeoInputs)."""
         if imgs.dim() != 4 or imgs.shape[1] != 3:
             raise AssertionError("images must be (V, 3, H, W)")
         VB, _, H, W = imgs.shape
@@ -468,7 +643,7 @@ class MapaEngine:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
         with torch.cuda.device(self.device):
-            fused_lp, (hp, wp) = self.encode(imgs, taps)
+            fused_lp, (hp, wp) = self.encode(imgs, taps, geo)
             T = hp * wp
             if shard is not None and (shard.counts[shard.rank] != VB or shard.tokens_per_view != T):
                 raise AssertionError("shard plan does not match the local views")

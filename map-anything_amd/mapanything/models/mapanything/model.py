@@ -193,29 +193,71 @@ class MapAnything:
         return self
 
     # ------------------------------------------------------------------------------------------ forward
-    def _check_image_only(self, views):
+    def _check_views(self, views):
         for i, v in enumerate(views):
-            extra = [k for k in ("ray_directions_cam", "depth_along_ray", "camera_pose_quats") if k in v]
-            if extra:
-                raise NotImplementedError(
-                    f"view {i}: geometric inputs {extra} are not yet supported by the MI355X engine "
-                    "(image-only inference; pass ignore_*_inputs=True to drop them)")
             if "img" not in v:
-                raise NotImplementedError(f"view {i}: views without images are not supported yet")
+                # the reference's _encode_n_views (model.py:700) indexes views[i]["img"] for every view
+                raise KeyError(f"view {i}: 'img'")
             if v["img"].shape[0] != 1:
                 raise NotImplementedError("batch size per view must be 1")
+
+    @staticmethod
+    def _metric_flags(views) -> List[bool]:
+        out = []
+        for v in views:
+            m = v.get("is_metric_scale")
+            out.append(True if m is None else bool(torch.as_tensor(m).reshape(-1)[0].item()))
+        return out
+
+    def _geo_inputs(self, views, plan, metric, use_calibration=True, use_depth=True, use_pose=True,
+                    use_depth_scale=True, use_pose_scale=True):
+        """GeoInputs for this rank's views with infer()'s deterministic masks (model.py:1292-1438, 2154-2197)."""
+        from .engine import GeoInputs
+
+        if not (use_calibration or use_depth or use_pose):
+            return None
+        V = len(views)
+        local = list(plan.local_views) if plan is not None else list(range(V))
+        s0 = local[0]
+        H, W = views[0]["img"].shape[-2:]
+        dev = self._device
+        g = GeoInputs(local_start=s0)
+        f32 = torch.float32
+        if use_calibration and any("ray_directions_cam" in views[v] for v in local):
+            g.ray_views = [i for i, v in enumerate(local) if "ray_directions_cam" in views[v]]
+            g.rays = torch.cat([views[v]["ray_directions_cam"].to(dev, f32) if "ray_directions_cam" in views[v]
+                                else torch.zeros(1, H, W, 3, device=dev, dtype=f32) for v in local], 0).contiguous()
+        if use_depth and any("depth_along_ray" in views[v] for v in local):
+            g.depth_views = [i for i, v in enumerate(local) if "depth_along_ray" in views[v]]
+            g.depth = torch.cat([views[v]["depth_along_ray"].to(dev, f32).reshape(1, H, W)
+                                 if "depth_along_ray" in views[v] else torch.zeros(1, H, W, device=dev, dtype=f32)
+                                 for v in local], 0).contiguous()
+            g.depth_metric = [bool(metric[v] and use_depth_scale) for v in local]
+        has_pose = [("camera_pose_quats" in v and "camera_pose_trans" in v) for v in views]
+        if use_pose and any(has_pose):
+            g.cam_mask = has_pose
+            g.pose_metric = [bool(metric[v] and use_pose_scale) for v in range(V)]
+            ident_q = torch.tensor([[0.0, 0.0, 0.0, 1.0]], device=dev, dtype=f32)
+            g.cam_quats = torch.cat([views[v]["camera_pose_quats"].to(dev, f32).reshape(1, 4) if has_pose[v]
+                                     else ident_q for v in range(V)], 0)
+            g.cam_trans = torch.cat([views[v]["camera_pose_trans"].to(dev, f32).reshape(1, 3) if has_pose[v]
+                                     else torch.zeros(1, 3, device=dev, dtype=f32) for v in range(V)], 0)
+        return None if g.empty() else g
 
     def forward(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False,
                 precision: Optional[str] = None) -> List[Dict[str, torch.Tensor]]:
         """Raw per-view outputs of model.py:1657-2152 (pts3d, pts3d_cam, ray_directions, depth_along_ray,
-        cam_trans, cam_quats, metric_scaling_factor, conf, non_ambiguous_mask, non_ambiguous_mask_logits)."""
-        self._check_image_only(views)
+        cam_trans, cam_quats, metric_scaling_factor, conf, non_ambiguous_mask, non_ambiguous_mask_logits).
+        Views are in the preprocessed form (ray_directions_cam, depth_along_ray, camera_pose_quats/trans,
+        is_metric_scale); every provided geometric input is used (infer()'s deterministic masks)."""
+        self._check_views(views)
         dnt = views[0].get("data_norm_type", ["dinov2"])
         if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
         local, plan = self._local_views(views)
+        geo = self._geo_inputs(views, plan, self._metric_flags(views))
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
-        raw = self.engine(precision).run(imgs, shard=plan, comm=self._comm)
+        raw = self.engine(precision).run(imgs, shard=plan, comm=self._comm, geo=geo)
         return self._assemble(split_views(raw, len(local), with_post=False), plan, len(views))
 
     @torch.inference_mode()
@@ -234,26 +276,26 @@ class MapAnything:
         else:
             precision = "fp32"
         validated = validate_input_views_for_inference(views)
+        self._check_views(validated)
+        metric = self._metric_flags(validated)   # host-side flags read before the H2D copies
         for v in validated:
             for k in list(v.keys()):
                 if k in ("instance", "idx", "true_shape", "data_norm_type"):
                     continue
                 if isinstance(v[k], torch.Tensor):
                     v[k] = v[k].to(self._device, non_blocking=True)
+                elif isinstance(v[k], tuple):
+                    v[k] = tuple(x.to(self._device, non_blocking=True) if isinstance(x, torch.Tensor) else x
+                                 for x in v[k])
         processed = preprocess_input_views_for_inference(validated)
-        for v in processed:
-            if ignore_calibration_inputs:
-                v.pop("ray_directions_cam", None)
-            if ignore_depth_inputs:
-                v.pop("depth_along_ray", None)
-            if ignore_pose_inputs:
-                v.pop("camera_pose_quats", None)
-                v.pop("camera_pose_trans", None)
-        self._check_image_only(processed)
         local, plan = self._local_views(processed)
+        geo = self._geo_inputs(processed, plan, metric, use_calibration=not ignore_calibration_inputs,
+                               use_depth=not ignore_depth_inputs, use_pose=not ignore_pose_inputs,
+                               use_depth_scale=not ignore_depth_scale_inputs,
+                               use_pose_scale=not ignore_pose_scale_inputs)
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
         eng = self.engine(precision)
-        raw = eng.run(imgs, shard=plan, comm=self._comm)
+        raw = eng.run(imgs, shard=plan, comm=self._comm, geo=geo)
         post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
                                    mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
                                    edge_depth_threshold=edge_depth_threshold,

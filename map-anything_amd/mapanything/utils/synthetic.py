@@ -139,6 +139,23 @@ def synthetic_intrinsics(num_views: int, height: int, width: int, seed: int, bat
     return out
 
 
+def synthetic_poses(num_views: int, seed: int, batch: int = 1) -> List[np.ndarray]:
+    """cam2world 4x4 poses: rotation from a normalised uniform quaternion, translation in U[-2, 2] m."""
+    out = []
+    for v in range(num_views):
+        u = splitmix_uniform(fnv1a64(f"pose/{seed}/{v}") ^ GLOBAL_SEED, batch * 7).reshape(batch, 7)
+        q = (2.0 * u[:, :4] - 1.0).astype(np.float64)
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        x, y, z, w = q[:, 0], q[:, 1], q[:, 2], q[:, 3]
+        P = np.zeros((batch, 4, 4), dtype=np.float64)
+        P[:, 0] = np.stack([1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y), 4 * u[:, 4] - 2], 1)
+        P[:, 1] = np.stack([2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x), 4 * u[:, 5] - 2], 1)
+        P[:, 2] = np.stack([2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y), 4 * u[:, 6] - 2], 1)
+        P[:, 3, 3] = 1.0
+        out.append(P.astype(np.float32))
+    return out
+
+
 def synthetic_sparse_depth(num_views: int, height: int, width: int, seed: int, keep: float = 0.1,
                            batch: int = 1) -> List[np.ndarray]:
     """depth_z in U[0.5, 10] m with (1-keep) of the pixels zeroed."""

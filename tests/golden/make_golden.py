@@ -67,6 +67,14 @@ def make_views(case):
             view["intrinsics"] = torch.from_numpy(K)
             view["depth_z"] = torch.from_numpy(d)
             view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
+        if case.get("mixed"):
+            # 3 views: intrinsics everywhere, depth on views 0 and 2, poses on views 0 and 1, view 2 not metric
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
+            if v in (0, 2):
+                view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
+            if v in (0, 1):
+                view["camera_poses"] = torch.from_numpy(synthetic.synthetic_poses(n, seed)[v])
+            view["is_metric_scale"] = torch.tensor([v != 2])
         views.append(view)
     return views
 
@@ -179,7 +187,7 @@ def shrink(d, out_step, tap_step, dpt_step):
     return {k: np.ascontiguousarray(v) for k, v in out.items()}
 
 
-STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "mm_224": (2, 4, 8)}
+STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8)}
 
 
 def rel_l2(a, b):
@@ -204,7 +212,12 @@ def main():
         "cfg1_224": dict(views=2, h=224, w=224, seed=1),
         "v2_518": dict(views=2, h=518, w=518, seed=2),
         "mm_224": dict(views=2, h=224, w=224, seed=4, multimodal=True),
+        "mixed_224": dict(views=3, h=224, w=224, seed=5, mixed=True),
     }
+    only = os.environ.get("GOLDEN_ONLY")
+    if only:
+        cases = {k: v for k, v in cases.items() if k in only.split(",")}
+        meta = json.load(open(os.path.join(HERE, "golden_meta.json")))
     fp32 = {}
     for name, case in cases.items():
         out, dt = run_case(model, case)
@@ -215,19 +228,22 @@ def main():
         np.savez_compressed(os.path.join(HERE, f"golden_{name}.npz"), **out)
         print(name, f"{dt:.2f}s", {k: v.shape for k, v in out.items()})
 
-    # bf16 yardstick (reference's own bf16 recipe vs its fp32 path)
-    out16, dt16 = run_case(model, cases["cfg1_224"], bf16=True)
-    yard = {"seconds": dt16}
-    for k, v in out16.items():
-        if v.dtype == np.bool_:
-            yard[k] = float(np.mean(v != fp32["cfg1_224"][k]))
-        else:
-            yard[k] = rel_l2(v, fp32["cfg1_224"][k])
-    with open(os.path.join(HERE, "golden_bf16_yardstick.json"), "w") as f:
-        json.dump(yard, f, indent=1, sort_keys=True)
+    # bf16 yardsticks (reference's own bf16 recipe vs its fp32 path)
+    for name, fname in (("cfg1_224", "golden_bf16_yardstick.json"), ("mixed_224", "golden_bf16_yardstick_mixed.json")):
+        if name not in cases:
+            continue
+        out16, dt16 = run_case(model, cases[name], bf16=True)
+        yard = {"seconds": dt16}
+        for k, v in out16.items():
+            if v.dtype == np.bool_:
+                yard[k] = float(np.mean(v != fp32[name][k]))
+            else:
+                yard[k] = rel_l2(v, fp32[name][k])
+        with open(os.path.join(HERE, fname), "w") as f:
+            json.dump(yard, f, indent=1, sort_keys=True)
     with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
-    print(json.dumps(yard, indent=1))
+    print("done")
 
 
 if __name__ == "__main__":

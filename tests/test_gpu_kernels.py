@@ -198,3 +198,79 @@ def test_patchify_and_tokens(nat):
     ref = F.unfold(img, 14, stride=14).transpose(1, 2).reshape(-1, 588)
     assert torch.equal(out[:, :588].cpu(), ref.cpu())
     assert torch.count_nonzero(out[:, 588:]).item() == 0
+
+
+# ------------------------------------------------------------------------------------------ geometric inputs
+def test_gemm_gelu_after_residual(nat):
+    """ResidualBlock tail (dense_rep_encoder.py:44-52): gelu(conv2(x) + b + identity)."""
+    M, N, K = 300, 96, 128
+    A, W, b, r = _rand(M, K, seed=21), _rand(N, K, scale=K ** -0.5, seed=22), _rand(N, seed=23), _rand(M, N, seed=24)
+    out = torch.empty(M, N, device="cuda")
+    nat.gemm(A, W, M, N, K, bias=b, resid1=r, act=nat.ACT_GELU_POST, out_f32=out)
+    ref = F.gelu(A @ W.t() + b + r)
+    assert rel_l2(out.cpu(), ref.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("C,lognorm", [(3, False), (1, True)])
+def test_pixel_unshuffle(nat, C, lognorm):
+    n, H, W, r = 2, 42, 56, 14
+    x = _rand(n, H, W, C, seed=31).abs() if lognorm else _rand(n, H, W, C, seed=31)
+    div = torch.tensor([1.7, 0.4], device="cuda") if lognorm else None
+    out = torch.empty(n * (H // r) * (W // r), C * r * r, device="cuda")
+    nat.pixel_unshuffle(x, n, H, W, C, r, out, view_div=div)
+    y = x
+    if lognorm:
+        y = y / div.view(-1, 1, 1, 1)
+        nrm = y.norm(dim=-1, keepdim=True)
+        y = y / nrm.clip(min=1e-8) * torch.log1p(nrm)
+    ref = F.pixel_unshuffle(y.permute(0, 3, 1, 2), r).permute(0, 2, 3, 1).reshape(out.shape)
+    assert rel_l2(out.cpu(), ref.cpu()) < 1e-6
+
+
+def test_depth_norm_factors(nat):
+    n, H, W = 3, 64, 80
+    d = _rand(n, H, W, seed=41).abs() * 5
+    d[d < 4] = 0
+    d[2] = 0  # a view without valid depth: nf = clip(0, 1e-8)
+    nf = torch.empty(n, device="cuda")
+    lnf = torch.empty(n, device="cuda")
+    nat.depth_norm_factors(d, n, H * W, nf, lnf)
+    valid = d > 0
+    ref = ((d * valid).sum((1, 2)) / (valid.sum((1, 2)) + 1e-8)).clip(min=1e-8)
+    assert torch.allclose(nf, ref, rtol=1e-5)
+    assert torch.allclose(lnf, torch.log(ref + 1e-8), rtol=1e-5)
+
+
+def test_pose_inputs_match_oracle(nat):
+    import importlib
+
+    orc = importlib.import_module("oracle.mapa_oracle")
+    V = 4
+    g = torch.Generator().manual_seed(5)
+    q = torch.randn(V, 4, generator=g)
+    q = q / q.norm(dim=1, keepdim=True)
+    t = torch.randn(V, 3, generator=g)
+    mask = torch.tensor([1, 1, 0, 1], dtype=torch.uint8)
+    oq, ot, ol = torch.empty(V, 4, device="cuda"), torch.empty(V, 3, device="cuda"), torch.empty(V, device="cuda")
+    nat.pose_inputs(q.cuda(), t.cuda(), mask.cuda(), V, oq, ot, ol)
+    rq, rt = torch.tensor([[0.0, 0, 0, 1]]).repeat(V, 1), torch.zeros(V, 3)
+    for v in range(V):
+        if mask[v]:
+            a, b = orc._pose_2_to_1(q[:1], t[:1], q[v:v + 1], t[v:v + 1])
+            rq[v], rt[v] = a[0], b[0]
+    assert float(ot[0].abs().max()) == 0.0  # the reference view's own translation cancels exactly
+    dis = rt.norm(dim=-1)
+    nf = (dis.sum() / ((dis > 0).sum() + 1e-8)).clip(min=1e-8)
+    assert torch.allclose(oq.cpu(), rq, atol=1e-6)
+    assert torch.allclose(ot.cpu(), rt / nf, atol=1e-5)
+    assert torch.allclose(ol.cpu(), torch.log(nf + 1e-8).repeat(V), atol=1e-6)
+
+
+def test_add_view_vectors(nat):
+    V, T, C = 3, 10, 64
+    x = _rand(V * T, C, seed=51)
+    vecs = _rand(2, V, C, seed=52)
+    sc = torch.tensor([[1.0, 0.0, 1.0], [0.0, 1.0, 1.0]], device="cuda")
+    ref = x.view(V, T, C) + (sc[:, :, None, None] * vecs[:, :, None, :]).sum(0)
+    nat.add_view_vectors(x, T, C, V, vecs, sc, 2)
+    assert torch.allclose(x.view(V, T, C), ref, atol=1e-6)

@@ -18,7 +18,7 @@ from conftest import GOLDEN, rel_l2
 
 pytestmark = pytest.mark.gpu
 
-CASES = {"cfg1_224": dict(views=2, h=224, w=224, seed=1), "v2_518": dict(views=2, h=518, w=518, seed=2)}
+from tests_helpers import CASES, make_views
 OUT_KEYS = ("pts3d", "ray_directions", "depth_along_ray", "conf", "non_ambiguous_mask_logits", "cam_trans",
             "cam_quats", "metric_scaling_factor", "intrinsics", "camera_poses")
 
@@ -33,18 +33,16 @@ def model():
 
 
 def _views(case):
-    from mapanything.utils import synthetic
-
-    imgs = synthetic.synthetic_images(case["views"], case["h"], case["w"], case["seed"])
-    return [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]} for i in imgs]
+    return make_views(case)
 
 
 def _meta(name):
     return json.load(open(os.path.join(GOLDEN, "golden_meta.json")))[name]
 
 
-def _yard():
-    return json.load(open(os.path.join(GOLDEN, "golden_bf16_yardstick.json")))
+def _yard(name="cfg1_224"):
+    f = "golden_bf16_yardstick_mixed.json" if name in ("mm_224", "mixed_224") else "golden_bf16_yardstick.json"
+    return json.load(open(os.path.join(GOLDEN, f)))
 
 
 def _compare(preds, g, step, tol_fn):
@@ -61,7 +59,7 @@ def _compare(preds, g, step, tol_fn):
     return errs
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "v2_518"])
+@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224"])
 def test_fp32_mode_matches_reference(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]
@@ -69,11 +67,11 @@ def test_fp32_mode_matches_reference(model, golden, name):
     _compare(preds, g, step, lambda k: 1e-4)
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "v2_518"])
+@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224"])
 def test_bf16_mode_within_reference_bf16_yardstick(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]
-    yard = _yard()
+    yard = _yard(name)
     preds = model.infer(_views(CASES[name]), apply_mask=False)
     _compare(preds, g, step, lambda k: max(2e-3, 3.0 * yard[f"out_{k}"]))
 
@@ -101,6 +99,48 @@ def test_fp32_taps_match_reference(model, golden):
     assert rel_l2(dpt[:, :, ::dpt_step, ::dpt_step], g["tap_dpt_feature"]) < 1e-4
     assert rel_l2(taps["pose_raw"].cpu().numpy(), g["tap_pose_raw"]) < 1e-4
     assert rel_l2(taps["scale_raw"].cpu().numpy().reshape(1, 1, 1), g["tap_scale_raw"]) < 1e-4
+
+
+def test_fp32_geometric_fused_tap(model, golden):
+    """Encoder + ray / depth / depth-scale / camera features + fusion LayerNorm against the reference tap."""
+    from mapanything.utils.inference import (preprocess_input_views_for_inference,
+                                             validate_input_views_for_inference)
+
+    name = "mixed_224"
+    g = golden(name)
+    _, tap_step, _ = _meta(name)["steps_out_tap_dpt"]
+    case = CASES[name]
+    views = validate_input_views_for_inference(_views(case))
+    metric = model._metric_flags(views)
+    for v in views:
+        for k in list(v):
+            if isinstance(v[k], torch.Tensor):
+                v[k] = v[k].cuda()
+    views = preprocess_input_views_for_inference(views)
+    geo = model._geo_inputs(views, None, metric)
+    assert geo is not None and geo.ray_views == [0, 1, 2] and geo.depth_views == [0, 2]
+    assert geo.cam_mask == [True, True, False] and geo.depth_metric == [True, True, False]
+    eng = model.engine("fp32")
+    imgs = torch.cat([v["img"] for v in views], 0).cuda()
+    taps = {}
+    eng.run(imgs, taps=taps, geo=geo)
+    V, hp = case["views"], case["h"] // 14
+    enc = taps["encoder"].view(V, hp, hp, 1024).permute(0, 3, 1, 2).cpu().numpy()
+    assert rel_l2(enc[:, :, ::tap_step, ::tap_step], g["tap_encoder"]) < 1e-4
+    fused = taps["fused"].view(V, hp, hp, 1024).cpu().numpy()
+    assert rel_l2(fused[:, ::tap_step, ::tap_step], g["tap_fused_nhwc"]) < 1e-4
+
+
+def test_ignore_all_geometric_inputs_is_image_only(model):
+    case = CASES["mixed_224"]
+    img_only = [{"img": v["img"], "data_norm_type": ["dinov2"]} for v in _views(case)]
+    a = model.infer(img_only, apply_mask=False)
+    b = model.infer(_views(case), apply_mask=False, ignore_calibration_inputs=True, ignore_depth_inputs=True,
+                    ignore_pose_inputs=True)
+    c = model.infer(_views(case), apply_mask=False)
+    for x, y, z in zip(a, b, c):
+        assert torch.equal(x["pts3d"], y["pts3d"]) and torch.equal(x["cam_quats"], y["cam_quats"])
+        assert not torch.equal(x["pts3d"], z["pts3d"])  # the inputs do change the prediction
 
 
 def test_deterministic_and_mask_consistent(model):

@@ -61,3 +61,48 @@ def test_sharded_equals_single(precision, tol, world, V):
     # every view produced exactly once
     owners = [sum(outs[r][v] is not None for r in range(world)) for v in range(V)]
     assert owners == [1] * V
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5)])
+def test_sharded_geometric_inputs_equal_single(precision, tol):
+    """Rays / depth (+ depth scale) / camera poses on a 2-rank shard: dense encoders run on local views only,
+    the camera translation normaliser is computed over ALL views on every rank."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ThreadComm
+    from tests_helpers import CASES, make_views, released_config
+
+    case = CASES["mixed_224"]
+    ref_model = MapAnything(**released_config(), precision=precision).load_synthetic_weights().to("cuda")
+    ref = ref_model.infer(make_views(case), use_amp=False, apply_mask=False)
+    world = 2
+    comm = ThreadComm(world)
+    model = MapAnything(**released_config(), precision=precision).to("cuda")
+    model._sd = ref_model._sd
+    model.enable_view_sharding(comm=comm)
+    model.engine("fp32")
+    outs = [None] * world
+    errs = []
+    per_rank_views = [make_views(case) for _ in range(world)]
+
+    def run(rank):
+        try:
+            comm.bind(rank)
+            outs[rank] = model.infer(per_rank_views[rank], use_amp=False, apply_mask=False)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            raise
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for r in range(world):
+        for v, o in enumerate(outs[r]):
+            if o is None:
+                continue
+            for k in ("pts3d", "conf", "cam_quats", "cam_trans", "metric_scaling_factor"):
+                e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
+                assert e < tol, (r, v, k, e)

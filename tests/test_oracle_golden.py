@@ -10,30 +10,9 @@ import pytest
 import torch
 
 from conftest import GOLDEN, rel_l2
-from mapanything.utils import synthetic
+from tests_helpers import CASES, make_views
 
 TOL = 2e-5
-
-CASES = {
-    "cfg1_224": dict(views=2, h=224, w=224, seed=1),
-    "v2_518": dict(views=2, h=518, w=518, seed=2),
-    "mm_224": dict(views=2, h=224, w=224, seed=4, multimodal=True),
-}
-
-
-def make_views(case):
-    n, h, w, seed = case["views"], case["h"], case["w"], case["seed"]
-    imgs = synthetic.synthetic_images(n, h, w, seed)
-    views = []
-    for v in range(n):
-        view = {"img": torch.from_numpy(imgs[v]), "data_norm_type": ["dinov2"]}
-        if case.get("multimodal"):
-            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
-            view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
-            view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
-        views.append(view)
-    return views
-
 
 @pytest.fixture(scope="module")
 def oracle(synthetic_sd):
@@ -48,7 +27,7 @@ def _steps(name):
     return meta[name]["steps_out_tap_dpt"]
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "v2_518"])
+@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "mixed_224", "v2_518"])
 def test_oracle_matches_reference(oracle, golden, name):
     g = golden(name)
     out_step, tap_step, dpt_step = _steps(name)
