@@ -26,7 +26,7 @@
 //  * XCD-aware tile order (bijective remap: consecutive tiles share an XCD's L2).
 #include <stdlib.h>
 
-#include "mapa_common.h"
+#include "gemm_internal.h"
 
 namespace mapa_gemm_impl {
 
@@ -51,34 +51,6 @@ struct TraitsF32 {
   using T = float;
   static constexpr int E = 4;
 };
-
-struct GemmArgs {
-  const void* A;
-  int64_t lda;
-  const void* W;
-  int64_t ldw;
-  int M, N, K;
-  int cv_C, cv_IH, cv_IW, cv_OH, cv_OW, cv_stride;
-  const float* bias;
-  int bias_mod;
-  const float* gamma;
-  int act;  // 0 none, 1 gelu(erf), 2 relu
-  const float* resid1;
-  const float* resid2;
-  float* out_f32;
-  void* out_lp;
-  void* out_lp_relu;
-  int64_t ldo;
-  int out_mode;  // 0 row-major, 1 pixel shuffle
-  int ps_s, ps_h, ps_w, ps_cout;
-  int vec_ok;    // N % 4 == 0, ldo % 4 == 0, ps_cout % 4 == 0: 4-wide epilogue
-};
-
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
-  // blocks b, b+8, ... share an XCD (round-robin dispatch); give each XCD a contiguous tile range.
-  const int q = nblk / 8, r = nblk % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
 
 template <typename Tr, int RB>
 __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int wm, int wn, int lane, int kg,
@@ -118,11 +90,6 @@ __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int 
   }
 }
 
-__device__ __forceinline__ float epi_act(float v, int act) {
-  if (act == 1) return gelu_erf(v);
-  if (act == 2) return fmaxf(v, 0.f);
-  return v;
-}
 
 // LDS-DMA of K tile kt into ring slot buf: NLD 16-B chunks of A and of W per thread (lane-linear LDS image).
 template <typename Tr, int AMODE, int RB>
@@ -179,8 +146,9 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // provably wave-uniform: no M0 waterfall
   const int wm = wave >> 1, wn = wave & 1;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
-  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
-  const int bm = (tile / ntn) * BM, bn = (tile % ntn) * BN;
+  int tm, tn;
+  tile_coords<8>(blockIdx.x, ntm, ntn, tm, tn);
+  const int bm = tm * BM, bn = tn * BN;
 
   // ---- per-thread staging geometry: NLD rows (one per load instruction), one fixed source chunk ---------
   const int lrow = lane / CPR, pos = lane % CPR;
@@ -258,22 +226,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
   float* ep = reinterpret_cast<float*>(lds) + wave * 32 * EPI_LD;
   const int c4 = (lane & 15) * 4;
   const int n0 = bn + wn * 64 + c4;
-  float bv[4], gv[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int n = min(n0 + e, p.N - 1);
-    bv[e] = p.bias ? p.bias[n % p.bias_mod] : 0.f;
-    gv[e] = p.gamma ? p.gamma[n] : 1.f;
-  }
-  int64_t col_off = n0;
-  int ps_ky = 0, ps_kx = 0;
-  if (p.out_mode == 1) {
-    const int co = n0 % p.ps_cout, t = n0 / p.ps_cout;
-    ps_ky = t / p.ps_s;
-    ps_kx = t - ps_ky * p.ps_s;
-    col_off = co;
-  }
-  const bool vec = p.vec_ok && (n0 + 3 < p.N);
+  const EpiCol ec = epi_col_setup(p, n0);
   const int g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -292,68 +245,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
         const int rloc = pass * 4 + (lane >> 4);
         const int m = bm + wm * 64 + half * 32 + rloc;
         if (m >= p.M) break;
-        const f32x4 a = *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c4);
-        int64_t off;
-        if (p.out_mode == 0) {
-          off = (int64_t)m * p.ldo + col_off;
-        } else {
-          const int hw = p.ps_h * p.ps_w;
-          const int img = m / hw, rem = m - img * hw;
-          const int y = rem / p.ps_w, x = rem - y * p.ps_w;
-          const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
-          off = (((int64_t)img * H2 + y * p.ps_s + ps_ky) * W2 + x * p.ps_s + ps_kx) * p.ps_cout + col_off;
-        }
-        f32x4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + bv[e], p.act) * gv[e];
-        if (vec) {
-          if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
-          if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
-          if (p.act == MAPA_ACT_GELU_POST) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
-          }
-          if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
-          if constexpr (sizeof(T) == 2) {
-            if (p.out_lp) {
-              uint2 u;
-              u.x = pack_bf16x2(v[0], v[1]);
-              u.y = pack_bf16x2(v[2], v[3]);
-              *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
-            }
-            if (p.out_lp_relu) {
-              uint2 u;
-              u.x = pack_bf16x2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
-              u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
-              *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
-            }
-          } else {
-            if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
-            if (p.out_lp_relu) {
-              f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
-              *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off) = rr;
-            }
-          }
-        } else {
-          // scalar tail (N % 4 != 0 or the last partial column group); row-major only
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n0 + e >= p.N) break;
-            const int64_t o = off + e;
-            float x = v[e];
-            if (p.resid1) x += p.resid1[o];
-            if (p.resid2) x += p.resid2[o];
-            if (p.act == MAPA_ACT_GELU_POST) x = gelu_erf(x);
-            if (p.out_f32) p.out_f32[o] = x;
-            if constexpr (sizeof(T) == 2) {
-              if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
-              if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
-            } else {
-              if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
-              if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);
-            }
-          }
-        }
+        epi_store_row<T>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c4));
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -373,6 +265,20 @@ void launch_variant(int variant, int nblk, hipStream_t stream, const GemmArgs& a
     default: k = gemm_kernel<Tr, AMODE, 128, 2>; break;
   }
   hipLaunchKernelGGL(k, dim3(nblk), dim3(NTHREADS), 0, stream, a);
+}
+
+// Kernel choice per shape, from tools/kbench.py sweeps of the path's shapes on MI355X (TF/s in DESIGN.md):
+//   2568 = 256x256 tile, 1 workgroup/CU, s_setprio around the MFMA bursts (long K, wide convs)
+//   2570/2571 = 256x128 tile, 2 workgroups/CU (one tile's epilogue overlaps the other's main loop)
+//   1282 / 643 = 128x128 tiles (fp32 parity mode; problems too small to fill the chip with 256-row tiles)
+int pick_variant(int dtype, bool conv, int M, int N, int K) {
+  if (dtype != MAPA_BF16) return (conv || K < 1024) ? 643 : 1282;
+  const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
+  if (big_tiles < 256) return (conv || K < 1024) ? 643 : 1282;
+  if (conv) return N >= 256 ? 2568 : 2571;
+  if (K >= 4096) return 2568;
+  if (N >= 3072 && K <= 1024) return 2570;
+  return 2571;
 }
 
 }  // namespace mapa_gemm_impl
@@ -430,8 +336,10 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
     const char* ev = getenv("MAPA_GEMM_VARIANT");
     forced = ev ? atoi(ev) : 0;
   }
-  const int variant = forced ? forced : ((conv || d->K < 1024) ? 643 : 1282);
-  if (d->dtype == MAPA_BF16) {
+  const int variant = forced ? forced : pick_variant(d->dtype, conv, d->M, d->N, d->K);
+  if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2571 && launch_gemm_big(a, conv, variant - 2560, stream)) {
+    // launched
+  } else if (d->dtype == MAPA_BF16) {
     if (conv) launch_variant<TraitsBF16, 1>(variant, nblk, stream, a);
     else launch_variant<TraitsBF16, 0>(variant, nblk, stream, a);
   } else {

@@ -1,0 +1,271 @@
+// 256-row bf16 MFMA GEMM / implicit-GEMM convolution for gfx950 (the large linears and 3x3 convs of the path).
+//
+//   C[M,N] = A[M,K] * W[N,K]^T, bf16 operands, fp32 accumulate, the shared fused epilogue (gemm_internal.h).
+//
+// Why a second tile: a 128x128 tile moves 64 B of operands per 2*128*128*32/... -> 64 flop per staged byte, which
+// the L2 / Infinity-cache path cannot feed at the MFMA rate; 256 x 256 doubles the flops per staged byte.
+//  * 512 threads = 8 waves, 1 workgroup per CU (128 KiB of LDS for two K stages of 256x64 A + BNx64 B).
+//  * BN = 256: waves 2 (M) x 4 (N), wave tile 128x64 = 8x4 MFMA 16x16x32 tiles (128 accumulators / lane).
+//    BN = 128: waves 4 (M) x 2 (N), wave tile 64x64 = 4x4 tiles.
+//  * HBM/L2 -> LDS with global_load_lds_dwordx4 (lane-linear LDS image, 16-B chunk XOR swizzle chunk ^ (row & 7)
+//    applied on the per-lane SOURCE address -> conflict-free ds_read_b128 fragment reads).
+//  * K tile t+1 is DMA'd into the other stage while tile t is multiplied; one barrier per K tile.
+//  * Epilogue: each wave stages 32 x 64 fp32 of its accumulators through LDS and stores 16-B row segments.
+#include "gemm_internal.h"
+
+namespace mapa_gemm_impl {
+namespace {
+
+constexpr int BBM = 256, BTHREADS = 512, BBK = 64, ROWB = 128;  // ROWB: LDS bytes per row of a K tile
+constexpr int ELD = 68;                                           // epilogue fp32 row stride (TN = 64 + 4 pad)
+
+template <int BN, int RB>
+struct Cfg {
+  static constexpr int WM = BN == 256 ? 2 : 4;
+  static constexpr int WN = 8 / WM;
+  static constexpr int TM = BBM / WM, TN = BN / WN;  // TN = 64 in both
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int CPR = RB / 16;                // 16-B chunks per LDS row
+  static constexpr int BK = CPR * 8;                 // K per tile (bf16)
+  static constexpr int KG = CPR / 4;                 // 32-deep MFMA k-groups per tile
+  static constexpr int RPI = 1024 / RB;              // rows per 1-KiB wave instruction
+  static constexpr int A_BYTES = BBM * RB, B_BYTES = BN * RB;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int NLA = BBM / (8 * RPI), NLB = BN / (8 * RPI);  // wave instructions per thread per tile
+  static constexpr int EPI = 8 * 32 * ELD * 4;
+};
+
+// 16-B chunk swizzle of an LDS row (applied on the DMA source address, undone on read): conflict-free
+// ds_read_b128 of the 16x16x32 fragment pattern for both row sizes.
+template <int RB>
+__device__ __forceinline__ int swz(int row) {
+  if constexpr (RB == 128) return row & 7;
+  else return (0x1320 >> (((row >> 2) & 3) * 4)) & 3;  // [0, 2, 3, 1][(row >> 2) & 3]
+}
+
+// LDS-DMA of K tile kt into stage buf: NLA 1-KiB wave instructions of A rows, NLB of W rows per wave.
+template <int AMODE, int BN, int RB>
+__device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf, int kt, int lds_wave, bool k_exact,
+                                          const char* const* a_src, const int* a_sc, const int* cv_base,
+                                          const int* cv_iy, const int* cv_ix, const char* const* w_src,
+                                          const int* w_sc) {
+  using C = Cfg<BN, RB>;
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  char* As = lds + buf * C::STAGE;
+  char* Bs = As + C::A_BYTES;
+  const int64_t koff = (int64_t)kt * C::BK * 2;
+#pragma unroll
+  for (int i = 0; i < C::NLA; ++i) {
+    const int kc = kt * C::BK + a_sc[i] * 8;
+    const bool kin = k_exact || kc < p.K;
+    const char* src;
+    if constexpr (AMODE == 0) {
+      src = kin ? a_src[i] + koff : zero;
+    } else {
+      const int tap = kc / p.cv_C, ci = kc - tap * p.cv_C;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
+      const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+      src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * 2
+               : zero;
+    }
+    __builtin_amdgcn_global_load_lds(src, As + lds_wave + i * 8192, 16, 0, 0);
+  }
+#pragma unroll
+  for (int i = 0; i < C::NLB; ++i) {
+    const int kc = kt * C::BK + w_sc[i] * 8;
+    const bool kin = k_exact || kc < p.K;
+    __builtin_amdgcn_global_load_lds(kin ? w_src[i] + koff : zero, Bs + lds_wave + i * 8192, 16, 0, 0);
+  }
+}
+
+template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1>
+__global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
+  using C = Cfg<BN, RB>;
+  constexpr int MAIN = STAGES * C::STAGE;
+  constexpr int LDS = MAIN > C::EPI ? MAIN : C::EPI;
+  constexpr int NPT = C::NLA + C::NLB;  // LDS-DMA instructions per thread per K tile
+  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BBM - 1) / BBM;
+  int tm, tn;
+  tile_coords<4>(blockIdx.x, ntm, ntn, tm, tn);
+  const int bm = tm * BBM, bn = tn * BN;
+
+  // ---- staging geometry: wave instruction i of this wave covers rows (i*8 + wave)*RPI .. +RPI-1
+  const int lrow = lane / C::CPR, pos = lane % C::CPR;
+  const char* a_src[C::NLA];
+  int a_sc[C::NLA];
+  int cv_base[C::NLA], cv_iy[C::NLA], cv_ix[C::NLA];
+  const char* w_src[C::NLB];
+  int w_sc[C::NLB];
+#pragma unroll
+  for (int i = 0; i < C::NLA; ++i) {
+    const int r = (i * 8 + wave) * C::RPI + lrow;
+    a_sc[i] = pos ^ swz<RB>(r);
+    const int m = min(bm + r, p.M - 1);
+    if constexpr (AMODE == 0) {
+      a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + a_sc[i] * 8) * 2;
+    } else {
+      const int hw = p.cv_OH * p.cv_OW;
+      const int img = m / hw, rem = m - img * hw;
+      const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
+      cv_base[i] = img * p.cv_IH * p.cv_IW;
+      cv_iy[i] = oy * p.cv_stride - 1;
+      cv_ix[i] = ox * p.cv_stride - 1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < C::NLB; ++i) {
+    const int r = (i * 8 + wave) * C::RPI + lrow;
+    w_sc[i] = pos ^ swz<RB>(r);
+    const int n = min(bn + r, p.N - 1);
+    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + w_sc[i] * 8) * 2;
+  }
+  const int nk = (p.K + C::BK - 1) / C::BK;
+  const bool k_exact = (p.K % C::BK) == 0;
+  const int lds_wave = wave * 1024;
+
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  const int g = lane >> 4, r16 = lane & 15;
+  auto compute = [&](int slot) __attribute__((always_inline)) {
+    const char* As = lds + slot * C::STAGE;
+    const char* Bs = As + C::A_BYTES;
+    b8 a[C::KG][C::FM], b[C::KG][C::FN];
+#pragma unroll
+    for (int kg = 0; kg < C::KG; ++kg) {  // every k-group's fragment reads in flight before the first MFMA
+      const int chunk = kg * 4 + g;
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const int rb = wn * C::TN + j * 16 + r16;
+        b[kg][j] = *reinterpret_cast<const b8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int ra = wm * C::TM + i * 16 + r16;
+        a[kg][i] = *reinterpret_cast<const b8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
+      }
+    }
+#pragma unroll
+    for (int kg = 0; kg < C::KG; ++kg) {
+      if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kg][i], b[kg][j], acc[i][j], 0, 0, 0);
+      if (PRIO) __builtin_amdgcn_s_setprio(0);
+    }
+  };
+
+  if constexpr (STAGES == 2) {
+    stage_big<AMODE, BN, RB>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
+    for (int kt = 0; kt < nk; ++kt) {
+      __syncthreads();  // tile kt landed (vmcnt(0) before the barrier); every wave is done with tile kt-1
+      if (kt + 1 < nk && DIAG != 1)
+        stage_big<AMODE, BN, RB>(p, lds, (kt + 1) & 1, kt + 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
+                                 cv_ix, w_src, w_sc);
+      if (DIAG != 2) compute(kt & 1);
+    }
+  } else {
+    // ring of STAGES slots; tiles kt+1 .. kt+STAGES-2 stay in flight across the barrier of tile kt
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+      if (s0 < nk)
+        stage_big<AMODE, BN, RB>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
+    int slot = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const int ahead = min(STAGES - 2, nk - 1 - kt);  // tiles issued after kt that may still be in flight
+      if (ahead >= STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT * (STAGES - 2)) : "memory");
+      else if (STAGES > 3 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT * 2) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's DMA for tile kt landed; every wave done with tile kt-1
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + STAGES - 1 < nk) {
+        const int ns = slot == 0 ? STAGES - 1 : slot - 1;  // (kt + STAGES - 1) % STAGES
+        stage_big<AMODE, BN, RB>(p, lds, ns, kt + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
+                                 cv_ix, w_src, w_sc);
+      }
+      compute(slot);
+      slot = slot + 1 == STAGES ? 0 : slot + 1;
+    }
+  }
+  __syncthreads();  // all waves done with the last stage: LDS becomes the epilogue staging area
+
+  // ---- epilogue: 32 rows x 64 fp32 per wave per pass through LDS, 16-B stores --------------------------------
+  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
+  const int c4 = (lane & 15) * 4;
+  const int n0 = bn + wn * C::TN + c4;
+  const EpiCol ec = epi_col_setup(p, n0);
+#pragma unroll
+  for (int part = 0; part < C::FM / 2; ++part) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (n0 < p.N) {
+#pragma unroll 2
+      for (int pass = 0; pass < 8; ++pass) {
+        const int rloc = pass * 4 + g;
+        const int m = bm + wm * C::TM + part * 32 + rloc;
+        if (m >= p.M) break;
+        epi_store_row<bf16_t>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c4));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+}  // namespace
+
+bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream) {
+  // variant: 0 = 256x256 / 128-B rows / 2 stages, 1 = 256x128 / 128 / 2, 2 = 256x256 / 64-B rows / 4 stages,
+  //          3 = 256x128 / 64 / 4, 4 = 256x128 / 64 / 6, 5 = 256x128 / 128 / 3
+  static const int bns[12] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128};
+  if (variant < 0 || variant > 11) return false;
+  if (conv && (variant == 6 || variant == 7)) return false;  // diagnostics exist for dense A only
+  const int BN = bns[variant];
+  const int nblk = ((a.M + BBM - 1) / BBM) * ((a.N + BN - 1) / BN);
+  void (*k)(GemmArgs) = nullptr;
+#define MAPA_BIG(V, BN_, RB_, S_) \
+  case V: k = conv ? gemm_big_kernel<1, BN_, RB_, S_> : gemm_big_kernel<0, BN_, RB_, S_>; break;
+  switch (variant) {
+    MAPA_BIG(0, 256, 128, 2)
+    MAPA_BIG(1, 128, 128, 2)
+    MAPA_BIG(2, 256, 64, 4)
+    MAPA_BIG(3, 128, 64, 4)
+    MAPA_BIG(4, 128, 64, 6)
+    MAPA_BIG(5, 128, 128, 3)
+    // timing diagnostics (wrong results): 6 = no K-tile reloads (compute only), 7 = loads only (no MFMA)
+    case 6: k = gemm_big_kernel<0, 256, 128, 2, 1>; break;
+    case 7: k = gemm_big_kernel<0, 256, 128, 2, 2>; break;
+    case 8: k = conv ? gemm_big_kernel<1, 256, 128, 2, 0, 1> : gemm_big_kernel<0, 256, 128, 2, 0, 1>; break;
+    case 9: k = conv ? gemm_big_kernel<1, 128, 128, 3, 0, 1> : gemm_big_kernel<0, 128, 128, 3, 0, 1>; break;
+    // two workgroups per CU (72 KiB LDS, <= 128 VGPRs): one tile's epilogue overlaps the other's main loop
+    case 10: k = conv ? gemm_big_kernel<1, 128, 64, 3, 0, 0, 2> : gemm_big_kernel<0, 128, 64, 3, 0, 0, 2>; break;
+    case 11: k = conv ? gemm_big_kernel<1, 128, 64, 3, 0, 1, 2> : gemm_big_kernel<0, 128, 64, 3, 0, 1, 2>; break;
+  }
+#undef MAPA_BIG
+  hipLaunchKernelGGL(k, dim3(nblk), dim3(BTHREADS), 0, stream, a);
+  return true;
+}
+
+}  // namespace mapa_gemm_impl

@@ -1,0 +1,157 @@
+// Internal to the GEMM translation units (gemm.hip: 128x128 tiles, all dtypes; gemm_big.hip: 256-row bf16
+// tiles): launch arguments and the shared fused epilogue.
+#pragma once
+#include "mapa_common.h"
+
+namespace mapa_gemm_impl {
+
+struct GemmArgs {
+  const void* A;
+  int64_t lda;
+  const void* W;
+  int64_t ldw;
+  int M, N, K;
+  int cv_C, cv_IH, cv_IW, cv_OH, cv_OW, cv_stride;
+  const float* bias;
+  int bias_mod;
+  const float* gamma;
+  int act;  // MAPA_ACT_*
+  const float* resid1;
+  const float* resid2;
+  float* out_f32;
+  void* out_lp;
+  void* out_lp_relu;
+  int64_t ldo;
+  int out_mode;  // 0 row-major, 1 pixel shuffle
+  int ps_s, ps_h, ps_w, ps_cout;
+  int vec_ok;    // N % 4 == 0, ldo % 4 == 0, ps_cout % 4 == 0: 4-wide epilogue
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  // blocks b, b+8, ... share an XCD (round-robin dispatch); give each XCD a contiguous tile range.
+  const int q = nblk / 8, r = nblk % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
+// Output tile of this workgroup: XCD-contiguous tile ranges (xcd_remap), walked in groups of GM tile-rows so the
+// ~32 tiles an XCD runs at once form a GM x (32/GM) patch: its A row-blocks and W column-blocks are re-read
+// from that XCD's L2 instead of the Infinity Cache.
+template <int GM>
+__device__ __forceinline__ void tile_coords(int b, int ntm, int ntn, int& tm, int& tn) {
+  const int t = xcd_remap(b, ntm * ntn);
+  const int group = t / (GM * ntn);
+  const int first = group * GM;
+  const int rows = min(GM, ntm - first);
+  const int in = t - group * GM * ntn;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
+__device__ __forceinline__ float epi_act(float v, int act) {
+  if (act == MAPA_ACT_GELU) return gelu_erf(v);
+  if (act == MAPA_ACT_RELU) return fmaxf(v, 0.f);
+  return v;  // NONE, GELU_POST (applied after the residuals)
+}
+
+// Per-thread column state of the epilogue: 4 consecutive output columns n0..n0+3.
+struct EpiCol {
+  int n0;
+  float bv[4], gv[4];
+  int64_t col_off;
+  int ps_ky, ps_kx;
+  bool vec;
+};
+
+__device__ __forceinline__ EpiCol epi_col_setup(const GemmArgs& p, int n0) {
+  EpiCol c;
+  c.n0 = n0;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int n = min(n0 + e, p.N - 1);
+    c.bv[e] = p.bias ? p.bias[n % p.bias_mod] : 0.f;
+    c.gv[e] = p.gamma ? p.gamma[n] : 1.f;
+  }
+  c.col_off = n0;
+  c.ps_ky = c.ps_kx = 0;
+  if (p.out_mode == 1) {
+    const int co = n0 % p.ps_cout, t = n0 / p.ps_cout;
+    c.ps_ky = t / p.ps_s;
+    c.ps_kx = t - c.ps_ky * p.ps_s;
+    c.col_off = co;
+  }
+  c.vec = p.vec_ok && (n0 + 3 < p.N);
+  return c;
+}
+
+// out = resid1 + resid2 + gamma * act(acc + bias)   (GELU_POST: gelu(acc + bias + resid1 + resid2))
+// for row m, columns c.n0..c.n0+3 (caller guarantees m < M and n0 < N).
+template <typename T>
+__device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c, int m, f32x4 a) {
+  int64_t off;
+  if (p.out_mode == 0) {
+    off = (int64_t)m * p.ldo + c.col_off;
+  } else {
+    const int hw = p.ps_h * p.ps_w;
+    const int img = m / hw, rem = m - img * hw;
+    const int y = rem / p.ps_w, x = rem - y * p.ps_w;
+    const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
+    off = (((int64_t)img * H2 + y * p.ps_s + c.ps_ky) * W2 + x * p.ps_s + c.ps_kx) * p.ps_cout + c.col_off;
+  }
+  f32x4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + c.bv[e], p.act) * c.gv[e];
+  if (c.vec) {
+    if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
+    if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
+    if (p.act == MAPA_ACT_GELU_POST) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+    }
+    if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
+    if constexpr (sizeof(T) == 2) {
+      if (p.out_lp) {
+        uint2 u;
+        u.x = pack_bf16x2(v[0], v[1]);
+        u.y = pack_bf16x2(v[2], v[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
+      }
+      if (p.out_lp_relu) {
+        uint2 u;
+        u.x = pack_bf16x2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
+        u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+        *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
+      }
+    } else {
+      if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
+      if (p.out_lp_relu) {
+        f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+        *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off) = rr;
+      }
+    }
+  } else {
+    // scalar tail (N % 4 != 0 or the last partial column group); row-major only
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (c.n0 + e >= p.N) break;
+      const int64_t o = off + e;
+      float x = v[e];
+      if (p.resid1) x += p.resid1[o];
+      if (p.resid2) x += p.resid2[o];
+      if (p.act == MAPA_ACT_GELU_POST) x = gelu_erf(x);
+      if (p.out_f32) p.out_f32[o] = x;
+      if constexpr (sizeof(T) == 2) {
+        if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
+        if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
+      } else {
+        if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
+        if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);
+      }
+    }
+  }
+}
+
+// 256-row bf16 kernel (gemm_big.hip): variant 0 = 256x256 tile, 1 = 256x128 tile.  Returns false if it does not
+// take this shape.
+bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
+
+}  // namespace mapa_gemm_impl

@@ -14,8 +14,15 @@ R, L = V * (T + 1), V * T + 1
 GEMMS = [("enc.qkv", R, 3072, 1024), ("enc.proj", R, 1024, 1024), ("enc.fc1", R, 4096, 1024),
          ("enc.fc2", R, 1024, 4096), ("aat.qkv", L, 2304, 768), ("aat.proj", L, 768, 768),
          ("aat.fc1", L, 3072, 768), ("aat.fc2", L, 768, 3072), ("pose.res", V * T, 784, 784)]
+if os.environ.get("KB_SQ"):
+    GEMMS = [("sq4096", 4096, 4096, 4096), ("sq8192", 8192, 8192, 8192)]
+ONLY = os.environ.get("KB_ONLY")
+if ONLY:
+    GEMMS = [g for g in GEMMS if g[0] in ONLY.split(",")]
 CONVS = [("rn1.c@148", V, 148, 148, 256, 256), ("reg.c2@518", V, 518, 518, 128, 128),
          ("reg.c1@296", V, 296, 296, 256, 128), ("rn2.c@74", V, 74, 74, 256, 256)]
+if ONLY:
+    CONVS = [c for c in CONVS if c[0] in ONLY.split(",")]
 
 
 def timeit(fn, reps):
