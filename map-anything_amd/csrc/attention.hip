@@ -15,6 +15,8 @@
 //  * K LDS rows are XOR-swizzled by (row>>1)&7 and V rows by ((row>>1)&1)<<2 (applied on the LDS-DMA source
 //    address), which makes both the b128 K reads and the transposed V reads bank-conflict free.
 //  * Precise variant (dtype f32): identical dataflow on v_mfma_f32_32x32x2_f32 (exact fp32 products).
+#include <type_traits>
+
 #include "mapa_common.h"
 
 namespace {
@@ -38,16 +40,18 @@ struct AttnArgs {
   int seg_len[MAPA_MAX_KV_SEGMENTS];
 };
 
-// logical key -> physical K/V row (identity unless the keys are split into segments)
+// logical key -> physical K/V row (identity unless the keys are split into segments).  The segment loop is
+// wave-uniform (scalar loads of the descriptor; no divergent indexing, no vector load + vmcnt wait that would
+// drain the in-flight LDS-DMA).
 __device__ __forceinline__ int kv_row(const AttnArgs& p, int key) {
   if (p.nseg == 0) return key;
-  int acc = 0;
+  int off = p.seg_start[0], cum = p.seg_len[0];
 #pragma unroll 1
-  for (int s = 0; s < p.nseg; ++s) {
-    if (key < acc + p.seg_len[s]) return p.seg_start[s] + (key - acc);
-    acc += p.seg_len[s];
+  for (int s = 1; s < p.nseg; ++s) {
+    if (key >= cum) off = p.seg_start[s] - cum;
+    cum += p.seg_len[s];
   }
-  return 0;
+  return key + off;
 }
 
 __device__ __forceinline__ int xcd_remap(int b, int nblk) {
@@ -120,44 +124,75 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
+  // One K/V tile: S^T = K Q^T, online softmax, O^T += V^T P^T.  TAIL (the last, partial tile only) masks the
+  // keys past seq_kv; full tiles carry no masking code at all.
+  auto tile = [&](int kt, auto tail_tag) __attribute__((always_inline)) {
+    constexpr bool TAIL = decltype(tail_tag)::value;
     const int cur = kt & 1;
-    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
     const char* Ks = lds + cur * 2 * TILE;
     const char* Vs = Ks + TILE;
-
-    // S^T = K Q^T  (2 x 32x32 tiles = 64 keys x 32 queries)
-    f32x16 st[2];
+    // every LDS read of this tile is issued before the next tile's DMA, so the compiler's conservative
+    // vmcnt(0) (an LDS-DMA may alias any LDS read) never lands inside the tile: K fragments (b128) and the
+    // transposed V fragments (tr_b16) stay in registers, the DMA then has the whole tile to land.
+    b8 kf[2][4];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) st[kb][r] = 0.f;
       const int row = kb * 32 + l32;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const int chunk = kk * 2 + hl;
-        const b8 kf = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
-        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[kk], st[kb], 0, 0, 0);
+        kf[kb][kk] = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
       }
     }
-    // mask the tail tile (scores are already in the log2 domain), running max
-    if ((kt + 1) * KT > p.seq_kv) {
+    b8 vf[2][2][2];
+    {
+      const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int dt = 0; dt < 2; ++dt) {
+        const int c0 = dt * 32 + 16 * grp + 4 * p4;  // column (d) this lane addresses
+        const int chunk = c0 >> 3, within = (c0 & 7) * 2;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          if (key >= p.seq_kv) st[kb][r] = -INFINITY;
-        }
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const int R0 = kb * 32 + 16 * s + 4 * hl + q4;
+            const int R1 = R0 + 8;
+            const s4v lo = tr_read(Vs + R0 * 128 + ((chunk ^ (((R0 >> 1) & 1) << 2)) << 4) + within);
+            const s4v hi = tr_read(Vs + R1 * 128 + ((chunk ^ (((R1 >> 1) & 1) << 2)) << 4) + within);
+            const s8v vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            vf[dt][kb][s] = __builtin_bit_cast(b8, vv);
+          }
+      }
     }
-    float mx = -INFINITY;
+    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
+
+    // S^T = K Q^T  (2 x 32x32 tiles = 64 keys x 32 queries); masked keys enter as -inf through the C operand
+    f32x16 st[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb][r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int r = 0; r < 16; ++r) {
+        if constexpr (TAIL) {
+          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          st[kb][r] = key < p.seq_kv ? 0.f : -INFINITY;
+        } else {
+          st[kb][r] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
+    }
+    float mx0 = st[0][0], mx1 = st[1][0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) {
+      mx0 = fmaxf(mx0, st[0][r]);
+      mx1 = fmaxf(mx1, st[1][r]);
+    }
+    float mx = fmaxf(mx0, mx1);
+    {  // the other 32 keys of this query row live in lane l ^ 32
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
     const float m_new = fmaxf(m_run, mx);
     if (__any(m_new > m_run)) {  // rescale only when some row max moved (exact: alpha == 1 otherwise)
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
@@ -168,18 +203,18 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
         for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
     }
     m_run = m_new;
-    float ls = 0.f;
+    float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float e = __builtin_amdgcn_exp2f(st[kb][r] - m_new);
         st[kb][r] = e;
-        ls += e;
+        ls[r & 3] += e;
       }
-    l_run += ls;
+    l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
 
-    // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T via transposed LDS reads
+    // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T (transposed LDS reads above)
     b8 pf[2][2];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -190,25 +225,20 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
         for (int j = 0; j < 8; ++j) t[j] = (__bf16)st[kb][8 * s + j];
         pf[kb][s] = t;
       }
-    const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-      const int c0 = dt * 32 + 16 * grp + 4 * p4;  // column (d) this lane addresses
-      const int chunk = c0 >> 3, within = (c0 & 7) * 2;
+    for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int R0 = kb * 32 + 16 * s + 4 * hl + q4;
-          const int R1 = R0 + 8;
-          const s4v lo = tr_read(Vs + R0 * 128 + ((chunk ^ (((R0 >> 1) & 1) << 2)) << 4) + within);
-          const s4v hi = tr_read(Vs + R1 * 128 + ((chunk ^ (((R1 >> 1) & 1) << 2)) << 4) + within);
-          const s8v vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(b8, vv), pf[kb][s], o[dt], 0, 0, 0);
-        }
-    }
+        for (int s = 0; s < 2; ++s) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
     __syncthreads();
-  }
+  };
+
+  stage(0, 0);
+  __syncthreads();
+  const int nfull = p.seq_kv / KT;
+  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::integral_constant<bool, false>());
+  if (nfull < nkt) tile(nfull, std::integral_constant<bool, true>());
 
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   if (qrow < p.seq_q) {

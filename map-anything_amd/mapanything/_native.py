@@ -69,7 +69,7 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = path or _LIB_PATH
+    p = path or os.environ.get("MAPA_LIB_PATH") or _LIB_PATH  # MAPA_LIB_PATH: A/B builds in tools/
     if not os.path.exists(p):
         raise NativeError(f"libmapa.so not found at {p}: build it with `make -C map-anything_amd/csrc` "
                           f"(or __graft_entry__.build()); there is no CPU fallback")
