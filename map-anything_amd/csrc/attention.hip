@@ -15,6 +15,8 @@
 //  * K LDS rows are XOR-swizzled by (row>>1)&7 and V rows by ((row>>1)&1)<<2 (applied on the LDS-DMA source
 //    address), which makes both the b128 K reads and the transposed V reads bank-conflict free.
 //  * Precise variant (dtype f32): identical dataflow on v_mfma_f32_32x32x2_f32 (exact fp32 products).
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "mapa_common.h"
@@ -68,12 +70,18 @@ __device__ __forceinline__ s4v tr_read(const char* p) {
 }
 
 // ------------------------------------------------------------------------------------------------ bf16
-__global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
+// QB query sub-blocks of 32 rows per wave (workgroup = 4 waves = 128*QB query rows).  QB = 2 halves the K/V
+// bytes staged per flop (the per-CU L2 -> LDS fill rate bounds this kernel at QB = 1) and gives each wave two
+// independent softmax / MFMA chains to interleave.
+template <int QB, int NW>
+__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 3) attn_fwd_bf16(AttnArgs p) {
   constexpr int TILE = KT * 128;  // 64 rows x 128 B
+  constexpr int QW = 32 * QB;     // query rows per wave
+  constexpr int QBLK_WG = NW * QW;
   __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5, l32 = lane & 31;
-  const int nqt = (p.seq_q + QBLK - 1) / QBLK;
+  const int nqt = (p.seq_q + QBLK_WG - 1) / QBLK_WG;
   const int nblk = nqt * p.heads * p.batch;
   const int bid = xcd_remap(blockIdx.x, nblk);
   const int qt = bid % nqt, hb = bid / nqt, h = hb % p.heads, b = hb / p.heads;
@@ -81,48 +89,59 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
   const bf16_t* qbase = reinterpret_cast<const bf16_t*>(p.q) + b * p.qb + h * 64;
   const bf16_t* kbase = reinterpret_cast<const bf16_t*>(p.k) + b * p.kb + h * 64;
   const bf16_t* vbase = reinterpret_cast<const bf16_t*>(p.v) + b * p.vb + h * 64;
-  const int qrow = qt * QBLK + wave * 32 + l32;
-  const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
+  int qrow[QB];
+#pragma unroll
+  for (int qb = 0; qb < QB; ++qb) qrow[qb] = qt * QBLK_WG + wave * QW + qb * 32 + l32;
 
   // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 * log2(e) so the
   // scores come out of the MFMA already in the log2 domain (one bf16 rounding of the scaled Q).
-  b8 qf[4];
+  b8 qf[QB][4];
 #pragma unroll
-  for (int kk = 0; kk < 4; ++kk) {
-    const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
-    b8 sc;
+  for (int qb = 0; qb < QB; ++qb) {
+    const int qrow_c = qrow[qb] < p.seq_q ? qrow[qb] : p.seq_q - 1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E));
-    qf[kk] = sc;
+    for (int kk = 0; kk < 4; ++kk) {
+      const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
+      b8 sc;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E));
+      qf[qb][kk] = sc;
+    }
   }
 
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const int nkt = (p.seq_kv + KT - 1) / KT;
 
+  // K and V tiles = 16 pieces of 8 rows x 128 B (one 1-KiB LDS-DMA wave instruction each), dealt over NW waves
   auto stage = [&](int slot, int kt) {
     char* Ks = lds + slot * 2 * TILE;
-    char* Vs = Ks + TILE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = (i * 4 + wave) * 8 + (lane >> 3), pos = lane & 7;
+    for (int i = 0; i < (16 + NW - 1) / NW; ++i) {
+      const int piece = i * NW + wave;
+      if (16 % NW != 0 && piece >= 16) break;
+      const bool isv = piece >= 8;
+      const int row = (piece & 7) * 8 + (lane >> 3), pos = lane & 7;
       const int key = kt * KT + row;
-      const int kc = pos ^ ((row >> 1) & 7);
-      const int vc = pos ^ (((row >> 1) & 1) << 2);
+      const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
       const int pr = kv_row(p, key);
-      const char* ks = key < p.seq_kv ? reinterpret_cast<const char*>(kbase + (int64_t)pr * p.kr + kc * 8) : zero;
-      const char* vs = key < p.seq_kv ? reinterpret_cast<const char*>(vbase + (int64_t)pr * p.vr + vc * 8) : zero;
-      const int base = (i * 4 + wave) * 64 * 16;
-      __builtin_amdgcn_global_load_lds(ks, Ks + base, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(vs, Vs + base, 16, 0, 0);
+      const bf16_t* base = isv ? vbase : kbase;
+      const int64_t rs = isv ? p.vr : p.kr;
+      const char* src = key < p.seq_kv ? reinterpret_cast<const char*>(base + (int64_t)pr * rs + c * 8) : zero;
+      __builtin_amdgcn_global_load_lds(src, Ks + piece * 1024, 16, 0, 0);
     }
   };
 
-  f32x16 o[2];
+  f32x16 o[QB][2];
+  float m_run[QB], l_run[QB];
 #pragma unroll
-  for (int d = 0; d < 2; ++d)
+  for (int qb = 0; qb < QB; ++qb) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[qb][d][r] = 0.f;
+    m_run[qb] = -INFINITY;
+    l_run[qb] = 0.f;
+  }
 
   // One K/V tile: S^T = K Q^T, online softmax, O^T += V^T P^T.  TAIL (the last, partial tile only) masks the
   // keys past seq_kv; full tiles carry no masking code at all.
@@ -144,6 +163,27 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
         kf[kb][kk] = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
       }
     }
+
+    // S^T = K Q^T  (per sub-block: 2 x 32x32 tiles = 64 keys x 32 queries); masked keys enter as -inf via C
+    f32x16 st[QB][2];
+#pragma unroll
+    for (int qb = 0; qb < QB; ++qb)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if constexpr (TAIL) {
+            const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            st[qb][kb][r] = key < p.seq_kv ? 0.f : -INFINITY;
+          } else {
+            st[qb][kb][r] = 0.f;
+          }
+        }
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          st[qb][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[qb][kk], st[qb][kb], 0, 0, 0);
+      }
+    // V^T fragments, then the next tile's DMA (K fragments are dead by now: fewer live registers)
     b8 vf[2][2][2];
     {
       const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
@@ -165,72 +205,67 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
       }
     }
     if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
-
-    // S^T = K Q^T  (2 x 32x32 tiles = 64 keys x 32 queries); masked keys enter as -inf through the C operand
-    f32x16 st[2];
+    float m_new[QB];
+    bool grow = false;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+    for (int qb = 0; qb < QB; ++qb) {
+      float mx0 = st[qb][0][0], mx1 = st[qb][1][0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if constexpr (TAIL) {
-          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          st[kb][r] = key < p.seq_kv ? 0.f : -INFINITY;
-        } else {
-          st[kb][r] = 0.f;
-        }
+      for (int r = 1; r < 16; ++r) {
+        mx0 = fmaxf(mx0, st[qb][0][r]);
+        mx1 = fmaxf(mx1, st[qb][1][r]);
       }
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
-    }
-    float mx0 = st[0][0], mx1 = st[1][0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) {
-      mx0 = fmaxf(mx0, st[0][r]);
-      mx1 = fmaxf(mx1, st[1][r]);
-    }
-    float mx = fmaxf(mx0, mx1);
-    {  // the other 32 keys of this query row live in lane l ^ 32
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-    }
-    const float m_new = fmaxf(m_run, mx);
-    if (__any(m_new > m_run)) {  // rescale only when some row max moved (exact: alpha == 1 otherwise)
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      l_run *= alpha;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
-    }
-    m_run = m_new;
-    float ls[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float e = __builtin_amdgcn_exp2f(st[kb][r] - m_new);
-        st[kb][r] = e;
-        ls[r & 3] += e;
+      float mx = fmaxf(mx0, mx1);
+      {  // the other 32 keys of this query row live in lane l ^ 32
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       }
-    l_run += (ls[0] + ls[1]) + (ls[2] + ls[3]);
-
-    // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T (transposed LDS reads above)
-    b8 pf[2][2];
+      m_new[qb] = fmaxf(m_run[qb], mx);
+      grow |= m_new[qb] > m_run[qb];
+    }
+    if (__any(grow)) {  // rescale only when some row max moved (exact: alpha == 1 otherwise)
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+      for (int qb = 0; qb < QB; ++qb) {
+        const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - m_new[qb]);
+        l_run[qb] *= alpha;
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        b8 t;
+        for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) t[j] = (__bf16)st[kb][8 * s + j];
-        pf[kb][s] = t;
+          for (int r = 0; r < 16; ++r) o[qb][d][r] *= alpha;
       }
+    }
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+    for (int qb = 0; qb < QB; ++qb) {
+      m_run[qb] = m_new[qb];
+      float ls[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
+        for (int r = 0; r < 16; ++r) {
+          const float e = __builtin_amdgcn_exp2f(st[qb][kb][r] - m_new[qb]);
+          st[qb][kb][r] = e;
+          ls[r & 3] += e;
+        }
+      l_run[qb] += (ls[0] + ls[1]) + (ls[2] + ls[3]);
+      // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T (transposed LDS reads above)
+      b8 pf[2][2];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          b8 t;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t[j] = (__bf16)st[qb][kb][8 * s + j];
+          pf[kb][s] = t;
+        }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            o[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[qb][dt], 0, 0, 0);
+    }
     __syncthreads();
   };
 
@@ -240,21 +275,25 @@ __global__ void __launch_bounds__(NT, 2) attn_fwd_bf16(AttnArgs p) {
   for (int kt = 0; kt < nfull; ++kt) tile(kt, std::integral_constant<bool, false>());
   if (nfull < nkt) tile(nfull, std::integral_constant<bool, true>());
 
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  if (qrow < p.seq_q) {
-    const float inv = 1.f / l_tot;
-    bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+  for (int qb = 0; qb < QB; ++qb) {
+    const float l_tot = l_run[qb] + __shfl_xor(l_run[qb], 32, 64);
+    if (qrow[qb] < p.seq_q) {
+      const float inv = 1.f / l_tot;
+      bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow[qb] * p.orr + h * 64;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hl;
-        uint2 pk;
-        pk.x = pack_bf16x2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-        pk.y = pack_bf16x2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(obase + d) = pk;
-      }
-    if (p.lse && hl == 0) p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_run + __log2f(l_tot)) * LN2;
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int d = dt * 32 + 8 * g + 4 * hl;
+          uint2 pk;
+          pk.x = pack_bf16x2(o[qb][dt][4 * g + 0] * inv, o[qb][dt][4 * g + 1] * inv);
+          pk.y = pack_bf16x2(o[qb][dt][4 * g + 2] * inv, o[qb][dt][4 * g + 3] * inv);
+          *reinterpret_cast<uint2*>(obase + d) = pk;
+        }
+      if (p.lse && hl == 0)
+        p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow[qb]] = (m_run[qb] + __log2f(l_tot)) * LN2;
+    }
   }
 }
 
@@ -420,11 +459,17 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   }
   MAPA_CHECK_ARG(d->kv_nseg == 0 || tot == d->seq_kv, "mapa_attention: kv segments sum %lld != seq_kv %d",
                  (long long)tot, d->seq_kv);
-  const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
-  if (d->dtype == MAPA_BF16)
-    hipLaunchKernelGGL(attn_fwd_bf16, dim3(nblk), dim3(NT), 0, stream, a);
-  else
+  if (d->dtype == MAPA_BF16) {
+    // 4 waves x 32 query rows per workgroup, 3 workgroups per CU (6- and 8-wave workgroups measured slower:
+    // the per-tile barrier then spans more waves)
+    constexpr int nw = 4;
+    const int qblk = 32 * nw;
+    const int nblk = ((d->seq_q + qblk - 1) / qblk) * d->heads * d->batch;
+    hipLaunchKernelGGL((attn_fwd_bf16<1, nw>), dim3(nblk), dim3(nw * 64), 0, stream, a);
+  } else {
+    const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
     hipLaunchKernelGGL(attn_fwd_f32, dim3(nblk), dim3(NT), 0, stream, a);
+  }
   MAPA_CHECK_LAUNCH("mapa_attention");
   return 0;
 }
