@@ -43,6 +43,10 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--geometric", action="store_true",
+                    help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1", "pmc_traffic.json"),
+                    help="HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_summary.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -69,6 +73,12 @@ def main():
         model.enable_view_sharding(dist.group.WORLD)
     imgs = synthetic.synthetic_images(V_total, H, W, seed=2)
     views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in imgs]
+    if args.geometric:
+        Ks = synthetic.synthetic_intrinsics(V_total, H, W, seed=4)
+        Ds = synthetic.synthetic_sparse_depth(V_total, H, W, seed=4)
+        for v, K, D in zip(views, Ks, Ds):
+            v.update(intrinsics=torch.from_numpy(K).to(dev), depth_z=torch.from_numpy(D).to(dev),
+                     is_metric_scale=torch.ones(1, dtype=torch.bool, device=dev))
 
     def step():
         return model.infer(views)
@@ -105,23 +115,31 @@ def main():
             kind = max(ktimes, key=lambda k: ktimes[k]["ms"])
             kt = ktimes[kind]
             achieved = kt["flops"] / (kt["ms"] * 1e-3) / 1e12 if kt["flops"] else None
+            traffic = None
+            if os.path.exists(args.traffic_json):
+                tj = json.load(open(args.traffic_json)).get(kind)
+                traffic = tj["hbm_bytes_per_launch"] if tj else None
             roofline = {"kernel": kind, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                         "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
-                        "traffic": None, "launches": kt["count"], "avg_launch_us": kt["ms"] * 1e3 / kt["count"],
+                        "traffic": traffic, "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)",
+                        "launches": kt["count"], "avg_launch_us": kt["ms"] * 1e3 / kt["count"],
                         "per_kernel": {k: {"ms_per_step": v["ms"] / args.steps,
                                            "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["flops"] else None}
                                        for k, v in ktimes.items()}}
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.geometric:
             cpu = cpu_baseline(model, imgs, H, W)
         L = V_total * T + 1
-        gf_view = (1870.9e9 + 36864.0 * L * L / V_total) / 1e12 if H == 518 else None
+        gf_view = (1870.9e9 + 36864.0 * L * L / V_total + (165.6e9 if args.geometric else 0.0)) / 1e12 \
+            if H == 518 else None
         line = {
             "metric": "views/sec + ms/infer, N-view 518x518 bf16 at 1/2/4/8 MI355X",
             "value": value, "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
-            "config": {"workload": f"{V_total}-view {H}x{W} image-only MapAnything.infer (configs[1] at N=1)",
+            "config": {"workload": f"{V_total}-view {H}x{W} " + (
+                           "images+intrinsics+sparse depth (cfg4 inputs)" if args.geometric else
+                           "image-only MapAnything.infer (configs[1] at N=1)"),
                        "views": V_total, "views_per_gpu": args.views_per_gpu, "height": H, "width": W,
                        "batch_per_view": 1,
                        "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else "single"},
