@@ -193,6 +193,12 @@ int mapa_pose_inputs(const float* quats, const float* trans, const uint8_t* cam_
 int mapa_add_view_vectors(float* x, int T, int C, int nviews, const float* vecs, const float* scales, int nvec,
                           mapa_stream_t stream);
 
+/* preprocess_input_views_for_inference per pixel (inference.py:222-311): rays [n][H][W][3] = unit rays from
+ * pinhole K [n][3][3] (get_rays_in_camera_frame, geometry.py:186-241) or rays_in / (|rays_in| + 1e-8); with depth_z
+ * [n][H][W]: depth_along_ray = |depth_z * rays / rays_z|.  Exactly one of K / rays_in. */
+int mapa_view_rays(const float* K, const float* rays_in, const float* depth_z, int n, int H, int W, float* rays,
+                   float* depth_along_ray, mapa_stream_t stream);
+
 /* dst[i] += src[i] (n % 4 == 0) */
 int mapa_add_f32(float* dst, const float* src, int64_t n, mapa_stream_t stream);
 

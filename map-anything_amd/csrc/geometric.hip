@@ -172,7 +172,58 @@ __global__ void add_f32_kernel(float* __restrict__ dst, const float* __restrict_
   }
 }
 
+// preprocess_input_views_for_inference (inference.py:222-311) per pixel: unit rays from pinhole intrinsics
+// (get_rays_in_camera_frame, geometry.py:186-241) or renormalised given rays, and depth_z -> depth along the ray.
+// Compiled without FMA contraction: same operation order as the reference's tensor expressions.
+__global__ void view_rays_kernel(const float* __restrict__ K, const float* __restrict__ rays_in,
+                                 const float* __restrict__ depth_z, int n, int H, int W, float* __restrict__ rays,
+                                 float* __restrict__ depth_ray) {
+  const int64_t total = (int64_t)n * H * W;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int x = (int)(e % W);
+    const int64_t r2 = e / W;
+    const int y = (int)(r2 % H);
+    const int v = (int)(r2 / H);
+    float d0, d1, d2;
+    if (K) {
+      const float* k = K + v * 9;
+      const float xx = ((float)x - k[2]) / k[0];
+      const float yy = ((float)y - k[5]) / k[4];
+      const float nrm = sqrtf(xx * xx + yy * yy + 1.f);
+      d0 = xx / nrm;
+      d1 = yy / nrm;
+      d2 = 1.f / nrm;
+    } else {
+      const float* r = rays_in + e * 3;
+      const float nrm = sqrtf(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]) + 1e-8f;
+      d0 = r[0] / nrm;
+      d1 = r[1] / nrm;
+      d2 = r[2] / nrm;
+    }
+    rays[e * 3 + 0] = d0;
+    rays[e * 3 + 1] = d1;
+    rays[e * 3 + 2] = d2;
+    if (depth_z) {
+      const float dz = depth_z[e];
+      const float p0 = dz * (d0 / d2), p1 = dz * (d1 / d2), p2 = dz * (d2 / d2);
+      depth_ray[e] = sqrtf(p0 * p0 + p1 * p1 + p2 * p2);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int mapa_view_rays(const float* K, const float* rays_in, const float* depth_z, int n, int H, int W,
+                              float* rays, float* depth_along_ray, hipStream_t stream) {
+  MAPA_CHECK_ARG((K != nullptr) != (rays_in != nullptr), "mapa_view_rays: exactly one of K / rays_in");
+  MAPA_CHECK_ARG(rays && n > 0 && H > 0 && W > 0, "mapa_view_rays: bad args");
+  MAPA_CHECK_ARG(!depth_z || depth_along_ray, "mapa_view_rays: depth_z needs depth_along_ray");
+  const int64_t total = (int64_t)n * H * W;
+  hipLaunchKernelGGL(view_rays_kernel, dim3(grid_for(total)), dim3(TPB), 0, stream, K, rays_in, depth_z, n, H, W, rays,
+                     depth_along_ray);
+  MAPA_CHECK_LAUNCH("mapa_view_rays");
+  return 0;
+}
 
 extern "C" int mapa_pixel_unshuffle(const float* in, int n, int H, int W, int C, int r, const float* view_div,
                                     int lognorm, void* out, int out_dtype, int64_t ldo, hipStream_t stream) {

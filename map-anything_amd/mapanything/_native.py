@@ -27,6 +27,7 @@ EXPORTED = (
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
+    "mapa_view_rays",
 )
 
 
@@ -99,6 +100,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_pose_inputs.argtypes = [vp, vp, vp, i, vp, vp, vp, vp]
     L.mapa_add_view_vectors.argtypes = [vp, i, i, i, vp, vp, i, vp]
     L.mapa_add_f32.argtypes = [vp, vp, i64, vp]
+    L.mapa_view_rays.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
     _lib = L
     return L
 
@@ -332,3 +334,8 @@ def add_view_vectors(x, T, C, nviews, vecs, scales, nvec):
 
 def add_f32(dst, src, n):
     check(lib().mapa_add_f32(ptr(dst), ptr(src), n, stream()), "mapa_add_f32")
+
+
+def view_rays(n, H, W, rays, *, K=None, rays_in=None, depth_z=None, depth_along_ray=None):
+    check(lib().mapa_view_rays(ptr(K), ptr(rays_in), ptr(depth_z), n, H, W, ptr(rays), ptr(depth_along_ray),
+                               stream()), "mapa_view_rays")

@@ -55,35 +55,38 @@ def validate_input_views_for_inference(views: List[Dict[str, Any]]) -> List[Dict
 
 
 def get_rays_in_camera_frame(intrinsics: torch.Tensor, height: int, width: int) -> torch.Tensor:
-    """geometry.py:186-241 (unit-sphere normalised ray directions, (B,H,W,3))."""
-    dev = intrinsics.device
-    x, y = torch.meshgrid(torch.arange(width, device=dev).float(), torch.arange(height, device=dev).float(),
-                          indexing="xy")
-    B = intrinsics.shape[0]
-    fx, fy = intrinsics[:, 0, 0].view(-1, 1, 1), intrinsics[:, 1, 1].view(-1, 1, 1)
-    cx, cy = intrinsics[:, 0, 2].view(-1, 1, 1), intrinsics[:, 1, 2].view(-1, 1, 1)
-    d = torch.stack(((x.expand(B, -1, -1) - cx) / fx, (y.expand(B, -1, -1) - cy) / fy,
-                     torch.ones(B, height, width, device=dev)), -1)
-    return d / torch.norm(d, dim=-1, keepdim=True)
+    """geometry.py:186-241 (unit-sphere normalised ray directions, (B,H,W,3)) — mapa_view_rays kernel."""
+    K = intrinsics.to(torch.float32).contiguous()
+    B = K.shape[0]
+    rays = torch.empty(B, height, width, 3, device=K.device, dtype=torch.float32)
+    nat.view_rays(B, height, width, rays, K=K)
+    return rays
 
 
 def preprocess_input_views_for_inference(views: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
-    """inference.py:222-311."""
+    """inference.py:222-311.  Per-pixel work (rays from intrinsics or renormalised rays, depth_z -> depth along
+    the ray) in one mapa_view_rays launch per view; the per-view 3x3 -> quaternion stays a small tensor op."""
     out = []
     for view in views:
         pv = dict(view)
-        if "intrinsics" in view:
+        if "intrinsics" in view or "ray_directions" in view:
             H, W = view["img"].shape[-2:]
-            pv["ray_directions"] = get_rays_in_camera_frame(view["intrinsics"], H, W)
-            del pv["intrinsics"]
-        elif "ray_directions" in view:
-            rd = view["ray_directions"]
-            pv["ray_directions"] = rd / (torch.norm(rd, dim=-1, keepdim=True) + 1e-8)
-        if "depth_z" in view:
-            rd = pv["ray_directions"]
-            pts = view["depth_z"][..., None] * (rd / rd[..., 2:3])
-            pv["depth_along_ray"] = torch.norm(pts, dim=-1, keepdim=True)
-            del pv["depth_z"]
+            dev = view["img"].device
+            B = view["img"].shape[0]
+            rays = torch.empty(B, H, W, 3, device=dev, dtype=torch.float32)
+            dz = view["depth_z"].to(torch.float32).contiguous() if "depth_z" in view else None
+            dar = torch.empty(B, H, W, 1, device=dev, dtype=torch.float32) if dz is not None else None
+            if "intrinsics" in view:
+                nat.view_rays(B, H, W, rays, K=view["intrinsics"].to(torch.float32).contiguous(), depth_z=dz,
+                              depth_along_ray=dar)
+                del pv["intrinsics"]
+            else:
+                nat.view_rays(B, H, W, rays, rays_in=view["ray_directions"].to(torch.float32).contiguous(),
+                              depth_z=dz, depth_along_ray=dar)
+            pv["ray_directions"] = rays
+            if dz is not None:
+                pv["depth_along_ray"] = dar
+                del pv["depth_z"]
         if "camera_poses" in view:
             cp = view["camera_poses"]
             if isinstance(cp, tuple) and len(cp) == 2:

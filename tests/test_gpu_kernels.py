@@ -274,3 +274,23 @@ def test_add_view_vectors(nat):
     ref = x.view(V, T, C) + (sc[:, :, None, None] * vecs[:, :, None, :]).sum(0)
     nat.add_view_vectors(x, T, C, V, vecs, sc, 2)
     assert torch.allclose(x.view(V, T, C), ref, atol=1e-6)
+
+
+def test_view_rays_and_depth_along_ray(nat):
+    """preprocess_input_views_for_inference per pixel (inference.py:222-311) vs its torch restatement."""
+    n, H, W = 2, 48, 64
+    K = torch.tensor([[[50.0, 0, 31.5], [0, 52.0, 23.0], [0, 0, 1]], [[70.0, 0, 30.0], [0, 66.0, 25.0], [0, 0, 1]]])
+    dz = (torch.rand(n, H, W, generator=torch.Generator().manual_seed(3)) * 5).cuda()
+    rays = torch.empty(n, H, W, 3, device="cuda")
+    dar = torch.empty(n, H, W, 1, device="cuda")
+    nat.view_rays(n, H, W, rays, K=K.cuda(), depth_z=dz, depth_along_ray=dar)
+    x, y = torch.meshgrid(torch.arange(W).float(), torch.arange(H).float(), indexing="xy")
+    d = torch.stack(((x - K[:, 0, 2, None, None]) / K[:, 0, 0, None, None],
+                     (y - K[:, 1, 2, None, None]) / K[:, 1, 1, None, None], torch.ones(n, H, W)), -1)
+    ref = d / torch.norm(d, dim=-1, keepdim=True)
+    assert torch.allclose(rays.cpu(), ref, atol=1e-6)
+    ref_d = torch.norm(dz.cpu()[..., None] * (ref / ref[..., 2:3]), dim=-1, keepdim=True)
+    assert torch.allclose(dar.cpu(), ref_d, rtol=1e-5)
+    raw = _rand(n, H, W, 3, seed=7)
+    nat.view_rays(n, H, W, rays, rays_in=raw)
+    assert torch.allclose(rays, raw / (torch.norm(raw, dim=-1, keepdim=True) + 1e-8), atol=1e-6)
