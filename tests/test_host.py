@@ -57,7 +57,9 @@ def test_validation_errors_match_reference_rules():
     assert val(ok) is ok
 
 
+@pytest.mark.gpu
 def test_preprocess_matches_oracle_restatement():
+    """Per-pixel preprocessing runs in the mapa_view_rays kernel (GPU); compared with the oracle's CPU restatement."""
     from mapanything.utils.inference import preprocess_input_views_for_inference
     from oracle.mapa_oracle import preprocess_views
 
@@ -67,10 +69,12 @@ def test_preprocess_matches_oracle_restatement():
     q = q / q.norm()
     views = [{"img": torch.zeros(1, 3, 28, 28), "data_norm_type": ["dinov2"], "intrinsics": K, "depth_z": d,
               "camera_poses": (q, torch.tensor([[1.0, 2.0, 3.0]]))}]
-    a = preprocess_input_views_for_inference([dict(v) for v in views])[0]
+    gpu_views = [{k: (v.cuda() if torch.is_tensor(v) else tuple(x.cuda() for x in v) if isinstance(v, tuple) else v)
+                  for k, v in view.items()} for view in views]
+    a = preprocess_input_views_for_inference(gpu_views)[0]
     b = preprocess_views([dict(v) for v in views])[0]
     for k in ("ray_directions_cam", "depth_along_ray", "camera_pose_quats", "camera_pose_trans"):
-        assert torch.allclose(a[k], b[k], atol=1e-6), k
+        assert torch.allclose(a[k].cpu(), b[k], atol=1e-6), k
     assert bool(a["is_metric_scale"].all())
 
 
