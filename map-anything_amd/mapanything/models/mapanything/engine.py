@@ -631,11 +631,12 @@ class MapaEngine:
     # ----------------------------------------------------------------------------------------------- run
     @torch.no_grad()
     def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None,
-            geo: Optional[GeoInputs] = None) -> Dict[str, torch.Tensor]:
+            geo: Optional[GeoInputs] = None, dpt_chunk: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
         per-pixel / per-view outputs of MapAnything.forward, view-major.  With `shard`/`comm`, imgs are this
         rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'.  `geo` carries the
-        optional geometric inputs of these views (GeoInputs)."""
+        optional geometric inputs of these views (GeoInputs).  dpt_chunk: run the dense head over at most that many
+        views at a time (memory_efficient_inference, model.py:1479-1516); None = all views at once."""
         if imgs.dim() != 4 or imgs.shape[1] != 3:
             raise AssertionError("images must be (V, 3, H, W)")
         VB, _, H, W = imgs.shape
@@ -654,16 +655,24 @@ class MapaEngine:
             scale = self._empty(1, dtype=torch.float32)
             poses44 = self._empty(VB, 4, 4, dtype=torch.float32)
             nat.pose_scale_finalize(pose_raw, scale_raw, VB, 1, pose_out, scale, poses44)
-            hid = self.dpt(fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps)
             f = torch.float32
             out = dict(
                 pts3d=self._empty(VB, H, W, 3, dtype=f), pts3d_cam=self._empty(VB, H, W, 3, dtype=f),
                 ray_directions=self._empty(VB, H, W, 3, dtype=f), depth_along_ray=self._empty(VB, H, W, 1, dtype=f),
                 conf=self._empty(VB, H, W, dtype=f), non_ambiguous_mask_logits=self._empty(VB, H, W, dtype=f),
                 non_ambiguous_mask=self._empty(VB, H, W, dtype=torch.uint8))
-            nat.dense_head_out(hid, VB, H * W, self.w.reg_w6, self.w.reg_b6, pose_out, scale, 1, out["pts3d"],
-                               out["pts3d_cam"], out["ray_directions"], out["depth_along_ray"], out["conf"],
-                               out["non_ambiguous_mask_logits"], out["non_ambiguous_mask"])
+            chunk = VB if not dpt_chunk else max(1, min(int(dpt_chunk), VB))
+            for v0 in range(0, VB, chunk):
+                n = min(chunk, VB - v0)
+                r0, r1 = v0 * T, (v0 + n) * T
+                hid = self.dpt(fused_lp[r0:r1], l11[r0:r1], l17[r0:r1], fin_lp[r0:r1], n, hp, wp, H, W,
+                               taps if n == VB else None)
+                nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, pose_out[v0:v0 + n], scale, 1,
+                                   out["pts3d"][v0:v0 + n], out["pts3d_cam"][v0:v0 + n],
+                                   out["ray_directions"][v0:v0 + n], out["depth_along_ray"][v0:v0 + n],
+                                   out["conf"][v0:v0 + n], out["non_ambiguous_mask_logits"][v0:v0 + n],
+                                   out["non_ambiguous_mask"][v0:v0 + n])
+                del hid
             out["cam_trans"] = pose_out[:, 0:3]
             out["cam_quats"] = pose_out[:, 3:7]
             out["metric_scaling_factor"] = scale.view(1, 1)

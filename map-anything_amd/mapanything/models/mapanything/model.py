@@ -257,7 +257,8 @@ class MapAnything:
         local, plan = self._local_views(views)
         geo = self._geo_inputs(views, plan, self._metric_flags(views))
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
-        raw = self.engine(precision).run(imgs, shard=plan, comm=self._comm, geo=geo)
+        raw = self.engine(precision).run(imgs, shard=plan, comm=self._comm, geo=geo,
+                                         dpt_chunk=self._dpt_chunk(memory_efficient_inference))
         return self._assemble(split_views(raw, len(local), with_post=False), plan, len(views))
 
     @torch.inference_mode()
@@ -295,13 +296,23 @@ class MapAnything:
                                use_pose_scale=not ignore_pose_scale_inputs)
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
         eng = self.engine(precision)
-        raw = eng.run(imgs, shard=plan, comm=self._comm, geo=geo)
+        raw = eng.run(imgs, shard=plan, comm=self._comm, geo=geo,
+                      dpt_chunk=self._dpt_chunk(memory_efficient_inference))
         post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
                                    mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
                                    edge_depth_threshold=edge_depth_threshold,
                                    apply_confidence_mask=apply_confidence_mask,
                                    confidence_percentile=confidence_percentile)
         return self._assemble(split_views(post, len(local), with_post=True), plan, len(views))
+
+    def _dpt_chunk(self, memory_efficient: bool):
+        """Views per dense-head pass.  memory_efficient_inference mirrors _compute_adaptive_minibatch_size
+        (model.py:1440-1477): 95 % of free HBM over a per-view bound (≈320 MB for this engine's dense head at
+        518², against the reference's 680 MB); otherwise every view in one pass."""
+        if not memory_efficient:
+            return None
+        free = torch.cuda.mem_get_info(self._device)[0]
+        return max(1, int(0.95 * free / (320 * 1024 * 1024)))
 
     def _local_views(self, views):
         if self._comm is None:

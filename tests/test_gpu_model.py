@@ -179,3 +179,15 @@ def test_invalid_views_raise_like_reference(model):
          "ray_directions": torch.zeros(1, 224, 224, 3)}
     with pytest.raises(ValueError):
         model.infer([v])
+
+
+def test_memory_efficient_dense_head_chunks_match(model):
+    """memory_efficient_inference runs the dense head over view chunks (model.py:1479-1516); same outputs."""
+    eng = model.engine("bf16")
+    imgs = torch.cat([v["img"] for v in _views(dict(views=3, h=224, w=224, seed=9))], 0).cuda()
+    full = eng.run(imgs)
+    part = eng.run(imgs, dpt_chunk=2)
+    for k in ("pts3d", "conf", "depth_along_ray", "non_ambiguous_mask_logits"):
+        assert rel_l2(part[k].float().cpu().numpy(), full[k].float().cpu().numpy()) < 1e-6, k
+    out = model.infer(_views(dict(views=3, h=224, w=224, seed=9)), memory_efficient_inference=True)
+    assert len(out) == 3 and out[0]["pts3d"].shape == (1, 224, 224, 3)
