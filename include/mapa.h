@@ -152,6 +152,16 @@ int mapa_postprocess_mask(const float* pts3d, const float* pts3d_cam, const uint
                           int n, int H, int W, float normal_tol_deg, float depth_rtol, int use_edges, void* work,
                           mapa_stream_t stream);
 
+/* apply_confidence_mask (inference.py:455-470): per view thr = quantile(conf, q) (torch.quantile's linear
+ * interpolation), mask_out = mask_in & (conf > thr).  conf [n][HW] f32, masks u8 [n][HW] (may alias). */
+int mapa_confidence_mask(const float* conf, const uint8_t* mask_in, uint8_t* mask_out, int n, int64_t HW, float q,
+                         mapa_stream_t stream);
+
+/* infer geometry zeroing (inference.py:486-500): pts3d, pts3d_cam ([npix][3]) and depth_along_ray ([npix]) are
+ * multiplied in place by mask (u8 0/1, [npix]). */
+int mapa_apply_mask(float* pts3d, float* pts3d_cam, float* depth_along_ray, const uint8_t* mask, int64_t npix,
+                    mapa_stream_t stream);
+
 /* recover_pinhole_intrinsics_from_ray_directions (geometry.py:304-447, <= 1 MPix branch): rays [n][H][W][3]
  * unit directions -> K [n][3][3]. */
 int mapa_recover_intrinsics(const float* rays, int n, int H, int W, float* K, mapa_stream_t stream);

@@ -73,6 +73,31 @@ __device__ __forceinline__ f32x4 load4(const T* p) {
   }
 }
 template <typename T>
+__device__ __forceinline__ void load8(const T* p, f32x4& lo, f32x4& hi) {
+  if constexpr (sizeof(T) == 2) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    lo = f32x4{bf16_to_f32(u.x & 0xffff), bf16_to_f32(u.x >> 16), bf16_to_f32(u.y & 0xffff), bf16_to_f32(u.y >> 16)};
+    hi = f32x4{bf16_to_f32(u.z & 0xffff), bf16_to_f32(u.z >> 16), bf16_to_f32(u.w & 0xffff), bf16_to_f32(u.w >> 16)};
+  } else {
+    lo = *reinterpret_cast<const f32x4*>(p);
+    hi = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, f32x4 lo, f32x4 hi) {
+  if constexpr (sizeof(T) == 2) {
+    uint4 u;
+    u.x = pack_bf16x2(lo[0], lo[1]);
+    u.y = pack_bf16x2(lo[2], lo[3]);
+    u.z = pack_bf16x2(hi[0], hi[1]);
+    u.w = pack_bf16x2(hi[2], hi[3]);
+    *reinterpret_cast<uint4*>(p) = u;
+  } else {
+    *reinterpret_cast<f32x4*>(p) = lo;
+    *reinterpret_cast<f32x4*>(p + 4) = hi;
+  }
+}
+template <typename T>
 __device__ __forceinline__ void store4(T* p, f32x4 v) {
   if constexpr (sizeof(T) == 2) {
     uint2 u;
@@ -86,31 +111,38 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 
 // F.interpolate(mode="bilinear", align_corners=True) as ATen computes it (scale = (in-1)/(out-1) in fp32,
 // h1 = h0 + (h0 < in-1), lambdas 1-l / l), NHWC, 4 channels per thread.
+// One thread = 8 channels of one output pixel (16-B bf16 accesses); consecutive threads walk the channels of a
+// pixel, so a wave reads each of the 4 source taps and writes the output as contiguous row segments.  32-bit
+// indexing (the caller checks the element count).
 template <typename TI, typename TO>
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                    int OW, TO* __restrict__ out) {
-  const int c4 = C / 4;
-  const int64_t total = (int64_t)n * OH * OW * c4;
+  const int c8 = C / 8;
+  const int total = n * OH * OW * c8;
   const float sh = OHf > 1 ? (float)(IH - 1) / (float)(OHf - 1) : 0.f;
   const float sw = OWf > 1 ? (float)(IW - 1) / (float)(OWf - 1) : 0.f;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(e % c4) * 4;
-    int64_t r = e / c4;
-    const int ox = (int)(r % OW);
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c = (e % c8) * 8;
+    int r = e / c8;
+    const int ox = r % OW;
     r /= OW;
-    const int oy = (int)(r % OH);
-    const int im = (int)(r / OH);
+    const int oy = r % OH;
+    const int im = r / OH;
     const float fy = sh * oy, fx = sw * ox;
     const int y0 = (int)fy, x0 = (int)fx;
     const int y1 = y0 + (y0 < IH - 1 ? 1 : 0), x1 = x0 + (x0 < IW - 1 ? 1 : 0);
     const float ly1 = fy - y0, ly0 = 1.f - ly1, lx1 = fx - x0, lx0 = 1.f - lx1;
-    const TI* base = in + (int64_t)im * IH * IW * C + c;
-    const f32x4 v00 = load4(base + ((int64_t)y0 * IW + x0) * C);
-    const f32x4 v01 = load4(base + ((int64_t)y0 * IW + x1) * C);
-    const f32x4 v10 = load4(base + ((int64_t)y1 * IW + x0) * C);
-    const f32x4 v11 = load4(base + ((int64_t)y1 * IW + x1) * C);
-    const f32x4 o = ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
-    store4(out + (((int64_t)im * OH + oy) * OW + ox) * C + c, o);
+    const TI* base = in + (size_t)im * IH * IW * C + c;
+    const size_t o00 = ((size_t)y0 * IW + x0) * C, o01 = ((size_t)y0 * IW + x1) * C;
+    const size_t o10 = ((size_t)y1 * IW + x0) * C, o11 = ((size_t)y1 * IW + x1) * C;
+    TO* op = out + (((size_t)im * OH + oy) * OW + ox) * C + c;
+    f32x4 a0, a1, b0, b1, c0, c1, d0, d1;
+    load8(base + o00, a0, a1);
+    load8(base + o01, b0, b1);
+    load8(base + o10, c0, c1);
+    load8(base + o11, d0, d1);
+    store8(op, ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0),
+           ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1));
   }
 }
 
@@ -305,8 +337,9 @@ extern "C" int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, c
 
 extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                 int OW, void* out, int out_dtype, hipStream_t stream) {
-  MAPA_CHECK_ARG(in && out && C % 4 == 0 && OH <= OHf && OW <= OWf, "mapa_bilinear_ac: bad args");
-  const int64_t total = (int64_t)n * OH * OW * (C / 4);
+  MAPA_CHECK_ARG(in && out && C % 8 == 0 && OH <= OHf && OW <= OWf, "mapa_bilinear_ac: bad args (C %% 8 == 0)");
+  const int64_t total = (int64_t)n * OH * OW * (C / 8);
+  MAPA_CHECK_ARG(total < (1LL << 31), "mapa_bilinear_ac: too many outputs for one launch");
   const dim3 g(grid_for(total)), b(TPB);
   if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
     hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,

@@ -210,7 +210,98 @@ inline int grid_for(int64_t n) {
   return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
 }
 
+// Geometry zeroing of infer (inference.py:486-500): pts3d / pts3d_cam / depth_along_ray *= mask (as float, so
+// masked values become +-0 and NaN stays NaN, exactly like the reference's multiply).
+__global__ void apply_mask_kernel(float* __restrict__ pts3d, float* __restrict__ pts_cam, float* __restrict__ depth,
+                                  const uint8_t* __restrict__ mask, int64_t npix) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npix; i += (int64_t)gridDim.x * blockDim.x) {
+    const float m = mask[i] ? 1.f : 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      pts3d[i * 3 + c] *= m;
+      pts_cam[i * 3 + c] *= m;
+    }
+    depth[i] *= m;
+  }
+}
+
+// apply_confidence_mask (inference.py:455-470): thr = torch.quantile(conf_view, q) (linear interpolation between
+// the floor / ceil order statistics of q*(N-1)), mask_out = mask_in & (conf > thr).  One workgroup per view; the
+// two order statistics by 4-pass 8-bit radix select on order-preserving keys of the fp32 bits.
+__device__ __forceinline__ uint32_t fkey(float f) {
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unkey(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+__device__ uint32_t radix_select(const float* __restrict__ x, int64_t N, int64_t k, uint32_t* hist, uint32_t* shared) {
+  uint32_t prefix = 0, mask = 0;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < N; i += blockDim.x) {
+      const uint32_t key = fkey(x[i]);
+      if ((key & mask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t kk = (int64_t)shared[1] | ((int64_t)shared[2] << 32);
+      if (shift == 24) kk = k;
+      uint32_t b = 0;
+      for (; b < 255; ++b) {
+        if ((int64_t)hist[b] > kk) break;
+        kk -= hist[b];
+      }
+      shared[0] = prefix | (b << shift);
+      shared[1] = (uint32_t)(kk & 0xffffffff);
+      shared[2] = (uint32_t)(kk >> 32);
+    }
+    __syncthreads();
+    prefix = shared[0];
+    mask |= 255u << shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
+__global__ void confidence_mask_kernel(const float* __restrict__ conf, const uint8_t* __restrict__ mask_in,
+                                       uint8_t* __restrict__ mask_out, int64_t N, float q) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t shared[3];
+  const float* x = conf + (int64_t)blockIdx.x * N;
+  const double pos = (double)q * (double)(N - 1);
+  const int64_t lo = (int64_t)floor(pos), hi = (int64_t)ceil(pos);
+  const float vlo = unkey(radix_select(x, N, lo, hist, shared));
+  const float vhi = hi == lo ? vlo : unkey(radix_select(x, N, hi, hist, shared));
+  const float thr = vlo + (vhi - vlo) * (float)(pos - (double)lo);
+  const uint8_t* mi = mask_in + (int64_t)blockIdx.x * N;
+  uint8_t* mo = mask_out + (int64_t)blockIdx.x * N;
+  for (int64_t i = threadIdx.x; i < N; i += blockDim.x) mo[i] = (mi[i] && x[i] > thr) ? 1 : 0;
+}
+
 }  // namespace
+
+extern "C" int mapa_confidence_mask(const float* conf, const uint8_t* mask_in, uint8_t* mask_out, int n, int64_t HW,
+                                    float q, hipStream_t stream) {
+  MAPA_CHECK_ARG(conf && mask_in && mask_out && n > 0 && HW > 0 && q >= 0.f && q <= 1.f,
+                 "mapa_confidence_mask: bad args");
+  hipLaunchKernelGGL(confidence_mask_kernel, dim3(n), dim3(1024), 0, stream, conf, mask_in, mask_out, HW, q);
+  MAPA_CHECK_LAUNCH("mapa_confidence_mask");
+  return 0;
+}
+
+extern "C" int mapa_apply_mask(float* pts3d, float* pts3d_cam, float* depth_along_ray, const uint8_t* mask,
+                               int64_t npix, hipStream_t stream) {
+  MAPA_CHECK_ARG(pts3d && pts3d_cam && depth_along_ray && mask && npix > 0, "mapa_apply_mask: bad args");
+  int64_t g = (npix + 255) / 256;
+  if (g > 65536) g = 65536;
+  hipLaunchKernelGGL(apply_mask_kernel, dim3((unsigned)g), dim3(256), 0, stream, pts3d, pts3d_cam, depth_along_ray,
+                     mask, npix);
+  MAPA_CHECK_LAUNCH("mapa_apply_mask");
+  return 0;
+}
 
 // mask_in: non-ambiguous (& confidence) mask u8 [n][H][W]; pts3d [n][H][W][3]; depth_z = pts3d_cam (z at +2,
 // stride 3); work = scratch of n*H*W*(3 floats + 1 float + 1 byte) bytes is carved from `work`.

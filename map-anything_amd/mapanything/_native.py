@@ -27,7 +27,7 @@ EXPORTED = (
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
-    "mapa_view_rays",
+    "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask",
 )
 
 
@@ -101,6 +101,8 @@ def load_library(path: Optional[str] = None):
     L.mapa_add_view_vectors.argtypes = [vp, i, i, i, vp, vp, i, vp]
     L.mapa_add_f32.argtypes = [vp, vp, i64, vp]
     L.mapa_view_rays.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
+    L.mapa_apply_mask.argtypes = [vp, vp, vp, vp, i64, vp]
+    L.mapa_confidence_mask.argtypes = [vp, vp, vp, i, i64, f, vp]
     _lib = L
     return L
 
@@ -339,3 +341,13 @@ def add_f32(dst, src, n):
 def view_rays(n, H, W, rays, *, K=None, rays_in=None, depth_z=None, depth_along_ray=None):
     check(lib().mapa_view_rays(ptr(K), ptr(rays_in), ptr(depth_z), n, H, W, ptr(rays), ptr(depth_along_ray),
                                stream()), "mapa_view_rays")
+
+
+def apply_mask(pts3d, pts3d_cam, depth_along_ray, mask, npix):
+    check(lib().mapa_apply_mask(ptr(pts3d), ptr(pts3d_cam), ptr(depth_along_ray), ptr(mask), npix, stream()),
+          "mapa_apply_mask")
+
+
+def confidence_mask(conf, mask_in, mask_out, n, HW, q):
+    check(lib().mapa_confidence_mask(ptr(conf), ptr(mask_in), ptr(mask_out), n, HW, float(q), stream()),
+          "mapa_confidence_mask")

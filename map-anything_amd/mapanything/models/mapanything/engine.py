@@ -660,7 +660,7 @@ class MapaEngine:
                 pts3d=self._empty(VB, H, W, 3, dtype=f), pts3d_cam=self._empty(VB, H, W, 3, dtype=f),
                 ray_directions=self._empty(VB, H, W, 3, dtype=f), depth_along_ray=self._empty(VB, H, W, 1, dtype=f),
                 conf=self._empty(VB, H, W, dtype=f), non_ambiguous_mask_logits=self._empty(VB, H, W, dtype=f),
-                non_ambiguous_mask=self._empty(VB, H, W, dtype=torch.uint8))
+                non_ambiguous_mask=self._empty(VB, H, W, dtype=torch.bool))  # kernel writes 0/1 bytes
             chunk = VB if not dpt_chunk else max(1, min(int(dpt_chunk), VB))
             for v0 in range(0, VB, chunk):
                 n = min(chunk, VB - v0)

@@ -99,7 +99,7 @@ def preprocess_input_views_for_inference(views: List[Dict[str, Any]]) -> List[Di
                                  "transformation matrices.")
             del pv["camera_poses"]
         if "is_metric_scale" not in pv:
-            pv["is_metric_scale"] = torch.ones(view["img"].shape[0], dtype=torch.bool, device=view["img"].device)
+            pv["is_metric_scale"] = torch.ones(view["img"].shape[0], dtype=torch.bool)  # host flag, read on host
         if "ray_directions" in pv:
             pv["ray_directions_cam"] = pv.pop("ray_directions")
         out.append(pv)
@@ -139,15 +139,14 @@ def postprocess_outputs(raw: Dict[str, torch.Tensor], imgs: torch.Tensor, mean: 
     if apply_mask:
         m_in = raw["non_ambiguous_mask"]
         if apply_confidence_mask:
-            conf = raw["conf"].reshape(V, -1)
-            thr = torch.quantile(conf, confidence_percentile / 100.0, dim=1).view(V, 1, 1)
-            m_in = (m_in.bool() & (raw["conf"] > thr)).to(torch.uint8)
-        m_out = torch.empty(V, H, W, device=imgs.device, dtype=torch.uint8)
+            m_conf = torch.empty(V, H, W, device=imgs.device, dtype=torch.bool)
+            nat.confidence_mask(raw["conf"], m_in, m_conf, V, H * W, confidence_percentile / 100.0)
+            m_in = m_conf
+        m_out = torch.empty(V, H, W, device=imgs.device, dtype=torch.bool)  # kernels write 0/1 bytes
         work = torch.empty(V * H * W * 17, device=imgs.device, dtype=torch.uint8) if mask_edges else None
         nat.postprocess_mask(raw["pts3d"], raw["pts3d_cam"], m_in, m_out, V, H, W, float(edge_normal_threshold),
                              float(edge_depth_threshold), bool(mask_edges), work)
-        mf = m_out.unsqueeze(-1).to(torch.float32)
-        for k in ("pts3d", "pts3d_cam", "depth_along_ray"):
-            out[k] = raw[k] * mf
+        # zero the masked geometry in place (the raw tensors are this call's own outputs)
+        nat.apply_mask(raw["pts3d"], raw["pts3d_cam"], raw["depth_along_ray"], m_out, V * H * W)
         out["mask"] = m_out
     return out

@@ -294,3 +294,25 @@ def test_view_rays_and_depth_along_ray(nat):
     raw = _rand(n, H, W, 3, seed=7)
     nat.view_rays(n, H, W, rays, rays_in=raw)
     assert torch.allclose(rays, raw / (torch.norm(raw, dim=-1, keepdim=True) + 1e-8), atol=1e-6)
+
+
+@pytest.mark.parametrize("q", [0.0, 0.1, 0.5, 0.937, 1.0])
+def test_confidence_mask_matches_torch_quantile(nat, q):
+    n, HW = 3, 50_000
+    g = torch.Generator().manual_seed(11)
+    conf = (1.0 + torch.rand(n, HW, generator=g).mul(7.0).round().div(3.0)).cuda()  # many duplicates
+    conf[1] = 1.0 + torch.rand(HW, generator=g).cuda()
+    m_in = (torch.rand(n, HW, generator=g) > 0.2).cuda()
+    out = torch.empty(n, HW, dtype=torch.bool, device="cuda")
+    nat.confidence_mask(conf, m_in, out, n, HW, q)
+    thr = torch.quantile(conf, q, dim=1, keepdim=True)
+    assert torch.equal(out, m_in & (conf > thr))
+
+
+def test_apply_mask_zeroes_geometry(nat):
+    n = 1000
+    p, pc, d = _rand(n, 3, seed=1), _rand(n, 3, seed=2), _rand(n, 1, seed=3)
+    m = (torch.rand(n, generator=torch.Generator().manual_seed(4)) > 0.5).cuda()
+    ref = (p * m[:, None], pc * m[:, None], d * m[:, None])
+    nat.apply_mask(p, pc, d, m, n)
+    assert torch.equal(p, ref[0]) and torch.equal(pc, ref[1]) and torch.equal(d, ref[2])

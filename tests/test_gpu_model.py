@@ -170,6 +170,17 @@ def test_infer_masked_outputs(model):
         assert torch.equal(p["depth_z"], p["pts3d_cam"][..., 2:3])
 
 
+def test_infer_confidence_mask(model):
+    views = _views(CASES["cfg1_224"])
+    a = model.infer(views, apply_confidence_mask=True, confidence_percentile=30)
+    b = model.infer(views, apply_confidence_mask=False)
+    for x, y in zip(a, b):
+        assert x["mask"].sum() < y["mask"].sum() or y["mask"].sum() == 0
+        conf = x["conf"]
+        thr = torch.quantile(conf.reshape(-1), 0.3)
+        assert bool((conf[x["mask"][..., 0]] > thr).all())
+
+
 def test_invalid_views_raise_like_reference(model):
     with pytest.raises(ValueError):
         model.infer([])
