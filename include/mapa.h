@@ -95,6 +95,13 @@ typedef struct {
 
 int mapa_attention(const mapa_attn_desc* d, mapa_stream_t stream);
 
+/* Merge two attention partials of the same queries over disjoint key sets using their LSEs (the sharded global
+ * layer overlaps its K/V all-gather with the local-key partial): o = (e^{lse_a} o_a + e^{lse_b} o_b) /
+ * (e^{lse_a} + e^{lse_b}).  o_* [rows][heads*64] (row stride ld, bf16 or f32 per dtype; o_out may alias o_a),
+ * lse_* [heads][rows] natural-log f32 as mapa_attention writes them (batch 1); lse_out optional. */
+int mapa_attn_merge(const void* o_a, const float* lse_a, const void* o_b, const float* lse_b, void* o_out,
+                    float* lse_out, int dtype, int rows, int heads, int64_t ld, mapa_stream_t stream);
+
 /* LayerNorm over the last dim (nn.LayerNorm eps=1e-6): y = (x-mean)/sqrt(var+eps)*w + b.
  * x: f32 rows (row stride ldx); outputs optional: y_f32 (ldy), y_lp (bf16 or f32 per lp_dtype, ldy).
  * Output row r reads input row (in_group > 0 ? (r / in_group) * in_group_stride + r % in_group : r) + in_row_off

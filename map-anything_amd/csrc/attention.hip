@@ -431,7 +431,60 @@ __global__ void __launch_bounds__(NT, 1) attn_fwd_f32(AttnArgs p) {
   }
 }
 
+// Merge of two attention partials over disjoint key sets (flash-decoding style):
+//   w_a = exp(lse_a - m), w_b = exp(lse_b - m), m = max(lse_a, lse_b);  o = (w_a o_a + w_b o_b) / (w_a + w_b)
+// o rows [rows][heads*64] (row stride ld), lse [heads][rows] (natural log, as attn_fwd writes it).
+template <typename T>
+__global__ void attn_merge_kernel(const T* __restrict__ oa, const float* __restrict__ la, const T* __restrict__ ob,
+                                  const float* __restrict__ lb, T* __restrict__ out, float* __restrict__ lse_out,
+                                  int rows, int heads, int64_t ld) {
+  const int64_t total = (int64_t)rows * heads * 16;  // 4 values per thread
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int d4 = (int)(e % 16) * 4;
+    const int64_t rh = e / 16;
+    const int h = (int)(rh % heads);
+    const int r = (int)(rh / heads);
+    const float a = la[(int64_t)h * rows + r], b = lb[(int64_t)h * rows + r];
+    const float m = fmaxf(a, b);
+    const float wa = __expf(a - m), wb = __expf(b - m);
+    const float inv = 1.f / (wa + wb);
+    const int64_t o = (int64_t)r * ld + h * 64 + d4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float va, vb;
+      if constexpr (sizeof(T) == 2) {
+        va = bf16_to_f32(oa[o + j]);
+        vb = bf16_to_f32(ob[o + j]);
+      } else {
+        va = oa[o + j];
+        vb = ob[o + j];
+      }
+      const float v = (wa * va + wb * vb) * inv;
+      if constexpr (sizeof(T) == 2) out[o + j] = f32_to_bf16(v);
+      else out[o + j] = v;
+    }
+    if (lse_out && d4 == 0) lse_out[(int64_t)h * rows + r] = m + __logf(wa + wb);
+  }
+}
+
 }  // namespace
+
+extern "C" int mapa_attn_merge(const void* o_a, const float* lse_a, const void* o_b, const float* lse_b, void* o_out,
+                               float* lse_out, int dtype, int rows, int heads, int64_t ld, hipStream_t stream) {
+  MAPA_CHECK_ARG(o_a && lse_a && o_b && lse_b && o_out && rows > 0 && heads > 0 && ld >= (int64_t)heads * 64,
+                 "mapa_attn_merge: bad args");
+  const int64_t total = (int64_t)rows * heads * 16;
+  int64_t g = (total + 255) / 256;
+  if (g > 65536) g = 65536;
+  if (dtype == MAPA_BF16)
+    hipLaunchKernelGGL(attn_merge_kernel<bf16_t>, dim3((unsigned)g), dim3(256), 0, stream, (const bf16_t*)o_a, lse_a,
+                       (const bf16_t*)o_b, lse_b, (bf16_t*)o_out, lse_out, rows, heads, ld);
+  else
+    hipLaunchKernelGGL(attn_merge_kernel<float>, dim3((unsigned)g), dim3(256), 0, stream, (const float*)o_a, lse_a,
+                       (const float*)o_b, lse_b, (float*)o_out, lse_out, rows, heads, ld);
+  MAPA_CHECK_LAUNCH("mapa_attn_merge");
+  return 0;
+}
 
 extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d != nullptr, "mapa_attention: null descriptor");

@@ -19,6 +19,7 @@ reference to ~1e-5).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -465,16 +466,36 @@ class MapaEngine:
         return inter[11], inter[17], fin_lp, fin_f32[VB * T:]
 
     def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm):
-        """Global SelfAttentionBlock on a view shard: Q for the local rows, K/V of all ranks (one all-gather)."""
+        """Global SelfAttentionBlock on a view shard: Q for the local rows, K/V of all ranks (one all-gather).
+        The all-gather runs on the communicator's stream while the local queries attend to this rank's own keys;
+        the remote-key partial follows the gather and the two partials are merged through their LSEs
+        (MAPA_KV_OVERLAP=0: gather first, one attention over every key)."""
         C = AAT_DIM
         self._ln(y, L, C, p["n1w"], p["n1b"], y_lp=yn)
         nat.gemm(yn, p["qkv"][:C], L, C, C, bias=p["qkv_b"][:C], out_lp=q_loc)
         slot = kv_full[shard.rank * shard.max_rows:]
         nat.gemm(yn, p["qkv"][C:], L, 2 * C, C, bias=p["qkv_b"][C:], out_lp=slot, ldo=2 * C)
-        comm.allgather_slots(kv_full, shard.max_rows)
-        nat.attention(q_loc, kv_full, kv_full[:, C:], ao, batch=1, heads=AAT_HEADS, seq_q=L, seq_kv=shard.total_kv,
-                      q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C, v_bstride=0, v_rstride=2 * C,
-                      o_bstride=0, o_rstride=C, kv_segments=shard.kv_segments())
+        strides = dict(batch=1, heads=AAT_HEADS, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
+                       v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C)
+        overlap = hasattr(comm, "allgather_slots_async") and os.environ.get("MAPA_KV_OVERLAP", "1") != "0"
+        if not overlap:
+            comm.allgather_slots(kv_full, shard.max_rows)
+            nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
+                          kv_segments=shard.kv_segments(), **strides)
+        else:
+            handle = comm.allgather_slots_async(kv_full, shard.max_rows)
+            segs = shard.kv_segments()
+            own = segs[shard.rank]
+            rest = [sg for r, sg in enumerate(segs) if r != shard.rank]
+            lse_l = self._empty(AAT_HEADS, L, dtype=torch.float32)
+            nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=own[1], kv_segments=[own], lse=lse_l,
+                          **strides)
+            handle.wait()
+            ao_r = self._empty(L, C)
+            lse_r = self._empty(AAT_HEADS, L, dtype=torch.float32)
+            nat.attention(q_loc, kv_full, kv_full[:, C:], ao_r, seq_kv=sum(sg[1] for sg in rest), kv_segments=rest,
+                          lse=lse_r, **strides)
+            nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, AAT_HEADS, C)
         nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
         self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)
         nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)

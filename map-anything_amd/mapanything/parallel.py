@@ -78,6 +78,12 @@ class DistComm:
         mine = full.narrow(0, self.rank * rows_per_slot, rows_per_slot)
         self.dist.all_gather_into_tensor(full, mine, group=self.group)
 
+    def allgather_slots_async(self, full: torch.Tensor, rows_per_slot: int):
+        """Start the slot all-gather on the communicator's stream (it waits for the current stream's K/V
+        projection); the returned handle's wait() makes the current stream wait for the gathered slots."""
+        mine = full.narrow(0, self.rank * rows_per_slot, rows_per_slot)
+        return self.dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+
 
 class ThreadComm:
     """In-process communicator for tests: P threads (one engine each, same device) exchange slots through a
@@ -109,3 +115,16 @@ class ThreadComm:
         if full.is_cuda:
             torch.cuda.current_stream().synchronize()
         self._barrier.wait()
+
+    def allgather_slots_async(self, full: torch.Tensor, rows_per_slot: int):
+        """Deferred exchange: this rank's slot is final now (synchronised), the other slots are filled at wait();
+        work enqueued in between may read only this rank's own slot, exactly as with the RCCL overlap."""
+        comm = self
+        if full.is_cuda:
+            torch.cuda.current_stream().synchronize()
+
+        class _Handle:
+            def wait(self_inner):
+                comm.allgather_slots(full, rows_per_slot)
+
+        return _Handle()

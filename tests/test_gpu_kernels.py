@@ -316,3 +316,22 @@ def test_apply_mask_zeroes_geometry(nat):
     ref = (p * m[:, None], pc * m[:, None], d * m[:, None])
     nat.apply_mask(p, pc, d, m, n)
     assert torch.equal(p, ref[0]) and torch.equal(pc, ref[1]) and torch.equal(d, ref[2])
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1e-2), (torch.float32, 2e-5)])
+def test_attention_partials_merge_to_full(nat, dtype, tol):
+    """Local-key + remote-key partials merged through their LSEs == attention over all keys (sharded overlap)."""
+    H, Sq, Skv, C = 4, 200, 333, 256
+    q = _rand(Sq, C, seed=61).to(dtype)
+    kv = _rand(Skv, 2 * C, seed=62).to(dtype)
+    st = dict(batch=1, heads=H, seq_q=Sq, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C, v_bstride=0,
+              v_rstride=2 * C, o_bstride=0, o_rstride=C)
+    full = torch.empty(Sq, C, device="cuda", dtype=dtype)
+    nat.attention(q, kv, kv[:, C:], full, seq_kv=Skv, **st)
+    segs_a, segs_b = [(0, 100)], [(100, 150), (250, 83)]
+    oa, ob = torch.empty_like(full), torch.empty_like(full)
+    la, lb = torch.empty(H, Sq, device="cuda"), torch.empty(H, Sq, device="cuda")
+    nat.attention(q, kv, kv[:, C:], oa, seq_kv=100, kv_segments=segs_a, lse=la, **st)
+    nat.attention(q, kv, kv[:, C:], ob, seq_kv=233, kv_segments=segs_b, lse=lb, **st)
+    nat.attn_merge(oa, la, ob, lb, oa, Sq, H, C)
+    assert rel_l2(oa.float().cpu(), full.float().cpu()) < tol

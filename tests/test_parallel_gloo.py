@@ -40,7 +40,13 @@ def _gather_rows(full, segs):
     return torch.cat([full[st:st + n] for st, n in segs], 0)
 
 
-def _worker(rank, world, port, V, T, C, q):
+def _attn_lse(qh, kh, vh):
+    s = qh @ kh.transpose(-1, -2) / 8.0
+    lse = torch.logsumexp(s, -1)
+    return torch.softmax(s, -1) @ vh, lse
+
+
+def _worker(rank, world, port, V, T, C, q, overlap=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -57,8 +63,25 @@ def _worker(rank, world, port, V, T, C, q):
         full = torch.zeros(world * plan.max_rows, 2 * C)
         L = plan.local_rows()
         full[rank * plan.max_rows:rank * plan.max_rows + L] = tokens_kv[rows]
-        comm.allgather_slots(full, plan.max_rows)
-        kv = _gather_rows(full, plan.kv_segments())
+        segs = plan.kv_segments()
+        if overlap:
+            # the engine's overlapped global layer: own-key partial while the gather is in flight, remote partial
+            # after wait(), LSE merge (engine._block_global_sharded / mapa_attn_merge)
+            h = comm.allgather_slots_async(full, plan.max_rows)
+            qh0 = tokens_q[rows].view(L, C // 64, 64).transpose(0, 1)
+            own = _gather_rows(full, [segs[rank]])
+            o_l, l_l = _attn_lse(qh0, own[:, :C].reshape(-1, C // 64, 64).transpose(0, 1),
+                                 own[:, C:].reshape(-1, C // 64, 64).transpose(0, 1))
+            h.wait()
+            rest = _gather_rows(full, [sg for r, sg in enumerate(segs) if r != rank])
+            o_r, l_r = _attn_lse(qh0, rest[:, :C].reshape(-1, C // 64, 64).transpose(0, 1),
+                                 rest[:, C:].reshape(-1, C // 64, 64).transpose(0, 1))
+            m = torch.maximum(l_l, l_r)
+            wl, wr = torch.exp(l_l - m)[..., None], torch.exp(l_r - m)[..., None]
+            merged = (wl * o_l + wr * o_r) / (wl + wr)
+        else:
+            comm.allgather_slots(full, plan.max_rows)
+        kv = _gather_rows(full, segs)
         assert kv.shape[0] == plan.total_kv
         # sharded attention for the local queries
         qh = tokens_q[rows].view(L, heads, hd).transpose(0, 1)
@@ -70,17 +93,20 @@ def _worker(rank, world, port, V, T, C, q):
                                              tokens_kv[:, :C].reshape(-1, heads, hd).transpose(0, 1)[None],
                                              tokens_kv[:, C:].reshape(-1, heads, hd).transpose(0, 1)[None])[0]
         err = (got - ref[:, rows]).abs().max().item()
+        if overlap:
+            err = max(err, (merged - ref[:, rows]).abs().max().item())
         q.put((rank, err, sorted(kv[:, 0].tolist()) == sorted(tokens_kv[:, 0].tolist())))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("world,V", [(2, 5), (3, 7)])
-def test_sharded_global_attention_gloo(world, V):
+def test_sharded_global_attention_gloo(world, V, overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, V, 16, 128, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, V, 16, 128, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in range(world)]
