@@ -67,6 +67,8 @@ def make_views(case):
             view["intrinsics"] = torch.from_numpy(K)
             view["depth_z"] = torch.from_numpy(d)
             view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
+        if case.get("rays_only"):
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
         if case.get("mixed"):
             # 3 views: intrinsics everywhere, depth on views 0 and 2, poses on views 0 and 1, view 2 not metric
             view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
@@ -187,7 +189,8 @@ def shrink(d, out_step, tap_step, dpt_step):
     return {k: np.ascontiguousarray(v) for k, v in out.items()}
 
 
-STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8)}
+STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8),
+         "ns_280x392": (4, 2, 8), "one_224": (2, 2, 8)}
 
 
 def rel_l2(a, b):
@@ -213,6 +216,8 @@ def main():
         "v2_518": dict(views=2, h=518, w=518, seed=2),
         "mm_224": dict(views=2, h=224, w=224, seed=4, multimodal=True),
         "mixed_224": dict(views=3, h=224, w=224, seed=5, mixed=True),
+        "ns_280x392": dict(views=2, h=280, w=392, seed=6),
+        "one_224": dict(views=1, h=224, w=224, seed=7, rays_only=True),
     }
     only = os.environ.get("GOLDEN_ONLY")
     if only:
@@ -228,10 +233,10 @@ def main():
         np.savez_compressed(os.path.join(HERE, f"golden_{name}.npz"), **out)
         print(name, f"{dt:.2f}s", {k: v.shape for k, v in out.items()})
 
-    # bf16 yardsticks (reference's own bf16 recipe vs its fp32 path)
-    for name, fname in (("cfg1_224", "golden_bf16_yardstick.json"), ("mixed_224", "golden_bf16_yardstick_mixed.json")):
-        if name not in cases:
-            continue
+    # bf16 yardsticks (reference's own bf16 recipe vs its fp32 path), per case
+    ypath = os.path.join(HERE, "golden_bf16_yardsticks.json")
+    yards = json.load(open(ypath)) if os.path.exists(ypath) else {}
+    for name in cases:
         out16, dt16 = run_case(model, cases[name], bf16=True)
         yard = {"seconds": dt16}
         for k, v in out16.items():
@@ -239,8 +244,9 @@ def main():
                 yard[k] = float(np.mean(v != fp32[name][k]))
             else:
                 yard[k] = rel_l2(v, fp32[name][k])
-        with open(os.path.join(HERE, fname), "w") as f:
-            json.dump(yard, f, indent=1, sort_keys=True)
+        yards[name] = yard
+    with open(ypath, "w") as f:
+        json.dump(yards, f, indent=1, sort_keys=True)
     with open(os.path.join(HERE, "golden_meta.json"), "w") as f:
         json.dump(meta, f, indent=1, sort_keys=True)
     print("done")

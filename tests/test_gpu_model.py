@@ -4,7 +4,7 @@ weights, same seeded inputs) and against the CPU oracle.
 Tolerances (rel-L2 per output):
   * precision "fp32" (exact-fp32 MFMA): 1e-4 — the structural proof that every op matches the reference;
   * precision "bf16" (the reference's own autocast recipe): 3x the reference's own bf16-vs-fp32 deviation
-    measured on the same case (tests/golden/golden_bf16_yardstick.json), floor 2e-3.
+    measured on the same case (tests/golden/golden_bf16_yardsticks.json), floor 2e-3.
 """
 
 import json
@@ -41,8 +41,7 @@ def _meta(name):
 
 
 def _yard(name="cfg1_224"):
-    f = "golden_bf16_yardstick_mixed.json" if name in ("mm_224", "mixed_224") else "golden_bf16_yardstick.json"
-    return json.load(open(os.path.join(GOLDEN, f)))
+    return json.load(open(os.path.join(GOLDEN, "golden_bf16_yardsticks.json")))[name]
 
 
 def _compare(preds, g, step, tol_fn):
@@ -59,7 +58,7 @@ def _compare(preds, g, step, tol_fn):
     return errs
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224"])
+@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224"])
 def test_fp32_mode_matches_reference(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]
@@ -67,7 +66,7 @@ def test_fp32_mode_matches_reference(model, golden, name):
     _compare(preds, g, step, lambda k: 1e-4)
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224"])
+@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224"])
 def test_bf16_mode_within_reference_bf16_yardstick(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]

@@ -27,7 +27,7 @@ def _steps(name):
     return meta[name]["steps_out_tap_dpt"]
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "mixed_224", "v2_518"])
+@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "mixed_224", "ns_280x392", "one_224", "v2_518"])
 def test_oracle_matches_reference(oracle, golden, name):
     g = golden(name)
     out_step, tap_step, dpt_step = _steps(name)

@@ -18,6 +18,8 @@ CASES = {
     "v2_518": dict(views=2, h=518, w=518, seed=2),
     "mm_224": dict(views=2, h=224, w=224, seed=4, multimodal=True),
     "mixed_224": dict(views=3, h=224, w=224, seed=5, mixed=True),
+    "ns_280x392": dict(views=2, h=280, w=392, seed=6),
+    "one_224": dict(views=1, h=224, w=224, seed=7, rays_only=True),
 }
 
 
@@ -36,6 +38,8 @@ def make_views(case):
             view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
             view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
             view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
+        if case.get("rays_only"):
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
         if case.get("mixed"):
             view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
             if v in (0, 2):
