@@ -64,9 +64,20 @@ typedef struct {
   int64_t ldo;
   int out_mode; /* MAPA_OUT_ROWMAJOR or MAPA_OUT_PIXSHUF (n = (ky*s+kx)*cout + co, m = img*h*w + y*w + x) */
   int ps_s, ps_h, ps_w, ps_cout;
+  /* Optional scratch for the stream-K schedule (bf16 shapes whose tile count divides badly over the CUs):
+   * device memory, ZERO-FILLED before its first use, used by one stream at a time; mapa_gemm leaves it zeroed
+   * again when each call completes.  NULL / too small -> the data-parallel schedule (same results to rounding). */
+  void* workspace;
+  int64_t workspace_bytes;
 } mapa_gemm_desc;
 
 int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
+/* Workspace bytes mapa_gemm would use for this problem (0 if its schedule needs none). */
+int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
+/* Tuning / test hook: force one kernel variant for every later mapa_gemm call (0 = automatic per-shape choice,
+ * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
+ * 2560..2571 = 256-row tiles, 2580/2581 = stream-K (needs a workspace; without one the automatic choice runs). */
+int mapa_gemm_set_variant(int variant);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Flash attention forward, head_dim 64, non-causal, softmax scale 1/8 (F.scaled_dot_product_attention at

@@ -281,6 +281,24 @@ int pick_variant(int dtype, bool conv, int M, int N, int K) {
   return 2571;
 }
 
+static int g_forced = -1;  // -1: not read yet; 0: automatic; else a kernel variant code (tuning / tests)
+
+static int forced_variant() {
+  if (g_forced < 0) {
+    const char* ev = getenv("MAPA_GEMM_VARIANT");
+    g_forced = ev ? atoi(ev) : 0;
+  }
+  return g_forced;
+}
+
+// Stream-K variants (2580 + v) are chosen only when the caller passes a workspace; 0 = none.
+int pick_streamk(int dtype, bool conv, int M, int N, int K) {
+  const int f = forced_variant();
+  if (f) return f >= 2580 && f <= 2581 ? f : 0;
+  (void)dtype; (void)conv; (void)M; (void)N; (void)K;
+  return 0;
+}
+
 }  // namespace mapa_gemm_impl
 using namespace mapa_gemm_impl;
 
@@ -331,13 +349,13 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const bool conv = d->a_mode == MAPA_A_CONV3X3;
   // Tile-pipeline variant (RB*10 + STAGES).  Measured on MI355X (tools/kbench.py): 64-B rows x 3 stages (occupancy
   // 3) wins for the implicit convs and K < 1024; 128-B rows x 2 stages for the K >= 1024 linears.
-  static int forced = -1;
-  if (forced < 0) {
-    const char* ev = getenv("MAPA_GEMM_VARIANT");
-    forced = ev ? atoi(ev) : 0;
-  }
+  const int forced = forced_variant();
   const int variant = forced ? forced : pick_variant(d->dtype, conv, d->M, d->N, d->K);
-  if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2571 && launch_gemm_big(a, conv, variant - 2560, stream)) {
+  const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
+  if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
+    // launched (persistent stream-K grid)
+  } else if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2571 &&
+             launch_gemm_big(a, conv, variant - 2560, stream)) {
     // launched
   } else if (d->dtype == MAPA_BF16) {
     if (conv) launch_variant<TraitsBF16, 1>(variant, nblk, stream, a);
@@ -348,4 +366,18 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   }
   MAPA_CHECK_LAUNCH("mapa_gemm");
   return 0;
+}
+
+extern "C" int mapa_gemm_set_variant(int variant) {
+  MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
+                     (variant >= 2560 && variant <= 2571) || variant == 2580 || variant == 2581,
+                 "mapa_gemm_set_variant: unknown variant %d", variant);
+  g_forced = variant;
+  return 0;
+}
+
+extern "C" int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d) {
+  if (!d || d->dtype != MAPA_BF16 || d->M <= 0 || d->N <= 0 || d->K <= 0) return 0;
+  const int sk = pick_streamk(d->dtype, d->a_mode == MAPA_A_CONV3X3, d->M, d->N, d->K);
+  return sk ? streamk_workspace_bytes(d->M, d->N, sk - 2580) : 0;
 }

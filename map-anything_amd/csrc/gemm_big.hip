@@ -17,7 +17,8 @@ namespace mapa_gemm_impl {
 namespace {
 
 constexpr int BBM = 256, BTHREADS = 512, BBK = 64, ROWB = 128;  // ROWB: LDS bytes per row of a K tile
-constexpr int ELD = 68;                                           // epilogue fp32 row stride (TN = 64 + 4 pad)
+constexpr int ELD = 68;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));                                           // epilogue fp32 row stride (TN = 64 + 4 pad)
 
 template <int BN, int RB>
 struct Cfg {
@@ -234,6 +235,269 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   }
 }
 
+
+// ---- stream-K: persistent grid, contiguous K-iteration ranges ---------------------------------------------
+// The (tile, K-tile) iteration space [0, tiles * nk) is cut into G equal contiguous ranges, one per persistent
+// workgroup (G = CUs x occupancy), so every CU does the same number of MFMA K-steps however badly the tile count
+// divides the CU count (M = 10960 -> 43 row tiles; N = 768..1024 -> 6..8 column tiles: 258..344 tiles on 256 CUs).
+// A tile whose iterations span several ranges is finished by its LAST-arriving contributor: each contributor stores
+// its fp32 accumulators to a slab with write-through (sc1) stores and publishes (every wave vmcnt(0) -> barrier ->
+// relaxed agent fetch_add on the tile's ticket; no release fence needed for sc1 payloads); the block drawing ticket
+// nseg-1 reads every slab with sc1 loads (no acquire: no plain load of slab bytes anywhere), sums them in range
+// order (bit-reproducible whatever the arrival order), resets the ticket and runs the fused epilogue.  No block ever waits on another, so the grid drains whatever the residency.
+struct SkArgs {
+  int* tickets;   // [tiles], zero at launch (zeroed once at workspace creation; the last arriver re-zeroes)
+  float* slabs;   // [G][2][BBM * BN] fp32 accumulator images in fragment order
+  int dp_tiles;   // tiles 0 .. dp_tiles-1: whole tiles, tile t on block t % G (data-parallel part)
+  int base;       // dp_tiles * nk: first stream-K iteration
+  int total;      // tiles * nk
+  int per;        // stream-K iterations per workgroup: ceil((total - base) / G)
+  int nk;
+};
+
+// block b owns stream-K iterations [base + b * per, min(base + (b + 1) * per, total)); its slab slot 0 holds the
+// segment its range starts with, slot 1 the one it ends with (a range touches at most two split tiles).
+__device__ __forceinline__ int64_t sk_slab(int b, int tb, const SkArgs& s) {
+  return (int64_t)b * 2 + (s.base + b * s.per >= tb ? 0 : 1);
+}
+
+template <int GM>
+__device__ __forceinline__ void group_coords(int t, int ntm, int ntn, int& tm, int& tn) {
+  const int group = t / (GM * ntn);
+  const int first = group * GM;
+  const int rows = min(GM, ntm - first);
+  const int in = t - group * GM * ntn;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
+template <int AMODE, int BN, int RB, int STAGES, int PRIO, int MINB>
+__global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkArgs s) {
+  using C = Cfg<BN, RB>;
+  constexpr int MAIN = STAGES * C::STAGE;
+  constexpr int BODY = MAIN > C::EPI ? MAIN : C::EPI;
+  constexpr int LDS = BODY + 16;  // + the "last arriver" word (one LDS array: see the guide's 2nd-__shared__ trap)
+  constexpr int NPT = C::NLA + C::NLB;
+  constexpr int SLAB = BBM * BN;
+  static_assert(STAGES >= 3, "ring pipeline");
+  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+  int* last_word = reinterpret_cast<int*>(lds + BODY);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BBM - 1) / BBM;
+  const int vb = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ranges (shared tiles) on one XCD
+  const int r0 = s.base + vb * s.per, r1 = min(r0 + s.per, s.total);
+  const bool k_exact = (p.K % C::BK) == 0;
+  const int lds_wave = wave * 1024;
+  const int lrow = lane / C::CPR, pos = lane % C::CPR;
+  const int g = lane >> 4, r16 = lane & 15;
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+
+  int dp_t = vb;
+  for (int it = r0;;) {
+    int t, k0, k1;
+    if (dp_t < s.dp_tiles) {  // data-parallel whole tiles first
+      t = dp_t;
+      k0 = 0;
+      k1 = s.nk;
+      dp_t += gridDim.x;
+    } else if (it < r1) {
+      t = it / s.nk;
+      k0 = it - t * s.nk;
+      k1 = min(s.nk, r1 - t * s.nk);
+      it = t * s.nk + k1;
+    } else {
+      break;
+    }
+    const int tb = t * s.nk;
+    int tm, tn;
+    group_coords<4>(t, ntm, ntn, tm, tn);
+    const int bm = tm * BBM, bn = tn * BN;
+
+    const char* a_src[C::NLA];
+    int a_sc[C::NLA];
+    int cv_base[C::NLA], cv_iy[C::NLA], cv_ix[C::NLA];
+    const char* w_src[C::NLB];
+    int w_sc[C::NLB];
+#pragma unroll
+    for (int i = 0; i < C::NLA; ++i) {
+      const int r = (i * 8 + wave) * C::RPI + lrow;
+      a_sc[i] = pos ^ swz<RB>(r);
+      const int m = min(bm + r, p.M - 1);
+      if constexpr (AMODE == 0) {
+        a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + a_sc[i] * 8) * 2;
+      } else {
+        const int hw = p.cv_OH * p.cv_OW;
+        const int img = m / hw, rem = m - img * hw;
+        const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
+        cv_base[i] = img * p.cv_IH * p.cv_IW;
+        cv_iy[i] = oy * p.cv_stride - 1;
+        cv_ix[i] = ox * p.cv_stride - 1;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < C::NLB; ++i) {
+      const int r = (i * 8 + wave) * C::RPI + lrow;
+      w_sc[i] = pos ^ swz<RB>(r);
+      const int n = min(bn + r, p.N - 1);
+      w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + w_sc[i] * 8) * 2;
+    }
+
+    f32x4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int slot) __attribute__((always_inline)) {
+      const char* As = lds + slot * C::STAGE;
+      const char* Bs = As + C::A_BYTES;
+      b8 a[C::KG][C::FM], b[C::KG][C::FN];
+#pragma unroll
+      for (int kg = 0; kg < C::KG; ++kg) {
+        const int chunk = kg * 4 + g;
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int rb = wn * C::TN + j * 16 + r16;
+          b[kg][j] = *reinterpret_cast<const b8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const int ra = wm * C::TM + i * 16 + r16;
+          a[kg][i] = *reinterpret_cast<const b8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
+        }
+      }
+#pragma unroll
+      for (int kg = 0; kg < C::KG; ++kg) {
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kg][i], b[kg][j], acc[i][j], 0, 0, 0);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+      }
+    };
+
+    // ring of STAGES slots over K tiles k0 .. k1-1 (same pipeline as gemm_big_kernel)
+    const int n = k1 - k0;
+#pragma unroll
+    for (int s0 = 0; s0 < STAGES - 1; ++s0)
+      if (s0 < n)
+        stage_big<AMODE, BN, RB>(p, lds, s0, k0 + s0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src,
+                                 w_sc);
+    int slot = 0;
+    for (int kk = 0; kk < n; ++kk) {
+      const int ahead = min(STAGES - 2, n - 1 - kk);
+      if (ahead >= STAGES - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT * (STAGES - 2)) : "memory");
+      else if (STAGES > 3 && ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT * 2) : "memory");
+      else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (kk + STAGES - 1 < n) {
+        const int ns = slot == 0 ? STAGES - 1 : slot - 1;
+        stage_big<AMODE, BN, RB>(p, lds, ns, k0 + kk + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
+                                 cv_ix, w_src, w_sc);
+      }
+      compute(slot);
+      slot = slot + 1 == STAGES ? 0 : slot + 1;
+    }
+    __syncthreads();  // LDS free for the epilogue
+
+    const int lo = t < s.dp_tiles ? 0 : (tb - s.base) / s.per;
+    const int hi = t < s.dp_tiles ? 0 : (tb + s.nk - 1 - s.base) / s.per;
+    if (lo != hi) {
+      // split tile: publish this segment's partial sums.  Buffer stores/loads: the per-fragment offset is an
+      // SGPR (soffset), the only VGPR is the lane's 16-B column -> no hoisted 64-bit addresses across the
+      // persistent loop.
+      const int voff = lane * 16;
+      {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(s.slabs + sk_slab(vb, tb, s) * SLAB, 0, SLAB * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, voff,
+                                                   ((wave * C::FM + i) * C::FN + j) * 1024, 16);  // sc1
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+      __syncthreads();
+      if (tid == 0) {
+        const int ticket = __hip_atomic_fetch_add(&s.tickets[t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == hi - lo;
+        if (last) {
+          __hip_atomic_store(&s.tickets[t], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *last_word = last;
+      }
+      __syncthreads();
+      const int last = *last_word;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below the ticket
+      if (!last) continue;  // another contributor finishes this tile (LDS: the next segment re-stages after a
+                            // barrier, and last_word is outside the staging area)
+      // sum every contributor's slab (this block's included) in range order: bit-reproducible whatever the
+      // arrival order.  Half a slab (8 x 16 B per lane) in flight at a time: the (dead) accumulators plus 32 VGPRs.
+      for (int b = lo; b <= hi; ++b) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(s.slabs + sk_slab(b, tb, s) * SLAB, 0, SLAB * 4, 0x00020000);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          f32x4 v[C::FM / 2][C::FN];
+#pragma unroll
+          for (int i = 0; i < C::FM / 2; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+              v[i][j] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                             rs, voff, ((wave * C::FM + h * (C::FM / 2) + i) * C::FN + j) * 1024, 16));
+#pragma unroll
+          for (int i = 0; i < C::FM / 2; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) {
+              f32x4& a = acc[h * (C::FM / 2) + i][j];
+              a = b == lo ? v[i][j] : a + v[i][j];
+            }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+
+    // ---- fused epilogue (as gemm_big_kernel) ----
+    float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
+    const int c4 = (lane & 15) * 4;
+    const int n0 = bn + wn * C::TN + c4;
+    const EpiCol ec = epi_col_setup(p, n0);
+#pragma unroll
+    for (int part = 0; part < C::FM / 2; ++part) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (n0 < p.N) {
+#pragma unroll 2
+        for (int pass = 0; pass < 8; ++pass) {
+          const int rloc = pass * 4 + g;
+          const int m = bm + wm * C::TM + part * 32 + rloc;
+          if (m >= p.M) break;
+          epi_store_row<bf16_t>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c4));
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();  // every wave done with the epilogue staging before the next segment's DMA
+  }
+}
+
 }  // namespace
 
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream) {
@@ -265,6 +529,70 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
   }
 #undef MAPA_BIG
   hipLaunchKernelGGL(k, dim3(nblk), dim3(BTHREADS), 0, stream, a);
+  return true;
+}
+
+
+// Stream-K variants: 0 = 256x128 / 64-B rows / 3 stages / setprio / 2 per CU, 1 = 256x256 / 64-B rows / 3 stages
+// / setprio / 1 per CU.  Workspace: [tickets: 64 Ki words][slabs: G * 2 * 256 * BN * 4].
+static int sk_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+static void sk_shape(int variant, int& bn, int& per_cu) {
+  bn = variant == 0 ? 128 : 256;
+  per_cu = variant == 0 ? 2 : 1;
+}
+
+// Ticket words live in a fixed-size head shared by every shape (a shape-dependent split would let one shape's slabs
+// overwrite another's tickets, which must stay zero between calls); shapes with more tiles use the DP schedule.
+constexpr int64_t SK_MAX_TILES = 65536, SK_TICKET_BYTES = SK_MAX_TILES * 4;
+
+int64_t streamk_workspace_bytes(int M, int N, int variant) {
+  if (variant < 0 || variant > 1) return 0;
+  int bn, per_cu;
+  sk_shape(variant, bn, per_cu);
+  const int64_t tiles = (int64_t)((M + BBM - 1) / BBM) * ((N + bn - 1) / bn);
+  if (tiles > SK_MAX_TILES) return 0;
+  const int64_t G = (int64_t)sk_cus() * per_cu;
+  return SK_TICKET_BYTES + G * 2 * BBM * bn * 4;
+}
+
+bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  if (variant < 0 || variant > 1 || !ws) return false;
+  const int64_t need = streamk_workspace_bytes(a.M, a.N, variant);
+  if (need == 0 || ws_bytes < need) return false;
+  int bn, per_cu;
+  sk_shape(variant, bn, per_cu);
+  const int bk = 32;  // 64-B LDS rows
+  const int64_t tiles = (int64_t)((a.M + BBM - 1) / BBM) * ((a.N + bn - 1) / bn);
+  const int64_t nk = (a.K + bk - 1) / bk;
+  if (tiles * nk >= (int64_t(1) << 31)) return false;
+  SkArgs s;
+  s.nk = (int)nk;
+  s.total = (int)(tiles * nk);
+  const int g = sk_cus() * per_cu;
+  // Data-parallel whole tiles for all but the last one-to-two waves; stream-K spreads the rest evenly, so at most
+  // ~one tile per block is split (each split costs a 128-256 KB slab write + read).
+  static const int dp_env = getenv("MAPA_SK_DP") ? atoi(getenv("MAPA_SK_DP")) : 1;  // tuning: 0 = pure stream-K
+  s.dp_tiles = (dp_env && tiles >= 2 * g) ? (int)((tiles / g - 1) * g) : 0;
+  s.base = s.dp_tiles * s.nk;
+  s.per = (s.total - s.base + g - 1) / g;
+  static const int per_env = getenv("MAPA_SK_PER") ? atoi(getenv("MAPA_SK_PER")) : 0;  // tuning: iterations/block
+  if (per_env > s.per) s.per = per_env;  // only coarser: G stays within the workspace's slab count
+  const int G = (s.total - s.base + s.per - 1) / s.per;
+  s.tickets = reinterpret_cast<int*>(ws);
+  s.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + SK_TICKET_BYTES);
+  void (*k)(GemmArgs, SkArgs);
+  if (variant == 0) k = conv ? gemm_sk_kernel<1, 128, 64, 3, 1, 4> : gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
+  else k = conv ? gemm_sk_kernel<1, 256, 64, 3, 1, 1> : gemm_sk_kernel<0, 256, 64, 3, 1, 1>;
+  hipLaunchKernelGGL(k, dim3(G), dim3(BTHREADS), 0, stream, a, s);
   return true;
 }
 

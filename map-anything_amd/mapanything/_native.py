@@ -22,7 +22,8 @@ ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_POST = 0, 1, 2, 3
 
 # Every extern "C" symbol declared in include/mapa.h (checked by tests/test_capi.py).
 EXPORTED = (
-    "mapa_last_error", "mapa_version", "mapa_device_check", "mapa_gemm", "mapa_attention", "mapa_layernorm",
+    "mapa_last_error", "mapa_version", "mapa_device_check", "mapa_gemm", "mapa_gemm_workspace_bytes",
+    "mapa_gemm_set_variant", "mapa_attention", "mapa_layernorm",
     "mapa_patchify", "mapa_assemble_tokens", "mapa_add_rowvec", "mapa_bilinear_ac", "mapa_mean_tokens",
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
@@ -41,7 +42,7 @@ class GemmDesc(ctypes.Structure):
         ("resid1", ctypes.c_void_p), ("resid2", ctypes.c_void_p), ("out_f32", ctypes.c_void_p),
         ("out_lp", ctypes.c_void_p), ("out_lp_relu", ctypes.c_void_p), ("ldo", ctypes.c_int64),
         ("out_mode", ctypes.c_int), ("ps_s", ctypes.c_int), ("ps_h", ctypes.c_int), ("ps_w", ctypes.c_int),
-        ("ps_cout", ctypes.c_int),
+        ("ps_cout", ctypes.c_int), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
     ]
 
 
@@ -80,6 +81,9 @@ def load_library(path: Optional[str] = None):
     L.mapa_version.restype = i
     L.mapa_device_check.argtypes = [i]
     L.mapa_gemm.argtypes = [ctypes.POINTER(GemmDesc), vp]
+    L.mapa_gemm_workspace_bytes.argtypes = [ctypes.POINTER(GemmDesc)]
+    L.mapa_gemm_workspace_bytes.restype = i64
+    L.mapa_gemm_set_variant.argtypes = [i]
     L.mapa_attention.argtypes = [ctypes.POINTER(AttnDesc), vp]
     L.mapa_layernorm.argtypes = [vp, i64, i, i, vp, vp, f, vp, vp, i, i64, i, i64, i, vp]
     L.mapa_patchify.argtypes = [vp, i, i, i, vp, i, i, vp]
@@ -184,6 +188,29 @@ def _toc(tok, kind, flops=0.0):
 
 
 # ------------------------------------------------------------------------------------------------ wrappers
+_WS_NEED = {}
+_WS = {}
+
+
+def gemm_workspace(nbytes: int) -> torch.Tensor:
+    """Zero-filled GEMM scratch (stream-K tickets + partial-sum slabs) for the current device and stream.
+
+    mapa_gemm leaves it zeroed after every call; one buffer per stream because concurrent calls must not share it.
+    Grown (re-allocated zeroed, stream-ordered) when a larger problem needs more."""
+    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = _WS[key] = torch.zeros(max(nbytes, 0 if ws is None else ws.numel()), dtype=torch.uint8,
+                                    device="cuda")
+    return ws
+
+
+def gemm_set_variant(variant: int = 0):
+    """Force one GEMM kernel variant (0 = automatic); see include/mapa.h."""
+    check(lib().mapa_gemm_set_variant(variant), "mapa_gemm_set_variant")
+    _WS_NEED.clear()
+
+
 def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_NONE, resid1=None, resid2=None,
          out_f32=None, out_lp=None, out_lp_relu=None, ldo=None, conv=None, pixshuf=None):
     """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout)."""
@@ -212,6 +239,13 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     if pixshuf is not None:
         d.out_mode = OUT_PIXSHUF
         d.ps_s, d.ps_h, d.ps_w, d.ps_cout = pixshuf
+    key = (d.dtype, M, N, K, d.a_mode)
+    need = _WS_NEED.get(key)
+    if need is None:
+        need = _WS_NEED[key] = int(lib().mapa_gemm_workspace_bytes(ctypes.byref(d)))
+    if need:
+        ws = gemm_workspace(need)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     tok = _tic()
     check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
     _toc(tok, "conv3x3" if conv is not None else "gemm", 2.0 * M * N * K)

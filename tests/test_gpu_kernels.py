@@ -62,6 +62,49 @@ def test_gemm_epilogues(nat):
     assert rel_l2(x.cpu(), (r1 + g * acc).cpu()) < 1e-4
 
 
+@pytest.mark.parametrize("variant", [2580, 2581, 2571, 2568])
+@pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72)])
+def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
+    """Every 256-row schedule, incl. the stream-K ones (split tiles summed by the last arriver), on the path's
+    narrow-N shapes and on ragged tails; stream-K must be bit-reproducible and leave its workspace zeroed."""
+    A = _rand(M, K, seed=21).to(torch.bfloat16)
+    W = _rand(N, K, scale=K ** -0.5, seed=22).to(torch.bfloat16)
+    b, g, r = _rand(N, seed=23), _rand(N, seed=24), _rand(M, N, seed=25)
+    ref = r + g * (A.float() @ W.float().t() + b)
+    out = torch.empty(M, N, device="cuda")
+    lp = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=r, out_f32=out, out_lp=lp)
+        again = torch.empty_like(out)
+        nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=r, out_f32=again)
+        torch.cuda.synchronize()
+    finally:
+        nat.gemm_set_variant(0)
+    assert rel_l2(out.cpu(), ref.cpu()) < 1e-4
+    assert rel_l2(lp.float().cpu(), ref.cpu()) < 5e-3
+    assert torch.equal(out, again)
+    if variant >= 2580:  # tickets (the workspace head) back to zero for the next call
+        ws = nat.gemm_workspace(0)
+        assert ws.numel() > 0 and int(ws[: 4 * 65536].count_nonzero()) == 0
+
+
+@pytest.mark.parametrize("variant", [2580, 2581])
+def test_conv3x3_streamk(nat, variant):
+    n, H, W, C, Co = 2, 37, 37, 256, 256
+    x = _rand(n, C, H, W, seed=26).to(torch.bfloat16)
+    w = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=27).to(torch.bfloat16)
+    ref = F.conv2d(x.float(), w.float(), None, padding=1)
+    out = torch.empty(n * H * W, Co, device="cuda")
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(x.permute(0, 2, 3, 1).contiguous(), w.permute(0, 2, 3, 1).reshape(Co, -1).contiguous(), n * H * W,
+                 Co, 9 * C, out_f32=out, conv=(C, H, W, H, W, 1))
+    finally:
+        nat.gemm_set_variant(0)
+    assert rel_l2(out.view(n, H, W, Co).permute(0, 3, 1, 2).cpu(), ref.cpu()) < 1e-4
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("n,H,W,C,Co,stride", [(2, 19, 19, 96, 256, 1), (1, 37, 37, 768, 768, 2),
                                               (3, 16, 20, 128, 128, 1), (1, 8, 8, 256, 6, 1)])

@@ -1,5 +1,6 @@
 """Kernel micro-benchmark: TFLOP/s of the hot GEMM / conv / attention shapes of the 8-view 518x518 workload
-(HIP-event timing, random data).  Usage: python tools/kbench.py [gemm|attn|conv|all] [reps]"""
+(HIP-event timing, random data).  Usage: python tools/kbench.py [gemm|attn|conv|all] [reps]
+KB_VARIANTS=0,2580,2568 sweeps GEMM/conv kernel variants (0 = the automatic choice; include/mapa.h)."""
 import os
 import sys
 
@@ -17,6 +18,7 @@ GEMMS = [("enc.qkv", R, 3072, 1024), ("enc.proj", R, 1024, 1024), ("enc.fc1", R,
 if os.environ.get("KB_SQ"):
     GEMMS = [("sq4096", 4096, 4096, 4096), ("sq8192", 8192, 8192, 8192)]
 ONLY = os.environ.get("KB_ONLY")
+VARIANTS = [int(v) for v in os.environ.get("KB_VARIANTS", "0").split(",")]
 if ONLY:
     GEMMS = [g for g in GEMMS if g[0] in ONLY.split(",")]
 CONVS = [("rn1.c@148", V, 148, 148, 256, 256), ("reg.c2@518", V, 518, 518, 128, 128),
@@ -48,10 +50,14 @@ def main():
             W = (torch.randn(N, K, device="cuda") * K ** -0.5).to(dt)
             b = torch.randn(N, device="cuda")
             o = torch.empty(M, N, device="cuda", dtype=dt)
-            ms = timeit(lambda: nat.gemm(A, W, M, N, K, bias=b, out_lp=o), reps)
-            ms_t = timeit(lambda: torch.nn.functional.linear(A, W, b.to(dt)), reps) if "torch" in sys.argv else 0
-            print(f"gemm {name:10s} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s"
-                  + (f"   [hipBLASLt via torch: {2*M*N*K/ms_t/1e9:7.1f} TF/s]" if ms_t else ""), flush=True)
+            for var in VARIANTS:
+                nat.gemm_set_variant(var)
+                ms = timeit(lambda: nat.gemm(A, W, M, N, K, bias=b, out_lp=o), reps)
+                ms_t = (timeit(lambda: torch.nn.functional.linear(A, W, b.to(dt)), reps)
+                        if "torch" in sys.argv and var == VARIANTS[0] else 0)
+                print(f"gemm {name:10s} v{var:<4d} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s"
+                      + (f"   [hipBLASLt via torch: {2*M*N*K/ms_t/1e9:7.1f} TF/s]" if ms_t else ""), flush=True)
+            nat.gemm_set_variant(0)
     if what in ("conv", "all"):
         for name, n, H, W_, C, Co in CONVS:
             x = (torch.randn(n, H, W_, C, device="cuda") * 0.5).to(dt)
@@ -59,9 +65,12 @@ def main():
             b = torch.randn(Co, device="cuda")
             o = torch.empty(n * H * W_, Co, device="cuda", dtype=dt)
             M = n * H * W_
-            ms = timeit(lambda: nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1)), reps)
-            print(f"conv {name:10s} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  {2*M*Co*9*C/ms/1e9:7.1f} TF/s",
-                  flush=True)
+            for var in VARIANTS:
+                nat.gemm_set_variant(var)
+                ms = timeit(lambda: nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1)), reps)
+                print(f"conv {name:10s} v{var:<4d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
+                      f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
+            nat.gemm_set_variant(0)
     if what in ("attn", "all"):
         for name, B, Hh, S in [("enc", V, 16, T + 1), ("frame", V, 12, T), ("global", 1, 12, L)]:
             C = Hh * 64
