@@ -236,6 +236,222 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
 }
 
 
+// ---- ping-pong schedule: two wave groups offset by one barrier ------------------------------------------------
+// 256x256 tile, 32-deep K tiles (64-B LDS rows), a ring of NBUF K-tile buffers (32 KiB each).  Waves 0-3 (group 0,
+// output rows 0-127) and 4-7 (group 1, rows 128-255) run the same program, group 1 one barrier behind, so on every
+// SIMD one wave issues its 16-MFMA cluster while the other reads its next fragments from LDS and issues LDS-DMA:
+//   per K tile t, per wave:  [stage A(t+D); read A0..3, B0..3; lgkm(0)] bar [16 MFMA] bar
+//                            [stage B(t+D); vmcnt -> tile t+1 landed; read A4..7; lgkm(0)] bar [16 MFMA] bar
+// RAW: every wave's vmcnt for tile t+1 precedes global barrier 4t+4 (group 1's one barrier later than group 0's),
+// and the first reads of tile t+1 follow it.  WAR: tile t+D (D = NBUF-1) overwrites tile t-1's buffer, whose last
+// reads (group 1, before global barrier 4t) were retired by lgkmcnt(0) before that barrier.
+template <int AMODE, int NBUF>
+__global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
+  using C = Cfg<256, 64>;
+  constexpr int DIST = NBUF - 1;
+  constexpr int MAIN = NBUF * C::STAGE;
+  constexpr int LDS = MAIN > C::EPI ? MAIN : C::EPI;
+  static_assert(C::NLA == 2 && C::NLB == 2 && C::FM == 8 && C::FN == 4 && C::KG == 1, "geometry");
+  __shared__ __attribute__((aligned(1024))) char lds[LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  const int ntn = (p.N + 255) / 256, ntm = (p.M + BBM - 1) / BBM;
+  int tm, tn;
+  tile_coords<4>(blockIdx.x, ntm, ntn, tm, tn);
+  const int bm = tm * BBM, bn = tn * 256;
+
+  const int lrow = lane / C::CPR, pos = lane % C::CPR;
+  const char* a_src[C::NLA];
+  int a_sc[C::NLA];
+  int cv_base[C::NLA], cv_iy[C::NLA], cv_ix[C::NLA];
+  const char* w_src[C::NLB];
+  int w_sc[C::NLB];
+#pragma unroll
+  for (int i = 0; i < C::NLA; ++i) {
+    const int r = (i * 8 + wave) * C::RPI + lrow;
+    a_sc[i] = pos ^ swz<64>(r);
+    const int m = min(bm + r, p.M - 1);
+    if constexpr (AMODE == 0) {
+      a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + a_sc[i] * 8) * 2;
+    } else {
+      const int hw = p.cv_OH * p.cv_OW;
+      const int img = m / hw, rem = m - img * hw;
+      const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
+      cv_base[i] = img * p.cv_IH * p.cv_IW;
+      cv_iy[i] = oy * p.cv_stride - 1;
+      cv_ix[i] = ox * p.cv_stride - 1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < C::NLB; ++i) {
+    const int r = (i * 8 + wave) * C::RPI + lrow;
+    w_sc[i] = pos ^ swz<64>(r);
+    const int n = min(bn + r, p.N - 1);
+    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + w_sc[i] * 8) * 2;
+  }
+  const int nk = (p.K + C::BK - 1) / C::BK;
+  const bool k_exact = (p.K % C::BK) == 0;
+  const int lds_wave = wave * 1024;
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+
+  auto stage_a = [&](int buf, int kt) __attribute__((always_inline)) {
+    char* As = lds + buf * C::STAGE;
+#pragma unroll
+    for (int i = 0; i < C::NLA; ++i) {
+      const int kc = kt * C::BK + a_sc[i] * 8;
+      const bool kin = k_exact || kc < p.K;
+      const char* src;
+      if constexpr (AMODE == 0) {
+        src = kin ? a_src[i] + (int64_t)kt * C::BK * 2 : zero;
+      } else {
+        const int tap = kc / p.cv_C, ci = kc - tap * p.cv_C;
+        const int ky = tap / 3, kx = tap - ky * 3;
+        const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
+        const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+        src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * 2
+                 : zero;
+      }
+      __builtin_amdgcn_global_load_lds(src, As + lds_wave + i * 8192, 16, 0, 0);
+    }
+  };
+  auto stage_b = [&](int buf, int kt) __attribute__((always_inline)) {
+    char* Bs = lds + buf * C::STAGE + C::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < C::NLB; ++i) {
+      const int kc = kt * C::BK + w_sc[i] * 8;
+      const bool kin = k_exact || kc < p.K;
+      __builtin_amdgcn_global_load_lds(kin ? w_src[i] + (int64_t)kt * C::BK * 2 : zero, Bs + lds_wave + i * 8192, 16,
+                                       0, 0);
+    }
+  };
+
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  const int g = lane >> 4, r16 = lane & 15;
+  // fragment byte offsets inside a K-tile buffer (16-B chunk g of the 32-deep row, swizzled)
+  int a_off[C::FM], b_off[C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) {
+    const int ra = wm * C::TM + i * 16 + r16;
+    a_off[i] = ra * 64 + ((g ^ swz<64>(ra)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) {
+    const int rb = wn * C::TN + j * 16 + r16;
+    b_off[j] = C::A_BYTES + rb * 64 + ((g ^ swz<64>(rb)) << 4);
+  }
+
+  // prologue: K tiles 0 .. DIST-1 in flight; tile 0 landed everywhere before the first reads
+#pragma unroll
+  for (int s0 = 0; s0 < DIST; ++s0)
+    if (s0 < nk) {
+      stage_a(s0, s0);
+      stage_b(s0, s0);
+    }
+  {
+    const int later = min(DIST, nk) - 1;  // tiles after tile 0 in flight
+    if (later >= 3) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (later == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();  // group 1 runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  int buf = 0, sbuf = DIST % NBUF;
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* base = lds + buf * C::STAGE;
+    const bool stage = kt + DIST < nk;
+    // ---- phase A: rows 0-63 of the wave tile
+    if (stage) stage_a(sbuf, kt + DIST);
+    b8 bf[C::FN], af[4];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) bf[j] = *reinterpret_cast<const b8*>(base + b_off[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const b8*>(base + a_off[i]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase B: rows 64-127; tile kt+1 must have landed (this wave's DMA) before the next barrier
+    if (stage) stage_b(sbuf, kt + DIST);
+    {
+      const int later = min(DIST - 1, nk - 2 - kt);  // tiles after kt+1 whose DMA may stay in flight
+      if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *reinterpret_cast<const b8*>(base + a_off[4 + i]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+        acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    buf = buf + 1 == NBUF ? 0 : buf + 1;
+    sbuf = sbuf + 1 == NBUF ? 0 : sbuf + 1;
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();  // rejoin: group 1's last MFMA cluster ends at this barrier
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- epilogue (as gemm_big_kernel): every LDS read retired before the barriers above
+  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
+  const int c4 = (lane & 15) * 4;
+  const int n0 = bn + wn * C::TN + c4;
+  const EpiCol ec = epi_col_setup(p, n0);
+#pragma unroll
+  for (int part = 0; part < C::FM / 2; ++part) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (n0 < p.N) {
+#pragma unroll 2
+      for (int pass = 0; pass < 8; ++pass) {
+        const int rloc = pass * 4 + g;
+        const int m = bm + wm * C::TM + part * 32 + rloc;
+        if (m >= p.M) break;
+        epi_store_row<bf16_t>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c4));
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
 // ---- stream-K: persistent grid, contiguous K-iteration ranges ---------------------------------------------
 // The (tile, K-tile) iteration space [0, tiles * nk) is cut into G equal contiguous ranges, one per persistent
 // workgroup (G = CUs x occupancy), so every CU does the same number of MFMA K-steps however badly the tile count
@@ -503,8 +719,8 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream) {
   // variant: 0 = 256x256 / 128-B rows / 2 stages, 1 = 256x128 / 128 / 2, 2 = 256x256 / 64-B rows / 4 stages,
   //          3 = 256x128 / 64 / 4, 4 = 256x128 / 64 / 6, 5 = 256x128 / 128 / 3
-  static const int bns[12] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128};
-  if (variant < 0 || variant > 11) return false;
+  static const int bns[14] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128, 256, 256};
+  if (variant < 0 || variant > 13) return false;
   if (conv && (variant == 6 || variant == 7)) return false;  // diagnostics exist for dense A only
   const int BN = bns[variant];
   const int nblk = ((a.M + BBM - 1) / BBM) * ((a.N + BN - 1) / BN);
@@ -526,6 +742,9 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
     // two workgroups per CU (72 KiB LDS, <= 128 VGPRs): one tile's epilogue overlaps the other's main loop
     case 10: k = conv ? gemm_big_kernel<1, 128, 64, 3, 0, 0, 2> : gemm_big_kernel<0, 128, 64, 3, 0, 0, 2>; break;
     case 11: k = conv ? gemm_big_kernel<1, 128, 64, 3, 0, 1, 2> : gemm_big_kernel<0, 128, 64, 3, 0, 1, 2>; break;
+    // ping-pong wave groups, 32-deep K tiles in a ring of 4 / 5 buffers (128 / 160 KiB)
+    case 12: k = conv ? gemm_pp_kernel<1, 4> : gemm_pp_kernel<0, 4>; break;
+    case 13: k = conv ? gemm_pp_kernel<1, 5> : gemm_pp_kernel<0, 5>; break;
   }
 #undef MAPA_BIG
   hipLaunchKernelGGL(k, dim3(nblk), dim3(BTHREADS), 0, stream, a);

@@ -18,6 +18,7 @@ from __future__ import annotations
 import json
 import os
 import warnings
+from collections import OrderedDict
 from typing import Any, Dict, List, Optional
 
 import numpy as np
@@ -62,7 +63,7 @@ class MapAnything:
     def __init__(self, name: str, encoder_config: Dict, info_sharing_config: Dict, pred_head_config: Dict,
                  geometric_input_config: Dict, fusion_norm_layer=None, pretrained_checkpoint_path: str = None,
                  load_specific_pretrained_submodules: bool = False, specific_pretrained_submodules: list = None,
-                 torch_hub_force_reload: bool = False, precision: str = "bf16"):
+                 torch_hub_force_reload: bool = False, precision: str = "bf16", hip_graphs: bool = True):
         _check_config(encoder_config, info_sharing_config, pred_head_config)
         self.name = name
         self.encoder_config = encoder_config
@@ -81,6 +82,10 @@ class MapAnything:
         self._device = torch.device("cpu")
         self._comm = None
         self.training = False
+        # Replay the engine's ~2.7k launches per forward from a captured HIP graph (image-only, single device,
+        # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
+        self.hip_graphs = hip_graphs and os.environ.get("MAPA_HIP_GRAPHS", "1") != "0"
+        self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)
 
@@ -136,6 +141,7 @@ class MapAnything:
             raise KeyError(f"missing keys in state_dict: {missing[:5]} ... ({len(missing)})")
         self._sd = sd
         self._engines.clear()
+        self._graphs.clear()
         return self
 
     def load_synthetic_weights(self):
@@ -144,6 +150,7 @@ class MapAnything:
 
         self._sd = synthetic_state_dict(canonical_spec())
         self._engines.clear()
+        self._graphs.clear()
         return self
 
     # ------------------------------------------------------------------------------------ nn.Module-ish
@@ -257,9 +264,42 @@ class MapAnything:
         local, plan = self._local_views(views)
         geo = self._geo_inputs(views, plan, self._metric_flags(views))
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
-        raw = self.engine(precision).run(imgs, shard=plan, comm=self._comm, geo=geo,
-                                         dpt_chunk=self._dpt_chunk(memory_efficient_inference))
+        raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference))
         return self._assemble(split_views(raw, len(local), with_post=False), plan, len(views))
+
+    _MAX_GRAPHS = 4
+
+    def _run_engine(self, eng, imgs, plan, geo, dpt_chunk):
+        """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: one device, no
+        geometric inputs, no chunked dense head, no per-launch kernel timing.  The graph is keyed on the image
+        batch shape and precision; inputs are copied into its static buffer and outputs cloned out of it, so
+        results never alias a later call's."""
+        if (not self.hip_graphs or plan is not None or geo is not None or dpt_chunk is not None
+                or nat._timing is not None or imgs.device.type != "cuda"):
+            return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk)
+        key = (eng.precision, tuple(imgs.shape), imgs.device.index)
+        with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
+            entry = self._graphs.get(key)
+            if entry is None:
+                static_in = imgs.clone()
+                side = torch.cuda.Stream(imgs.device)
+                side.wait_stream(torch.cuda.current_stream(imgs.device))
+                with torch.cuda.stream(side):  # eager warm-up: lazy packing, pos-embed caches
+                    eng.run(static_in)
+                torch.cuda.current_stream(imgs.device).wait_stream(side)
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    static_out = eng.run(static_in)
+                entry = (graph, static_in, static_out)
+                self._graphs[key] = entry
+                while len(self._graphs) > self._MAX_GRAPHS:
+                    self._graphs.popitem(last=False)
+            else:
+                self._graphs.move_to_end(key)
+            graph, static_in, static_out = entry
+            static_in.copy_(imgs)
+            graph.replay()
+        return {k: v.clone() for k, v in static_out.items()}
 
     @torch.inference_mode()
     def infer(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False, use_amp: bool = True,
@@ -296,8 +336,7 @@ class MapAnything:
                                use_pose_scale=not ignore_pose_scale_inputs)
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
         eng = self.engine(precision)
-        raw = eng.run(imgs, shard=plan, comm=self._comm, geo=geo,
-                      dpt_chunk=self._dpt_chunk(memory_efficient_inference))
+        raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference))
         post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
                                    mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
                                    edge_depth_threshold=edge_depth_threshold,
