@@ -270,11 +270,17 @@ void launch_variant(int variant, int nblk, hipStream_t stream, const GemmArgs& a
 // Kernel choice per shape, from tools/kbench.py sweeps of the path's shapes on MI355X (TF/s in DESIGN.md):
 //   2568 = 256x256 tile, 1 workgroup/CU, s_setprio around the MFMA bursts (long K, wide convs)
 //   2570/2571 = 256x128 tile, 2 workgroups/CU (one tile's epilogue overlaps the other's main loop)
+//   2574 = 192x256 tile, 1 workgroup/CU (tile quantization: more tiles in the one wave)
 //   1282 / 643 = 128x128 tiles (fp32 parity mode; problems too small to fill the chip with 256-row tiles)
 int pick_variant(int dtype, bool conv, int M, int N, int K) {
   if (dtype != MAPA_BF16) return (conv || K < 1024) ? 643 : 1282;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
   if (big_tiles < 256) return (conv || K < 1024) ? 643 : 1282;
+  // 192x256 tiles when they fit one wave on the CUs and 256-row tiles leave a quarter of them idle: the path's
+  // N <= 1024 linears at 8 views (M = 10960: 58 vs 43 row tiles) and the 74x74 DPT convs
+  const int64_t t192 = (int64_t)((M + 191) / 192) * ((N + 255) / 256);
+  const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  if (t192 <= 256 && t256 <= 192 && N >= 256) return 2574;
   if (conv) return N >= 256 ? 2568 : 2571;
   if (K >= 4096) return 2568;
   if (N >= 3072 && K <= 1024) return 2570;
@@ -354,7 +360,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
   if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
-  } else if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2573 &&
+  } else if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2574 &&
              launch_gemm_big(a, conv, variant - 2560, stream)) {
     // launched
   } else if (d->dtype == MAPA_BF16) {
@@ -370,7 +376,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2573) || variant == 2580 || variant == 2581,
+                     (variant >= 2560 && variant <= 2574) || variant == 2580 || variant == 2581,
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;

@@ -20,19 +20,21 @@ constexpr int BBM = 256, BTHREADS = 512, BBK = 64, ROWB = 128;  // ROWB: LDS byt
 constexpr int ELD = 68;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));                                           // epilogue fp32 row stride (TN = 64 + 4 pad)
 
-template <int BN, int RB>
+template <int BN, int RB, int BM = BBM>
 struct Cfg {
   static constexpr int WM = BN == 256 ? 2 : 4;
   static constexpr int WN = 8 / WM;
-  static constexpr int TM = BBM / WM, TN = BN / WN;  // TN = 64 in both
+  static constexpr int TM = BM / WM, TN = BN / WN;  // TN = 64 (256-wide) or 32..64
   static constexpr int FM = TM / 16, FN = TN / 16;
   static constexpr int CPR = RB / 16;                // 16-B chunks per LDS row
   static constexpr int BK = CPR * 8;                 // K per tile (bf16)
   static constexpr int KG = CPR / 4;                 // 32-deep MFMA k-groups per tile
   static constexpr int RPI = 1024 / RB;              // rows per 1-KiB wave instruction
-  static constexpr int A_BYTES = BBM * RB, B_BYTES = BN * RB;
+  static constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB;
   static constexpr int STAGE = A_BYTES + B_BYTES;
-  static constexpr int NLA = BBM / (8 * RPI), NLB = BN / (8 * RPI);  // wave instructions per thread per tile
+  static constexpr int NLA = BM / (8 * RPI), NLB = BN / (8 * RPI);  // wave instructions per thread per tile
+  static_assert(BM % (8 * RPI) == 0 && BN % (8 * RPI) == 0, "whole 1-KiB wave instructions per operand");
+  static_assert(TN == 64 && FM % 2 == 0, "epilogue: 64-column wave tiles, 32-row passes");
   static constexpr int EPI = 8 * 32 * ELD * 4;
 };
 
@@ -45,12 +47,12 @@ __device__ __forceinline__ int swz(int row) {
 }
 
 // LDS-DMA of K tile kt into stage buf: NLA 1-KiB wave instructions of A rows, NLB of W rows per wave.
-template <int AMODE, int BN, int RB>
+template <int AMODE, int BN, int RB, int BM = BBM>
 __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf, int kt, int lds_wave, bool k_exact,
                                           const char* const* a_src, const int* a_sc, const int* cv_base,
                                           const int* cv_iy, const int* cv_ix, const char* const* w_src,
                                           const int* w_sc) {
-  using C = Cfg<BN, RB>;
+  using C = Cfg<BN, RB, BM>;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   char* As = lds + buf * C::STAGE;
   char* Bs = As + C::A_BYTES;
@@ -80,9 +82,9 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
   }
 }
 
-template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1>
+template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1, int BM = BBM>
 __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
-  using C = Cfg<BN, RB>;
+  using C = Cfg<BN, RB, BM>;
   constexpr int MAIN = STAGES * C::STAGE;
   constexpr int LDS = MAIN > C::EPI ? MAIN : C::EPI;
   constexpr int NPT = C::NLA + C::NLB;  // LDS-DMA instructions per thread per K tile
@@ -91,10 +93,10 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
-  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BBM - 1) / BBM;
+  const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   int tm, tn;
   tile_coords<4>(blockIdx.x, ntm, ntn, tm, tn);
-  const int bm = tm * BBM, bn = tn * BN;
+  const int bm = tm * BM, bn = tn * BN;
 
   // ---- staging geometry: wave instruction i of this wave covers rows (i*8 + wave)*RPI .. +RPI-1
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
@@ -169,11 +171,11 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   };
 
   if constexpr (STAGES == 2) {
-    stage_big<AMODE, BN, RB>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
+    stage_big<AMODE, BN, RB, BM>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // tile kt landed (vmcnt(0) before the barrier); every wave is done with tile kt-1
       if (kt + 1 < nk && DIAG != 1)
-        stage_big<AMODE, BN, RB>(p, lds, (kt + 1) & 1, kt + 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
+        stage_big<AMODE, BN, RB, BM>(p, lds, (kt + 1) & 1, kt + 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
                                  cv_ix, w_src, w_sc);
       if (DIAG != 2) compute(kt & 1);
     }
@@ -182,7 +184,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
       if (s0 < nk)
-        stage_big<AMODE, BN, RB>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
+        stage_big<AMODE, BN, RB, BM>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
     int slot = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int ahead = min(STAGES - 2, nk - 1 - kt);  // tiles issued after kt that may still be in flight
@@ -195,7 +197,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
       __builtin_amdgcn_sched_barrier(0);
       if (kt + STAGES - 1 < nk) {
         const int ns = slot == 0 ? STAGES - 1 : slot - 1;  // (kt + STAGES - 1) % STAGES
-        stage_big<AMODE, BN, RB>(p, lds, ns, kt + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
+        stage_big<AMODE, BN, RB, BM>(p, lds, ns, kt + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
                                  cv_ix, w_src, w_sc);
       }
       compute(slot);
@@ -719,11 +721,13 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream) {
   // variant: 0 = 256x256 / 128-B rows / 2 stages, 1 = 256x128 / 128 / 2, 2 = 256x256 / 64-B rows / 4 stages,
   //          3 = 256x128 / 64 / 4, 4 = 256x128 / 64 / 6, 5 = 256x128 / 128 / 3
-  static const int bns[14] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128, 256, 256};
-  if (variant < 0 || variant > 13) return false;
+  static const int bns[15] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128, 256, 256, 256};
+  static const int bms[15] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 192};
+  if (variant < 0 || variant > 14) return false;
   if (conv && (variant == 6 || variant == 7)) return false;  // diagnostics exist for dense A only
   const int BN = bns[variant];
-  const int nblk = ((a.M + BBM - 1) / BBM) * ((a.N + BN - 1) / BN);
+  const int BMv = bms[variant];
+  const int nblk = ((a.M + BMv - 1) / BMv) * ((a.N + BN - 1) / BN);
   void (*k)(GemmArgs) = nullptr;
 #define MAPA_BIG(V, BN_, RB_, S_) \
   case V: k = conv ? gemm_big_kernel<1, BN_, RB_, S_> : gemm_big_kernel<0, BN_, RB_, S_>; break;
@@ -745,6 +749,10 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
     // ping-pong wave groups, 32-deep K tiles in a ring of 4 / 5 buffers (128 / 160 KiB)
     case 12: k = conv ? gemm_pp_kernel<1, 4> : gemm_pp_kernel<0, 4>; break;
     case 13: k = conv ? gemm_pp_kernel<1, 5> : gemm_pp_kernel<0, 5>; break;
+    // 192-row tiles: 10960 rows -> 58 row tiles, so N = 1024 gives 232 tiles for 256 CUs (256-row: 172)
+    case 14:
+      k = conv ? gemm_big_kernel<1, 256, 128, 2, 0, 1, 1, 192> : gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192>;
+      break;
   }
 #undef MAPA_BIG
   hipLaunchKernelGGL(k, dim3(nblk), dim3(BTHREADS), 0, stream, a);
