@@ -163,6 +163,13 @@ int mapa_dense_head_out(const void* hidden, int dtype, int n, int HW, const floa
                         float* pts3d_cam, float* rays, float* depth, float* conf, float* logits, uint8_t* mask,
                         mapa_stream_t stream);
 
+/* Dense adaptor on its own (RayDirectionsPlusDepthWithConfidenceAndMaskAdaptor, adaptors.py:1898-1951 ->
+ * 1740-1796, 393-523, 1012-1073, 1114-1133), for the module-level API (model.dense_adaptor): raw [n][HW][6] f32
+ * (the regressor's conv1x1 output rows) -> NCHW f32 planes value [n][4][HW] = (ray / max(|ray|, 1e-8), exp(depth)),
+ * conf [n][HW] = 1 + exp(c), logits [n][HW], mask [n][HW] = sigmoid(logits). */
+int mapa_dense_adaptor(const float* raw, int n, int64_t HW, float* value, float* conf, float* logits, float* mask,
+                       mapa_stream_t stream);
+
 /* infer() post-processing (inference.py:407-480): mask_out = mask_in & ~(depth_edge & normal_edge) per view
  * (geometry.py:1788-1853, 2102-2145, 2200-2258).  pts3d/pts3d_cam [n][H][W][3] f32 (depth_z = pts3d_cam z),
  * masks u8 [n][H][W].  work: n*H*W*17 bytes of scratch when use_edges. */

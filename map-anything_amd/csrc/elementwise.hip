@@ -274,6 +274,28 @@ __global__ void __launch_bounds__(256) dense_head_out_kernel(
   }
 }
 
+// Dense adaptor alone (module-level API): raw conv1x1 rows [n][HW][6] -> NCHW planes value [n][4][HW] (unit ray,
+// exp depth), conf [n][HW] = 1 + exp, logits [n][HW], mask [n][HW] = sigmoid (the probability, as MaskAdaptor).
+__global__ void __launch_bounds__(256) dense_adaptor_kernel(const float* __restrict__ raw, int n, int64_t HW,
+                                                            float* __restrict__ value, float* __restrict__ conf,
+                                                            float* __restrict__ logits, float* __restrict__ mask) {
+  const int64_t total = (int64_t)n * HW;
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < total; p += (int64_t)gridDim.x * blockDim.x) {
+    const float* r = raw + p * 6;
+    const int64_t v = p / HW, i = p - v * HW;
+    const float rx = r[0], ry = r[1], rz = r[2];
+    const float nr = fmaxf(sqrtf(rx * rx + ry * ry + rz * rz), 1e-8f);
+    float* val = value + v * 4 * HW + i;
+    val[0] = rx / nr;
+    val[HW] = ry / nr;
+    val[2 * HW] = rz / nr;
+    val[3 * HW] = expf(r[3]);
+    conf[p] = 1.f + expf(r[4]);
+    logits[p] = r[5];
+    mask[p] = 1.f / (1.f + expf(-r[5]));
+  }
+}
+
 __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, int rows, int cols, void* dst,
                                     int bf, int64_t ldd) {
   const int64_t total = (int64_t)rows * cols;
@@ -405,6 +427,16 @@ extern "C" int mapa_dense_head_out(const void* hidden, int dtype, int n, int HW,
     hipLaunchKernelGGL(dense_head_out_kernel<float>, g, b, 0, stream, (const float*)hidden, n, HW, w6, b6, pose_out,
                        scale, batch, pts3d, pts3d_cam, rays, depth, conf, logits, mask);
   MAPA_CHECK_LAUNCH("mapa_dense_head_out");
+  return 0;
+}
+
+extern "C" int mapa_dense_adaptor(const float* raw, int n, int64_t HW, float* value, float* conf, float* logits,
+                                  float* mask, hipStream_t stream) {
+  MAPA_CHECK_ARG(raw && value && conf && logits && mask && n > 0 && HW > 0, "mapa_dense_adaptor: bad args");
+  const int64_t total = (int64_t)n * HW;
+  hipLaunchKernelGGL(dense_adaptor_kernel, dim3(grid_for(total)), dim3(TPB), 0, stream, raw, n, HW, value, conf,
+                     logits, mask);
+  MAPA_CHECK_LAUNCH("mapa_dense_adaptor");
   return 0;
 }
 

@@ -28,7 +28,7 @@ EXPORTED = (
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
-    "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge",
+    "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
 )
 
 
@@ -108,6 +108,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_apply_mask.argtypes = [vp, vp, vp, vp, i64, vp]
     L.mapa_confidence_mask.argtypes = [vp, vp, vp, i, i64, f, vp]
     L.mapa_attn_merge.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i64, vp]
+    L.mapa_dense_adaptor.argtypes = [vp, i, i64, vp, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -391,3 +392,9 @@ def confidence_mask(conf, mask_in, mask_out, n, HW, q):
 def attn_merge(o_a, lse_a, o_b, lse_b, o_out, rows, heads, ld, lse_out=None):
     check(lib().mapa_attn_merge(ptr(o_a), ptr(lse_a), ptr(o_b), ptr(lse_b), ptr(o_out), ptr(lse_out),
                                 dt_code(o_a.dtype), rows, heads, ld, stream()), "mapa_attn_merge")
+
+
+def dense_adaptor(raw, n, HW, value, conf, logits, mask):
+    """raw [n][HW][6] f32 -> value [n][4][HW], conf / logits / mask [n][HW] (NCHW planes; include/mapa.h)."""
+    check(lib().mapa_dense_adaptor(ptr(raw), n, HW, ptr(value), ptr(conf), ptr(logits), ptr(mask), stream()),
+          "mapa_dense_adaptor")

@@ -283,6 +283,26 @@ class MapaEngine:
         VB, _, H, W = imgs.shape
         hp, wp = H // PATCH, W // PATCH
         T = hp * wp
+        enc = self.encoder_features(imgs)
+        if taps is not None:
+            taps["encoder"] = enc.clone()
+        if geo is not None and not geo.empty():
+            self.geometric(enc, geo, VB, H, W)
+        fused_lp = self._empty(VB * T + 1, ENC_DIM)
+        fused_f32 = self._empty(VB * T, ENC_DIM, dtype=torch.float32) if taps is not None else None
+        self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
+        nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
+        if taps is not None:
+            taps["fused"] = fused_f32
+        return fused_lp, (hp, wp)
+
+    def encoder_features(self, imgs):
+        """DINOv2Encoder.forward (dinov2.py:146-178): patch embed + cls + pos-embed, 24 blocks, final norm.
+        Returns the patch-token features [VB*T][1024] f32 (cls dropped)."""
+        w = self.w
+        VB, _, H, W = imgs.shape
+        hp, wp = H // PATCH, W // PATCH
+        T = hp * wp
         R = VB * (T + 1)
         patches = self._empty(VB * T, KPAD)
         nat.patchify(imgs, VB, H, W, patches, KPAD)
@@ -298,18 +318,7 @@ class MapaEngine:
         del xn, qkv, ao, hbuf
         enc = self._empty(VB * T, ENC_DIM, dtype=torch.float32)
         self._ln(x, VB * T, ENC_DIM, w.enc_nw, w.enc_nb, y_f32=enc, group=T, gstride=T + 1, off=1)
-        del x
-        if taps is not None:
-            taps["encoder"] = enc.clone()
-        if geo is not None and not geo.empty():
-            self.geometric(enc, geo, VB, H, W)
-        fused_lp = self._empty(VB * T + 1, ENC_DIM)
-        fused_f32 = self._empty(VB * T, ENC_DIM, dtype=torch.float32) if taps is not None else None
-        self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
-        nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
-        if taps is not None:
-            taps["fused"] = fused_f32
-        return fused_lp, (hp, wp)
+        return enc
 
     # ------------------------------------------------------------------------------ geometric inputs
     def geometric(self, enc, geo: GeoInputs, VB, H, W):
@@ -456,6 +465,9 @@ class MapaEngine:
                 inter[d] = t_lp
                 if taps is not None:
                     taps[f"aat_l{d}"] = t_f
+                    tk = self._empty(1, AAT_DIM, dtype=torch.float32)  # the scale token, normed as well
+                    self._ln(y[VB * T:], 1, AAT_DIM, w.aat_nw, w.aat_nb, y_f32=tk)
+                    taps[f"aat_l{d}_token"] = tk
         del yn, qkv, ao, hbuf
         fin_lp = self._empty(L, AAT_DIM)
         fin_f32 = self._empty(L, AAT_DIM, dtype=torch.float32)
@@ -504,6 +516,12 @@ class MapaEngine:
     # ----------------------------------------------------------------------------------------------- DPT
     def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None):
         """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Returns the ReLU'd 128-ch hidden map at HxW."""
+        owned = [self.dpt_feature(fused_lp, l11, l17, fin_lp, VB, hp, wp, taps)[0]]
+        return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W)  # freed after its first conv
+
+    def dpt_feature(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, taps=None, want_f32=False):
+        """DPTFeature (dpt.py:180-232): the four IFR features [VB*T][C] (lp) -> the 256-ch map at 8x
+        [VB][8hp][8wp][256] (lp; f32 copy too if taps is given or want_f32)."""
         w = self.w
         n, T = VB, hp * wp
         lp = self.lp
@@ -555,9 +573,17 @@ class MapaEngine:
         o = self._fusion_two(n, h1, w1, 2, path, L1f, L1r)
         path = self._upsample_outconv(o, n, h1, w1, 2)
         o = self._fusion_two(n, h0, w0, 1, path, L0f, L0r)
-        feat_lp = self._upsample_outconv(o, n, h0, w0, 1, lowp=True, taps=taps)
-        hf, wf = 2 * h0, 2 * w0
-        # regressor: conv3x3 256->128 @8x, bilinear(ac) -> HxW, conv3x3 128->128 + ReLU
+        t = taps if taps is not None else ({} if want_f32 else None)
+        feat_lp = self._upsample_outconv(o, n, h0, w0, 1, lowp=True, taps=t)
+        return feat_lp, (t["dpt_feature"] if t is not None else None)
+
+    def dpt_regress(self, feat_lp, n, hf, wf, H, W):
+        """DPTRegressionProcessor up to the last ReLU (dpt.py:285-311): conv3x3 256->128 at 8x, bilinear
+        (align_corners) to HxW, conv3x3 128->128 + ReLU -> hidden [n*H*W][128] (lp).  feat_lp may be a
+        one-element list, handed over so that the 8x map is freed as soon as it has been read."""
+        w = self.w
+        if isinstance(feat_lp, list):
+            feat_lp = feat_lp.pop()
         r1 = self._empty(n * hf * wf, 128)
         self._conv3(feat_lp, n, hf, wf, 256, w.reg_c1, 128, bias=w.reg_b1, out_lp=r1)
         del feat_lp

@@ -86,6 +86,7 @@ class MapAnything:
         # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
         self.hip_graphs = hip_graphs and os.environ.get("MAPA_HIP_GRAPHS", "1") != "0"
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
+        self._modules: Dict[str, Any] = {}
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)
 
@@ -142,6 +143,7 @@ class MapAnything:
         self._sd = sd
         self._engines.clear()
         self._graphs.clear()
+        self._modules.clear()
         return self
 
     def load_synthetic_weights(self):
@@ -151,7 +153,43 @@ class MapAnything:
         self._sd = synthetic_state_dict(canonical_spec())
         self._engines.clear()
         self._graphs.clear()
+        self._modules.clear()
         return self
+
+    # ------------------------------------------------------- sub-modules (uniception dataclass contracts, modules.py)
+    def _module(self, name: str):
+        m = self._modules.get(name)
+        if m is None:
+            from . import modules as M
+
+            make = {"encoder": M.DINOv2Encoder, "info_sharing": M.MultiViewAlternatingAttentionTransformerIFR,
+                    "dpt_feature_head": M.DPTFeature, "dpt_regressor_head": M.DPTRegressionProcessor,
+                    "dense_adaptor": M.RayDirectionsPlusDepthWithConfidenceAndMaskAdaptor,
+                    "pose_head": M.PoseHead, "pose_adaptor": M.CamTranslationPlusQuatsAdaptor,
+                    "scale_head": M.MLPHead, "scale_adaptor": M.ScaleAdaptor, "fusion_norm_layer": M.FusionNorm}
+            if name == "dense_head":
+                m = M.DenseHead(self.dpt_feature_head, self.dpt_regressor_head)
+            else:
+                m = make[name](self)
+            self._modules[name] = m
+        return m
+
+    encoder = property(lambda self: self._module("encoder"))                        # model.py:168-172
+    info_sharing = property(lambda self: self._module("info_sharing"))              # model.py:316
+    dpt_feature_head = property(lambda self: self._module("dpt_feature_head"))      # model.py:394
+    dpt_regressor_head = property(lambda self: self._module("dpt_regressor_head"))  # model.py:395
+    dense_head = property(lambda self: self._module("dense_head"))                  # model.py:398
+    dense_adaptor = property(lambda self: self._module("dense_adaptor"))            # model.py:470
+    pose_head = property(lambda self: self._module("pose_head"))                    # model.py:403
+    pose_adaptor = property(lambda self: self._module("pose_adaptor"))
+    scale_head = property(lambda self: self._module("scale_head"))                  # model.py:420
+    scale_adaptor = property(lambda self: self._module("scale_adaptor"))            # model.py:634
+    fusion_norm_layer = property(lambda self: self._module("fusion_norm_layer"))    # model.py:213
+
+    @property
+    def scale_token(self) -> torch.Tensor:
+        """The learned scale token (1024,) fp32 on the model's device (model.py:218)."""
+        return self.engine().w.scale_token.reshape(-1)
 
     # ------------------------------------------------------------------------------------ nn.Module-ish
     def to(self, device=None, *args, **kwargs):

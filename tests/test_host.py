@@ -88,3 +88,21 @@ def test_config_guard_rejects_other_architectures():
     cfg["pred_head_config"] = dict(cfg["pred_head_config"], type="linear")
     with pytest.raises(ValueError, match="unsupported"):
         MapAnything(**cfg)
+
+
+def test_module_surface_is_exposed():
+    """The sub-modules the reference's forward calls (model.py:168-634) exist under the same attribute names and
+    take the uniception dataclasses (tests/test_gpu_modules.py runs them)."""
+    from mapanything.models import MapAnything
+    from tests_helpers import released_config
+    from uniception.models.encoders import ViTEncoderInput, ViTEncoderOutput  # noqa: F401
+    from uniception.models.info_sharing import MultiViewTransformerInput, MultiViewTransformerOutput  # noqa: F401
+    from uniception.models.prediction_heads import (AdaptorInput, DPTFeatureInput, PixelTaskOutput,  # noqa: F401
+                                                    PredictionHeadInput, PredictionHeadLayeredInput,
+                                                    PredictionHeadTokenInput, SummaryTaskOutput)
+
+    m = MapAnything(**released_config())
+    for name in ("encoder", "info_sharing", "dpt_feature_head", "dpt_regressor_head", "dense_head", "dense_adaptor",
+                 "pose_head", "pose_adaptor", "scale_head", "scale_adaptor", "fusion_norm_layer"):
+        assert callable(getattr(m, name)), name
+    assert m.encoder is m.encoder and m.info_sharing.indices == (11, 17)
