@@ -163,6 +163,12 @@ int mapa_dense_head_out(const void* hidden, int dtype, int n, int HW, const floa
                         float* pts3d_cam, float* rays, float* depth, float* conf, float* logits, uint8_t* mask,
                         mapa_stream_t stream);
 
+/* Image normalisation of the input pipeline (image.py:270-275 / 466-470: torchvision ToTensor + Normalize):
+ * hwc u8 [n][H][W][3] (decoded, resized, cropped on the host) -> out f32 [n][3][H][W] = (u8 / 255 - mean) / std,
+ * IEEE float32 division and subtraction in torch's order.  mean3 / std3: HOST arrays of 3 floats. */
+int mapa_normalize_image(const uint8_t* hwc, int n, int H, int W, const float* mean3, const float* std3, float* out,
+                         mapa_stream_t stream);
+
 /* Dense adaptor on its own (RayDirectionsPlusDepthWithConfidenceAndMaskAdaptor, adaptors.py:1898-1951 ->
  * 1740-1796, 393-523, 1012-1073, 1114-1133), for the module-level API (model.dense_adaptor): raw [n][HW][6] f32
  * (the regressor's conv1x1 output rows) -> NCHW f32 planes value [n][4][HW] = (ray / max(|ray|, 1e-8), exp(depth)),

@@ -296,6 +296,21 @@ __global__ void __launch_bounds__(256) dense_adaptor_kernel(const float* __restr
   }
 }
 
+// ToTensor + Normalize (torchvision, image.py:270-275): out[v][c][y][x] = (u8 / 255 - mean_c) / std_c, the same
+// two IEEE float32 operations in the same order (bit-identical to torch on the CPU).
+__global__ void __launch_bounds__(256) normalize_image_kernel(const uint8_t* __restrict__ hwc, int64_t npix,
+                                                              int64_t HW, float m0, float m1, float m2, float s0,
+                                                              float s1, float s2, float* __restrict__ out) {
+  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p < npix; p += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = p / HW, i = p - v * HW;
+    const uint8_t* px = hwc + p * 3;
+    float* o = out + v * 3 * HW + i;
+    o[0] = __fdiv_rn(__fsub_rn(__fdiv_rn((float)px[0], 255.f), m0), s0);
+    o[HW] = __fdiv_rn(__fsub_rn(__fdiv_rn((float)px[1], 255.f), m1), s1);
+    o[2 * HW] = __fdiv_rn(__fsub_rn(__fdiv_rn((float)px[2], 255.f), m2), s2);
+  }
+}
+
 __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, int rows, int cols, void* dst,
                                     int bf, int64_t ldd) {
   const int64_t total = (int64_t)rows * cols;
@@ -437,6 +452,17 @@ extern "C" int mapa_dense_adaptor(const float* raw, int n, int64_t HW, float* va
   hipLaunchKernelGGL(dense_adaptor_kernel, dim3(grid_for(total)), dim3(TPB), 0, stream, raw, n, HW, value, conf,
                      logits, mask);
   MAPA_CHECK_LAUNCH("mapa_dense_adaptor");
+  return 0;
+}
+
+extern "C" int mapa_normalize_image(const uint8_t* hwc, int n, int H, int W, const float* mean3, const float* std3,
+                                    float* out, hipStream_t stream) {
+  MAPA_CHECK_ARG(hwc && out && mean3 && std3 && n > 0 && H > 0 && W > 0, "mapa_normalize_image: bad args");
+  MAPA_CHECK_ARG(std3[0] != 0.f && std3[1] != 0.f && std3[2] != 0.f, "mapa_normalize_image: zero std");
+  const int64_t HW = (int64_t)H * W, npix = (int64_t)n * HW;
+  hipLaunchKernelGGL(normalize_image_kernel, dim3(grid_for(npix)), dim3(TPB), 0, stream, hwc, npix, HW, mean3[0],
+                     mean3[1], mean3[2], std3[0], std3[1], std3[2], out);
+  MAPA_CHECK_LAUNCH("mapa_normalize_image");
   return 0;
 }
 

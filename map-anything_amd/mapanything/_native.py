@@ -29,6 +29,7 @@ EXPORTED = (
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
+    "mapa_normalize_image",
 )
 
 
@@ -109,6 +110,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_confidence_mask.argtypes = [vp, vp, vp, i, i64, f, vp]
     L.mapa_attn_merge.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i64, vp]
     L.mapa_dense_adaptor.argtypes = [vp, i, i64, vp, vp, vp, vp, vp]
+    L.mapa_normalize_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
     _lib = L
     return L
 
@@ -398,3 +400,11 @@ def dense_adaptor(raw, n, HW, value, conf, logits, mask):
     """raw [n][HW][6] f32 -> value [n][4][HW], conf / logits / mask [n][HW] (NCHW planes; include/mapa.h)."""
     check(lib().mapa_dense_adaptor(ptr(raw), n, HW, ptr(value), ptr(conf), ptr(logits), ptr(mask), stream()),
           "mapa_dense_adaptor")
+
+
+def normalize_image(hwc_u8, n, H, W, mean, std, out):
+    """hwc_u8 [n][H][W][3] uint8 (device) -> out [n][3][H][W] f32 = (x / 255 - mean) / std (include/mapa.h)."""
+    m = (ctypes.c_float * 3)(*[float(x) for x in mean])
+    s = (ctypes.c_float * 3)(*[float(x) for x in std])
+    check(lib().mapa_normalize_image(ptr(hwc_u8), n, H, W, ctypes.cast(m, ctypes.c_void_p),
+                                     ctypes.cast(s, ctypes.c_void_p), ptr(out), stream()), "mapa_normalize_image")

@@ -49,3 +49,39 @@ def make_views(case):
             view["is_metric_scale"] = torch.tensor([v != 2])
         views.append(view)
     return views
+
+
+IMAGE_FILES = [("a_land.jpg", 700, 520), ("b_land.png", 640, 480), ("c_small.png", 160, 120),
+               ("d_portrait.png", 300, 420), ("e_notes.txt", 0, 0), ("f_portrait.jpg", 240, 360)]
+
+
+def synthetic_image(W, H, seed):
+    """Smooth seeded RGB image (gradients + discs + mild noise) as a uint8 (H, W, 3) array."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:H, 0:W].astype(np.float32)
+    img = np.stack([x / max(W - 1, 1), y / max(H - 1, 1), (x + y) / max(W + H - 2, 1)], -1) * 200.0
+    for _ in range(4):
+        cx, cy, r = rng.uniform(0, W), rng.uniform(0, H), rng.uniform(0.1, 0.3) * min(W, H)
+        img[(x - cx) ** 2 + (y - cy) ** 2 < r * r] += rng.uniform(-60, 60, 3)
+    img += rng.normal(0, 3, img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def write_image_files(folder):
+    """The input files of the image-pipeline fixtures (PIL encodes them deterministically)."""
+    import os
+
+    import PIL.Image
+
+    os.makedirs(folder, exist_ok=True)
+    for i, (name, W, H) in enumerate(IMAGE_FILES):
+        path = os.path.join(folder, name)
+        if name.endswith(".txt"):
+            open(path, "w").write("not an image\n")
+        elif name.endswith(".jpg"):
+            PIL.Image.fromarray(synthetic_image(W, H, 100 + i)).save(path, quality=90)
+        else:
+            PIL.Image.fromarray(synthetic_image(W, H, 100 + i)).save(path)
+    return [n for n, _, _ in IMAGE_FILES]
