@@ -64,20 +64,43 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef short s8v __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 __device__ __forceinline__ s4v tr_read(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4v*)(p));
 }
 
 // ------------------------------------------------------------------------------------------------ bf16
-// QB query sub-blocks of 32 rows per wave (workgroup = 4 waves = 128*QB query rows).  QB = 2 halves the K/V
-// bytes staged per flop (the per-CU L2 -> LDS fill rate bounds this kernel at QB = 1) and gives each wave two
-// independent softmax / MFMA chains to interleave.
-template <int QB, int NW>
-__global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 3) attn_fwd_bf16(AttnArgs p) {
+// Row sums are plain f32 adds: attention.o is built with -fno-slp-vectorize so -O3 does not pack them into
+// v_pk_add_f32, which costs ~12 extra cycles per instruction beside MFMAs (MI355X_MICROARCH.md, per-instruction
+// cycle constants).  (An inline-asm v_add would dodge the packing too, but hipcc pads no hazards into asm: the
+// v_exp_f32 -> VALU and MFMA -> VALU wait states would be missing.)
+__device__ __forceinline__ float add_s(float a, float b) { return a + b; }
+
+// Softmax bookkeeping relative to a per-row REFERENCE max m_ref (log2 domain) instead of the exact running max:
+//  * the QK^T accumulator is initialised with -m_ref, so the MFMA itself produces s - m_ref (no per-score subtract);
+//  * P = exp2(s - m_ref) is used as long as every row sum of the tile stays <= 2^8 (then every P <= 256: no
+//    overflow, and bf16 P keeps its relative precision at any magnitude);
+//  * otherwise (rare, wave-uniform branch) the rows are rebased onto their true running max: O and l scaled by
+//    exp2(-d), P recomputed.  The first tile always takes the exact path (m_ref := its row max).
+// Exact softmax either way: O / l is invariant to the reference (the LSE output adds m_ref back).
+constexpr float REBASE_SUM = 256.f;
+#ifndef ATTN_SUM_MFMA
+#define ATTN_SUM_MFMA 0
+#endif
+#ifndef ATTN_EXACT_SCALE
+#define ATTN_EXACT_SCALE 0
+#endif
+// scores leave the MFMA in the log2 domain (Q pre-scaled by log2(e)/8, one bf16 rounding) or, with
+// ATTN_EXACT_SCALE, in natural units (Q scaled by the exact 1/8) and enter exp2 through one fma by log2(e)
+constexpr float SMUL = ATTN_EXACT_SCALE ? LOG2E : 1.f;
+
+template <int NW, bool SEG>
+__global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p) {
   constexpr int TILE = KT * 128;  // 64 rows x 128 B
-  constexpr int QW = 32 * QB;     // query rows per wave
-  constexpr int QBLK_WG = NW * QW;
+  constexpr int QBLK_WG = NW * 32;
+  constexpr int NP = 16 / NW;     // 1-KiB LDS-DMA pieces per wave per K/V tile (first half K, second half V)
+  static_assert(NW == 4 || NW == 8, "pieces are dealt K-first over 4 or 8 waves");
   __shared__ __attribute__((aligned(1024))) char lds[2 * 2 * TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5, l32 = lane & 31;
@@ -87,72 +110,116 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 3) attn_fwd_bf16(AttnAr
   const int qt = bid % nqt, hb = bid / nqt, h = hb % p.heads, b = hb / p.heads;
 
   const bf16_t* qbase = reinterpret_cast<const bf16_t*>(p.q) + b * p.qb + h * 64;
-  const bf16_t* kbase = reinterpret_cast<const bf16_t*>(p.k) + b * p.kb + h * 64;
-  const bf16_t* vbase = reinterpret_cast<const bf16_t*>(p.v) + b * p.vb + h * 64;
-  int qrow[QB];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) qrow[qb] = qt * QBLK_WG + wave * QW + qb * 32 + l32;
+  const char* kbase = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.k) + b * p.kb + h * 64);
+  const char* vbase = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.v) + b * p.vb + h * 64);
+  const int qrow = qt * QBLK_WG + wave * 32 + l32;
 
   // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 * log2(e) so the
   // scores come out of the MFMA already in the log2 domain (one bf16 rounding of the scaled Q).
-  b8 qf[QB][4];
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    const int qrow_c = qrow[qb] < p.seq_q ? qrow[qb] : p.seq_q - 1;
+  b8 qf[4];
+  {
+    const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
       b8 sc;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E));
-      qf[qb][kk] = sc;
+      for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E / SMUL));
+      qf[kk] = sc;
     }
   }
 
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const int nkt = (p.seq_kv + KT - 1) / KT;
+  const int nfull = p.seq_kv / KT;
 
-  // K and V tiles = 16 pieces of 8 rows x 128 B (one 1-KiB LDS-DMA wave instruction each), dealt over NW waves
-  auto stage = [&](int slot, int kt) {
-    char* Ks = lds + slot * 2 * TILE;
+  // Staging: piece = i*NW + wave is 8 rows x 128 B of K (piece < 8) or V; this lane's 16 B sit at tile row
+  // srow[i], byte column scol[i] (XOR-swizzled on the source so the LDS image stays lane-linear).  The byte
+  // offset inside a tile is loop-invariant; a full tile adds one wave-uniform base per tile.
+  int srow[NP];
+  uint32_t soff[NP];
 #pragma unroll
-    for (int i = 0; i < (16 + NW - 1) / NW; ++i) {
-      const int piece = i * NW + wave;
-      if (16 % NW != 0 && piece >= 16) break;
-      const bool isv = piece >= 8;
-      const int row = (piece & 7) * 8 + (lane >> 3), pos = lane & 7;
-      const int key = kt * KT + row;
-      const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
-      const int pr = kv_row(p, key);
-      const bf16_t* base = isv ? vbase : kbase;
-      const int64_t rs = isv ? p.vr : p.kr;
-      const char* src = key < p.seq_kv ? reinterpret_cast<const char*>(base + (int64_t)pr * rs + c * 8) : zero;
-      __builtin_amdgcn_global_load_lds(src, Ks + piece * 1024, 16, 0, 0);
+  for (int i = 0; i < NP; ++i) {
+    const int piece = i * NW + wave;
+    const bool isv = i >= NP / 2;
+    const int row = (piece & 7) * 8 + (lane >> 3), pos = lane & 7;
+    const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
+    srow[i] = row;
+    soff[i] = (uint32_t)(row * (isv ? p.vr : p.kr) * 2 + c * 16);
+  }
+  // physical row of logical key `key0` when the whole tile [key0, key0+64) sits in one K/V segment, else -1
+  auto seg_base = [&](int key0) -> int {
+    if (!SEG) return key0;
+    const int key1 = min(key0 + KT, p.seq_kv) - 1;
+    int cum = 0;
+#pragma unroll 1
+    for (int s = 0; s < p.nseg; ++s) {
+      const int len = p.seg_len[s];
+      if (key0 >= cum && key0 < cum + len) return key1 < cum + len ? p.seg_start[s] + (key0 - cum) : -1;
+      cum += len;
+    }
+    return -1;
+  };
+  auto stage = [&](int slot, int kt) {
+    char* dst = lds + slot * 2 * TILE;
+    const int key0 = kt * KT;
+    const int r0 = seg_base(key0);
+    const bool tail = key0 + KT > p.seq_kv;
+    if (r0 >= 0 && !tail) {  // wave-uniform fast path: per-tile buffer descriptors + loop-invariant lane offsets
+      const __amdgpu_buffer_rsrc_t rk =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (int64_t)r0 * p.kr * 2), 0, 0x7fffffff, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rv =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (int64_t)r0 * p.vr * 2), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= NP / 2 ? rv : rk, (lds_ptr_t)(dst + (i * NW + wave) * 1024), 16,
+                                                 (int)soff[i], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const bool isv = i >= NP / 2;
+        const int key = key0 + srow[i];
+        const int pr = SEG ? kv_row(p, key) : key;
+        const int c_off = (int)(soff[i] - (uint32_t)(srow[i] * (isv ? p.vr : p.kr) * 2));
+        const char* src = key < p.seq_kv
+                              ? (isv ? vbase : kbase) + (int64_t)pr * (isv ? p.vr : p.kr) * 2 + c_off
+                              : zero;
+        __builtin_amdgcn_global_load_lds(src, dst + (i * NW + wave) * 1024, 16, 0, 0);
+      }
     }
   };
 
-  f32x16 o[QB][2];
-  float m_run[QB], l_run[QB];
+  f32x16 o[2];
 #pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
+  for (int d = 0; d < 2; ++d)
 #pragma unroll
-    for (int d = 0; d < 2; ++d)
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m_ref = 0.f, l_run = 0.f;
+  b8 ones;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[qb][d][r] = 0.f;
-    m_run[qb] = -INFINITY;
-    l_run[qb] = 0.f;
-  }
+  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
 
-  // One K/V tile: S^T = K Q^T, online softmax, O^T += V^T P^T.  TAIL (the last, partial tile only) masks the
-  // keys past seq_kv; full tiles carry no masking code at all.
-  auto tile = [&](int kt, auto tail_tag) __attribute__((always_inline)) {
+  // K fragment LDS byte offsets (row kb*32 + l32, chunk kk*2 + hl) and V tr-read offsets: lane constants
+  // C operand of the first QK^T MFMA of every full tile: -m_ref in every element, kept in its own registers and
+  // rewritten only when m_ref moves (no per-tile splat)
+  f32x16 csplat;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) csplat[r] = 0.f;
+  auto set_ref = [&](float m) __attribute__((always_inline)) {
+    m_ref = m;
+    if (!ATTN_EXACT_SCALE) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) csplat[r] = -m;
+    }
+  };
+  // SLOT = kt & 1 as a compile-time constant (the loop below is unrolled by two): LDS addresses and the DMA
+  // destination fold into immediates
+  auto tile = [&](int kt, auto first_tag, auto tail_tag, auto slot_tag) __attribute__((always_inline)) {
+    constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool TAIL = decltype(tail_tag)::value;
-    const int cur = kt & 1;
+    constexpr int cur = decltype(slot_tag)::value;
     const char* Ks = lds + cur * 2 * TILE;
     const char* Vs = Ks + TILE;
-    // every LDS read of this tile is issued before the next tile's DMA, so the compiler's conservative
-    // vmcnt(0) (an LDS-DMA may alias any LDS read) never lands inside the tile: K fragments (b128) and the
-    // transposed V fragments (tr_b16) stay in registers, the DMA then has the whole tile to land.
     b8 kf[2][4];
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -163,34 +230,31 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 3) attn_fwd_bf16(AttnAr
         kf[kb][kk] = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
       }
     }
-
-    // S^T = K Q^T  (per sub-block: 2 x 32x32 tiles = 64 keys x 32 queries); masked keys enter as -inf via C
-    f32x16 st[QB][2];
+    // S^T - m_ref = K Q^T + C, C = -m_ref (masked keys of the tail tile: -inf)
+    f32x16 st[2];
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+    for (int kb = 0; kb < 2; ++kb) {
+      if constexpr (TAIL) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          if constexpr (TAIL) {
-            const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-            st[qb][kb][r] = key < p.seq_kv ? 0.f : -INFINITY;
-          } else {
-            st[qb][kb][r] = 0.f;
-          }
+          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          st[kb][r] = key < p.seq_kv ? csplat[r] : -INFINITY;
         }
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk)
-          st[qb][kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[qb][kk], st[qb][kb], 0, 0, 0);
+        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], st[kb], 0, 0, 0);
+      } else {
+        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], csplat, 0, 0, 0);
       }
-    // V^T fragments, then the next tile's DMA (K fragments are dead by now: fewer live registers)
+#pragma unroll
+      for (int kk = 1; kk < 4; ++kk)
+        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
+    }
     b8 vf[2][2][2];
     {
       const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
-        const int c0 = dt * 32 + 16 * grp + 4 * p4;  // column (d) this lane addresses
-        const int chunk = c0 >> 3, within = (c0 & 7) * 2;
+        const int cc = dt * 32 + 16 * grp + 4 * p4;
+        const int chunk = cc >> 3, within = (cc & 7) * 2;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -205,95 +269,116 @@ __global__ void __launch_bounds__(NW * 64, NW == 4 ? 2 : 3) attn_fwd_bf16(AttnAr
       }
     }
     if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
-    float m_new[QB];
-    bool grow = false;
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      float mx0 = st[qb][0][0], mx1 = st[qb][1][0];
-#pragma unroll
-      for (int r = 1; r < 16; ++r) {
-        mx0 = fmaxf(mx0, st[qb][0][r]);
-        mx1 = fmaxf(mx1, st[qb][1][r]);
-      }
-      float mx = fmaxf(mx0, mx1);
-      {  // the other 32 keys of this query row live in lane l ^ 32
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-        mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
-      }
-      m_new[qb] = fmaxf(m_run[qb], mx);
-      grow |= m_new[qb] > m_run[qb];
-    }
-    if (__any(grow)) {  // rescale only when some row max moved (exact: alpha == 1 otherwise)
-#pragma unroll
-      for (int qb = 0; qb < QB; ++qb) {
-        const float alpha = __builtin_amdgcn_exp2f(m_run[qb] - m_new[qb]);
-        l_run[qb] *= alpha;
-#pragma unroll
-        for (int d = 0; d < 2; ++d)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[qb][d][r] *= alpha;
-      }
-    }
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-      m_run[qb] = m_new[qb];
-      float ls[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float e = __builtin_amdgcn_exp2f(st[qb][kb][r] - m_new[qb]);
-          st[qb][kb][r] = e;
-          ls[r & 3] += e;
-        }
-      l_run[qb] += (ls[0] + ls[1]) + (ls[2] + ls[3]);
-      // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T (transposed LDS reads above)
-      b8 pf[2][2];
+
+    // P = exp2(S - m_ref) -> bf16 fragments, row partial sums (this lane's 32 keys)
+    b8 pf[2][2];
+    float ls;
+    auto exp_pack = [&](float shift) __attribute__((always_inline)) {
+      float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
           b8 t;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) t[j] = (__bf16)st[qb][kb][8 * s + j];
+          for (int j = 0; j < 8; ++j) {
+            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(st[kb][8 * s + j], SMUL, -shift));
+            if (!ATTN_SUM_MFMA) a[j & 3] = add_s(a[j & 3], e);
+            t[j] = (__bf16)e;
+          }
           pf[kb][s] = t;
         }
+      if (ATTN_SUM_MFMA) {  // row sums on the matrix pipe: ones(32x16) * P^T -> every row = the full 64-key sum
+        f32x16 acc;
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
+        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s = 0; s < 2; ++s)
-            o[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[qb][dt], 0, 0, 0);
+          for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kb][s], acc, 0, 0, 0);
+        ls = acc[0];
+      } else {
+        ls = add_s(add_s(a[0], a[1]), add_s(a[2], a[3]));
+      }
+    };
+    auto row_max = [&]() __attribute__((always_inline)) {
+      float mx = st[0][0];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb][r]);
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    };
+    if constexpr (FIRST) {
+      const float d = row_max() * SMUL;  // finite: the first tile always holds a valid key
+      set_ref(d);
+      exp_pack(d);
+    } else {
+      const float cur = ATTN_EXACT_SCALE ? m_ref : 0.f;  // (x - 0 folds: the MFMA already produced s - m_ref)
+      exp_pack(cur);
+      if (__builtin_expect(__any(!(ls <= REBASE_SUM)), 0)) {  // rebase (NaN-safe compare: inf sums rebase too)
+        const float d = fmaxf(row_max() * SMUL - cur, 0.f);
+        set_ref(m_ref + d);
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+        l_run *= alpha;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        exp_pack(cur + d);
+      }
     }
+    l_run = add_s(l_run, ls);
+    // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T (transposed LDS reads above)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
     __syncthreads();
   };
 
+  using T_ = std::integral_constant<bool, true>;
+  using F_ = std::integral_constant<bool, false>;
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
   stage(0, 0);
   __syncthreads();
-  const int nfull = p.seq_kv / KT;
-  for (int kt = 0; kt < nfull; ++kt) tile(kt, std::integral_constant<bool, false>());
-  if (nfull < nkt) tile(nfull, std::integral_constant<bool, true>());
-
-#pragma unroll
-  for (int qb = 0; qb < QB; ++qb) {
-    const float l_tot = l_run[qb] + __shfl_xor(l_run[qb], 32, 64);
-    if (qrow[qb] < p.seq_q) {
-      const float inv = 1.f / l_tot;
-      bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow[qb] * p.orr + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int d = dt * 32 + 8 * g + 4 * hl;
-          uint2 pk;
-          pk.x = pack_bf16x2(o[qb][dt][4 * g + 0] * inv, o[qb][dt][4 * g + 1] * inv);
-          pk.y = pack_bf16x2(o[qb][dt][4 * g + 2] * inv, o[qb][dt][4 * g + 3] * inv);
-          *reinterpret_cast<uint2*>(obase + d) = pk;
-        }
-      if (p.lse && hl == 0)
-        p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow[qb]] = (m_run[qb] + __log2f(l_tot)) * LN2;
+  if (nfull == 0) {
+    tile(0, T_(), T_(), S0());
+  } else {
+    tile(0, T_(), F_(), S0());
+    int kt = 1;
+    for (; kt + 1 < nfull; kt += 2) {
+      tile(kt, F_(), F_(), S1());
+      tile(kt + 1, F_(), F_(), S0());
     }
+    if (kt < nfull) tile(kt, F_(), F_(), S1());
+    if (nfull < nkt) {
+      if (nfull & 1) tile(nfull, F_(), T_(), S1());
+      else tile(nfull, F_(), T_(), S0());
+    }
+  }
+
+  const float l_tot = ATTN_SUM_MFMA ? l_run : l_run + __shfl_xor(l_run, 32, 64);
+  if (qrow < p.seq_q) {
+    const float inv = 1.f / l_tot;
+    bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int d = dt * 32 + 8 * g + 4 * hl;
+        uint2 pk;
+        pk.x = pack_bf16x2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
+        pk.y = pack_bf16x2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
+        *reinterpret_cast<uint2*>(obase + d) = pk;
+      }
+    if (p.lse && hl == 0)
+      p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_ref + __log2f(l_tot)) * LN2;
   }
 }
 
@@ -518,7 +603,10 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
     constexpr int nw = 4;
     const int qblk = 32 * nw;
     const int nblk = ((d->seq_q + qblk - 1) / qblk) * d->heads * d->batch;
-    hipLaunchKernelGGL((attn_fwd_bf16<1, nw>), dim3(nblk), dim3(nw * 64), 0, stream, a);
+    if (a.nseg > 0)
+      hipLaunchKernelGGL((attn_fwd_bf16<nw, true>), dim3(nblk), dim3(nw * 64), 0, stream, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_bf16<nw, false>), dim3(nblk), dim3(nw * 64), 0, stream, a);
   } else {
     const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
     hipLaunchKernelGGL(attn_fwd_f32, dim3(nblk), dim3(NT), 0, stream, a);

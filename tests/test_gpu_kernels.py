@@ -191,6 +191,58 @@ def test_attention_softmax_rescale_branch(nat):
     assert rel_l2(o.float().cpu(), ref.cpu()) < 8e-3
 
 
+@pytest.mark.parametrize("trend", [1.0, -1.0])
+def test_attention_score_drift_past_exp2_range(nat, trend):
+    """Scores drift by ~±600 (log2 units) along the keys: with a growing drift every later tile exceeds the
+    first tile's max by far more than exp2's range, so the reference-max softmax must rebase (repeatedly);
+    with a falling drift everything after the first tiles underflows to 0, exactly as in fp32."""
+    Hh, S = 2, 1000
+    q = _rand(S, Hh * 64, scale=0.2, seed=40)
+    q[:, 0::64] = 4.0  # a constant component so that score ~ 4 * k[:, 0] / 8 for every query
+    k = _rand(S, Hh * 64, scale=0.2, seed=41)
+    drift = trend * torch.linspace(-300.0, 300.0, S, device="cuda")
+    k[:, 0::64] = drift[:, None] * 2.0 * 0.6931471805599453  # score = k0 / 2 (natural log) = drift (log2)
+    v = _rand(S, Hh * 64, seed=42)
+    q, k, v = (t.to(torch.bfloat16) for t in (q, k, v))
+    o = torch.empty(S, Hh * 64, device="cuda", dtype=torch.bfloat16)
+    lse = torch.empty(1, Hh, S, device="cuda")
+    C = Hh * 64
+    nat.attention(q, k, v, o, batch=1, heads=Hh, seq_q=S, seq_kv=S, q_bstride=0, q_rstride=C, k_bstride=0,
+                  k_rstride=C, v_bstride=0, v_rstride=C, o_bstride=0, o_rstride=C, lse=lse)
+    qh, kh, vh = (t.view(S, Hh, 64).transpose(0, 1)[None] for t in (q, k, v))
+    ref = _sdpa_ref(qh, kh, vh)[0].transpose(0, 1).reshape(S, C)
+    assert torch.isfinite(o.float()).all()
+    assert rel_l2(o.float().cpu(), ref.cpu()) < 8e-3
+    # the kernel's scores are bf16(q * log2(e) / 8) . k in the log2 domain (one documented bf16 rounding of the
+    # scaled Q, ~2^-9 relative per score); at |score| ~ 200 that alone moves the LSE by ~0.4, so the LSE is held
+    # to the log2-domain reference of those same scores
+    log2e = 1.4426950408889634
+    s2 = (qh.float() * (log2e / 8.0)).to(torch.bfloat16).float() @ kh.float().transpose(-1, -2)
+    assert rel_l2(lse.cpu(), (torch.logsumexp(s2 / log2e, -1)).cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("segs", [[(0, 100), (300, 37), (500, 200), (800, 64)], [(64, 128), (0, 64), (700, 1)]])
+def test_attention_kv_segments(nat, segs):
+    """Logical keys = concatenation of physical K/V row ranges (the sharded layer's slot table); segment
+    boundaries both on and off the 64-key tile grid."""
+    Hh, Sq = 3, 150
+    C = Hh * 64
+    kv = _rand(1024, 2 * C, seed=43).to(torch.bfloat16)
+    q = _rand(Sq, C, seed=44).to(torch.bfloat16)
+    o = torch.empty(Sq, C, device="cuda", dtype=torch.bfloat16)
+    skv = sum(n for _, n in segs)
+    nat.attention(q, kv, kv[:, C:], o, batch=1, heads=Hh, seq_q=Sq, seq_kv=skv, q_bstride=0, q_rstride=C,
+                  k_bstride=0, k_rstride=2 * C, v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C,
+                  kv_segments=segs)
+    rows = torch.cat([torch.arange(s0, s0 + n) for s0, n in segs]).cuda()
+    kvl = kv[rows]
+    qh = q.view(Sq, Hh, 64).transpose(0, 1)[None]
+    kh = kvl[:, :C].reshape(skv, Hh, 64).transpose(0, 1)[None]
+    vh = kvl[:, C:].reshape(skv, Hh, 64).transpose(0, 1)[None]
+    ref = _sdpa_ref(qh, kh, vh)[0].transpose(0, 1).reshape(Sq, C)
+    assert rel_l2(o.float().cpu(), ref.cpu()) < 8e-3
+
+
 # ----------------------------------------------------------------------------------------------- others
 @pytest.mark.parametrize("dim", [768, 1024])
 def test_layernorm(nat, dim):
