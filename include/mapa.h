@@ -102,9 +102,15 @@ typedef struct {
   int kv_nseg;
   int kv_seg_start[MAPA_MAX_KV_SEGMENTS];
   int kv_seg_len[MAPA_MAX_KV_SEGMENTS];
+  /* optional scratch (bf16 only, mapa_attention_workspace_bytes() bytes): the 128-row query blocks left over after
+   * the full waves of the device's resident workgroups are split into K/V chunks (partials merged by LSE);
+   * without it one workgroup per block */
+  void* workspace;
+  int64_t workspace_bytes;
 } mapa_attn_desc;
 
 int mapa_attention(const mapa_attn_desc* d, mapa_stream_t stream);
+int64_t mapa_attention_workspace_bytes(const mapa_attn_desc* d);
 
 /* Merge two attention partials of the same queries over disjoint key sets using their LSEs (the sharded global
  * layer overlaps its K/V all-gather with the local-key partial): o = (e^{lse_a} o_a + e^{lse_b} o_b) /

@@ -17,6 +17,7 @@
 //  * Precise variant (dtype f32): identical dataflow on v_mfma_f32_32x32x2_f32 (exact fp32 products).
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "mapa_common.h"
@@ -85,18 +86,29 @@ __device__ __forceinline__ float add_s(float a, float b) { return a + b; }
 //    exp2(-d), P recomputed.  The first tile always takes the exact path (m_ref := its row max).
 // Exact softmax either way: O / l is invariant to the reference (the LSE output adds m_ref back).
 constexpr float REBASE_SUM = 256.f;
-#ifndef ATTN_SUM_MFMA
-#define ATTN_SUM_MFMA 0
-#endif
 #ifndef ATTN_EXACT_SCALE
 #define ATTN_EXACT_SCALE 0
 #endif
 // scores leave the MFMA in the log2 domain (Q pre-scaled by log2(e)/8, one bf16 rounding) or, with
 // ATTN_EXACT_SCALE, in natural units (Q scaled by the exact 1/8) and enter exp2 through one fma by log2(e)
+// (measured 3 % slower; the same for summing P on the MFMA pipe with a ones operand: 5 % slower)
 constexpr float SMUL = ATTN_EXACT_SCALE ? LOG2E : 1.f;
 
+// Work split.  A task = (batch, head, 128-row query block).  The grid holds n_dp whole tasks (data-parallel, the
+// full waves of the device's resident workgroup slots) followed by the remaining tasks each cut into `chunks`
+// contiguous K/V tile ranges so that the last, partial wave is spread over all slots instead of leaving most of
+// the chip idle for a whole task time (e.g. 1032 global-layer tasks on 512 slots: 2 waves + 8 tasks -> the 8 tasks
+// run as 8 x 43 chunks).  Chunks leave normalised fp32 rows + LSE in the workspace (slot = tail workgroup index)
+// and attn_split_merge combines them.  The tail workgroups have the highest ids, so they are dispatched last.
+struct SplitArgs {
+  float* part_o;    // [slots][128][64] fp32
+  float* part_lse;  // [slots][128]     natural-log LSE
+  int n_dp;         // whole tasks (grid ids [0, n_dp))
+  int chunks;       // K/V chunks per remaining task (grid ids n_dp + j: task n_dp + j / chunks, chunk j % chunks)
+};
+
 template <int NW, bool SEG>
-__global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p) {
+__global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArgs sp) {
   constexpr int TILE = KT * 128;  // 64 rows x 128 B
   constexpr int QBLK_WG = NW * 32;
   constexpr int NP = 16 / NW;     // 1-KiB LDS-DMA pieces per wave per K/V tile (first half K, second half V)
@@ -105,37 +117,25 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hl = lane >> 5, l32 = lane & 31;
   const int nqt = (p.seq_q + QBLK_WG - 1) / QBLK_WG;
-  const int nblk = nqt * p.heads * p.batch;
-  const int bid = xcd_remap(blockIdx.x, nblk);
-  const int qt = bid % nqt, hb = bid / nqt, h = hb % p.heads, b = hb / p.heads;
-
-  const bf16_t* qbase = reinterpret_cast<const bf16_t*>(p.q) + b * p.qb + h * 64;
-  const char* kbase = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.k) + b * p.kb + h * 64);
-  const char* vbase = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.v) + b * p.vb + h * 64);
-  const int qrow = qt * QBLK_WG + wave * 32 + l32;
-
-  // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 * log2(e) so the
-  // scores come out of the MFMA already in the log2 domain (one bf16 rounding of the scaled Q).
-  b8 qf[4];
-  {
-    const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
-      b8 sc;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E / SMUL));
-      qf[kk] = sc;
-    }
+  const int nkt = (p.seq_kv + KT - 1) / KT;
+  const bool has_tail = (p.seq_kv % KT) != 0;
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  int task, k0, k1, slot = -1;
+  if ((int)blockIdx.x < sp.n_dp) {  // whole task; consecutive tasks (same batch/head: shared K/V) on one XCD
+    task = xcd_remap(blockIdx.x, sp.n_dp);
+    k0 = 0;
+    k1 = nkt;
+  } else {
+    slot = blockIdx.x - sp.n_dp;
+    task = sp.n_dp + slot / sp.chunks;
+    const int ch = slot % sp.chunks;
+    k0 = (int)((int64_t)ch * nkt / sp.chunks);
+    k1 = (int)((int64_t)(ch + 1) * nkt / sp.chunks);
   }
 
-  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
-  const int nkt = (p.seq_kv + KT - 1) / KT;
-  const int nfull = p.seq_kv / KT;
-
   // Staging: piece = i*NW + wave is 8 rows x 128 B of K (piece < 8) or V; this lane's 16 B sit at tile row
-  // srow[i], byte column scol[i] (XOR-swizzled on the source so the LDS image stays lane-linear).  The byte
-  // offset inside a tile is loop-invariant; a full tile adds one wave-uniform base per tile.
+  // srow[i] (XOR-swizzled 16-B column on the source so the LDS image stays lane-linear).  The byte offset inside
+  // a tile is loop-invariant; a full tile adds one wave-uniform base per tile.
   int srow[NP];
   uint32_t soff[NP];
 #pragma unroll
@@ -160,226 +160,291 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p) {
     }
     return -1;
   };
-  auto stage = [&](int slot, int kt) {
-    char* dst = lds + slot * 2 * TILE;
-    const int key0 = kt * KT;
-    const int r0 = seg_base(key0);
-    const bool tail = key0 + KT > p.seq_kv;
-    if (r0 >= 0 && !tail) {  // wave-uniform fast path: per-tile buffer descriptors + loop-invariant lane offsets
-      const __amdgpu_buffer_rsrc_t rk =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (int64_t)r0 * p.kr * 2), 0, 0x7fffffff, 0x00020000);
-      const __amdgpu_buffer_rsrc_t rv =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (int64_t)r0 * p.vr * 2), 0, 0x7fffffff, 0x00020000);
+
+  {
+    const int qt = task % nqt, hb = task / nqt, h = hb % p.heads, b = hb / p.heads;
+    const bf16_t* qbase = reinterpret_cast<const bf16_t*>(p.q) + b * p.qb + h * 64;
+    const char* kbase = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.k) + b * p.kb + h * 64);
+    const char* vbase = reinterpret_cast<const char*>(reinterpret_cast<const bf16_t*>(p.v) + b * p.vb + h * 64);
+    const int qrow = qt * QBLK_WG + wave * 32 + l32;
+
+    auto stage = [&](int slot, int kt) {
+      char* dst = lds + slot * 2 * TILE;
+      const int key0 = kt * KT;
+      const int r0 = seg_base(key0);
+      const bool tail = key0 + KT > p.seq_kv;
+      if (r0 >= 0 && !tail) {  // wave-uniform fast path: per-tile buffer descriptors + loop-invariant lane offsets
+        const __amdgpu_buffer_rsrc_t rk =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(kbase + (int64_t)r0 * p.kr * 2), 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rv =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(vbase + (int64_t)r0 * p.vr * 2), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < NP; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= NP / 2 ? rv : rk, (lds_ptr_t)(dst + (i * NW + wave) * 1024), 16,
-                                                 (int)soff[i], 0, 0, 0);
-    } else {
+        for (int i = 0; i < NP; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(i >= NP / 2 ? rv : rk, (lds_ptr_t)(dst + (i * NW + wave) * 1024),
+                                                   16, (int)soff[i], 0, 0, 0);
+      } else {
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const bool isv = i >= NP / 2;
-        const int key = key0 + srow[i];
-        const int pr = SEG ? kv_row(p, key) : key;
-        const int c_off = (int)(soff[i] - (uint32_t)(srow[i] * (isv ? p.vr : p.kr) * 2));
-        const char* src = key < p.seq_kv
-                              ? (isv ? vbase : kbase) + (int64_t)pr * (isv ? p.vr : p.kr) * 2 + c_off
-                              : zero;
-        __builtin_amdgcn_global_load_lds(src, dst + (i * NW + wave) * 1024, 16, 0, 0);
+        for (int i = 0; i < NP; ++i) {
+          const bool isv = i >= NP / 2;
+          const int key = key0 + srow[i];
+          const int pr = SEG ? kv_row(p, key) : key;
+          const int c_off = (int)(soff[i] - (uint32_t)(srow[i] * (isv ? p.vr : p.kr) * 2));
+          const char* src = key < p.seq_kv
+                                ? (isv ? vbase : kbase) + (int64_t)pr * (isv ? p.vr : p.kr) * 2 + c_off
+                                : zero;
+          __builtin_amdgcn_global_load_lds(src, dst + (i * NW + wave) * 1024, 16, 0, 0);
+        }
       }
-    }
-  };
+    };
+    stage(0, k0);  // the first tile's DMA flies while Q is read
 
-  f32x16 o[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m_ref = 0.f, l_run = 0.f;
-  b8 ones;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ones[j] = (__bf16)1.f;
-
-  // K fragment LDS byte offsets (row kb*32 + l32, chunk kk*2 + hl) and V tr-read offsets: lane constants
-  // C operand of the first QK^T MFMA of every full tile: -m_ref in every element, kept in its own registers and
-  // rewritten only when m_ref moves (no per-tile splat)
-  f32x16 csplat;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) csplat[r] = 0.f;
-  auto set_ref = [&](float m) __attribute__((always_inline)) {
-    m_ref = m;
-    if (!ATTN_EXACT_SCALE) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) csplat[r] = -m;
-    }
-  };
-  // SLOT = kt & 1 as a compile-time constant (the loop below is unrolled by two): LDS addresses and the DMA
-  // destination fold into immediates
-  auto tile = [&](int kt, auto first_tag, auto tail_tag, auto slot_tag) __attribute__((always_inline)) {
-    constexpr bool FIRST = decltype(first_tag)::value;
-    constexpr bool TAIL = decltype(tail_tag)::value;
-    constexpr int cur = decltype(slot_tag)::value;
-    const char* Ks = lds + cur * 2 * TILE;
-    const char* Vs = Ks + TILE;
-    b8 kf[2][4];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      const int row = kb * 32 + l32;
+    // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 * log2(e) so the
+    // scores come out of the MFMA already in the log2 domain (one bf16 rounding of the scaled Q).
+    b8 qf[4];
+    {
+      const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const int chunk = kk * 2 + hl;
-        kf[kb][kk] = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+        const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
+        b8 sc;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E / SMUL));
+        qf[kk] = sc;
       }
     }
-    // S^T - m_ref = K Q^T + C, C = -m_ref (masked keys of the tail tile: -inf)
-    f32x16 st[2];
+
+    f32x16 o[2];
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-      if constexpr (TAIL) {
+    for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          st[kb][r] = key < p.seq_kv ? csplat[r] : -INFINITY;
+      for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+    float m_ref = 0.f, l_run = 0.f;
+    // C operand of the first QK^T MFMA of every full tile: -m_ref in every element, kept in its own registers and
+    // rewritten only when m_ref moves (no per-tile splat)
+    f32x16 csplat;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) csplat[r] = 0.f;
+    auto set_ref = [&](float m) __attribute__((always_inline)) {
+      m_ref = m;
+      if (!ATTN_EXACT_SCALE) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) csplat[r] = -m;
+      }
+    };
+
+    // One K/V tile: S^T = K Q^T, softmax, O^T += V^T P^T.  FIRST (a segment's first tile) sets m_ref; TAIL (the
+    // last, partial tile of the key range) masks keys past seq_kv; SLOT = the LDS ring slot as a compile-time
+    // constant (tiles alternate slots; the loops below unroll by two) so LDS addresses fold into immediates.
+    auto tile = [&](int kt, auto first_tag, auto tail_tag, auto slot_tag) __attribute__((always_inline)) {
+      constexpr bool FIRST = decltype(first_tag)::value;
+      constexpr bool TAIL = decltype(tail_tag)::value;
+      constexpr int cur = decltype(slot_tag)::value;
+      const char* Ks = lds + cur * 2 * TILE;
+      const char* Vs = Ks + TILE;
+      // every LDS read of this tile is issued before the next tile's DMA, so the compiler's conservative
+      // vmcnt(0) (an LDS-DMA may alias any LDS read) never lands inside the tile
+      b8 kf[2][4];
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int row = kb * 32 + l32;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int chunk = kk * 2 + hl;
+          kf[kb][kk] = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
         }
-        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], st[kb], 0, 0, 0);
-      } else {
-        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], csplat, 0, 0, 0);
       }
+      // S^T - m_ref = K Q^T + C, C = -m_ref (masked keys of the tail tile: -inf)
+      f32x16 st[2];
 #pragma unroll
-      for (int kk = 1; kk < 4; ++kk)
-        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
-    }
-    b8 vf[2][2][2];
-    {
-      const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
+      for (int kb = 0; kb < 2; ++kb) {
+        if constexpr (TAIL) {
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int cc = dt * 32 + 16 * grp + 4 * p4;
-        const int chunk = cc >> 3, within = (cc & 7) * 2;
+          for (int r = 0; r < 16; ++r) {
+            const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            st[kb][r] = key < p.seq_kv ? csplat[r] : -INFINITY;
+          }
+          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], st[kb], 0, 0, 0);
+        } else {
+          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], csplat, 0, 0, 0);
+        }
+#pragma unroll
+        for (int kk = 1; kk < 4; ++kk)
+          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
+      }
+      // V^T fragments (transposed LDS reads), then the next tile's DMA
+      b8 vf[2][2][2];
+      {
+        const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int cc = dt * 32 + 16 * grp + 4 * p4;
+          const int chunk = cc >> 3, within = (cc & 7) * 2;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const int R0 = kb * 32 + 16 * s + 4 * hl + q4;
+              const int R1 = R0 + 8;
+              const s4v lo = tr_read(Vs + R0 * 128 + ((chunk ^ (((R0 >> 1) & 1) << 2)) << 4) + within);
+              const s4v hi = tr_read(Vs + R1 * 128 + ((chunk ^ (((R1 >> 1) & 1) << 2)) << 4) + within);
+              const s8v vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+              vf[dt][kb][s] = __builtin_bit_cast(b8, vv);
+            }
+        }
+      }
+      if (kt + 1 < k1) stage(cur ^ 1, kt + 1);
+
+      // P = exp2(S - m_ref) -> bf16 fragments, row partial sums (this lane's 32 keys)
+      b8 pf[2][2];
+      float ls;
+      auto exp_pack = [&](float shift) __attribute__((always_inline)) {
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const int R0 = kb * 32 + 16 * s + 4 * hl + q4;
-            const int R1 = R0 + 8;
-            const s4v lo = tr_read(Vs + R0 * 128 + ((chunk ^ (((R0 >> 1) & 1) << 2)) << 4) + within);
-            const s4v hi = tr_read(Vs + R1 * 128 + ((chunk ^ (((R1 >> 1) & 1) << 2)) << 4) + within);
-            const s8v vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            vf[dt][kb][s] = __builtin_bit_cast(b8, vv);
+            b8 t;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(st[kb][8 * s + j], SMUL, -shift));
+              a[j & 3] = add_s(a[j & 3], e);
+              t[j] = (__bf16)e;
+            }
+            pf[kb][s] = t;
           }
-      }
-    }
-    if (kt + 1 < nkt) stage(cur ^ 1, kt + 1);
-
-    // P = exp2(S - m_ref) -> bf16 fragments, row partial sums (this lane's 32 keys)
-    b8 pf[2][2];
-    float ls;
-    auto exp_pack = [&](float shift) __attribute__((always_inline)) {
-      float a[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          b8 t;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(st[kb][8 * s + j], SMUL, -shift));
-            if (!ATTN_SUM_MFMA) a[j & 3] = add_s(a[j & 3], e);
-            t[j] = (__bf16)e;
-          }
-          pf[kb][s] = t;
-        }
-      if (ATTN_SUM_MFMA) {  // row sums on the matrix pipe: ones(32x16) * P^T -> every row = the full 64-key sum
-        f32x16 acc;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        ls = add_s(add_s(a[0], a[1]), add_s(a[2], a[3]));
+      };
+      auto row_max = [&]() __attribute__((always_inline)) {
+        float mx = st[0][0];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-          for (int s = 0; s < 2; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pf[kb][s], acc, 0, 0, 0);
-        ls = acc[0];
+          for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb][r]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+        return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+      };
+      if constexpr (FIRST) {
+        const float d = row_max() * SMUL;  // finite: a segment's first tile always holds a valid key
+        set_ref(d);
+        exp_pack(d);
       } else {
-        ls = add_s(add_s(a[0], a[1]), add_s(a[2], a[3]));
+        const float cur_ref = ATTN_EXACT_SCALE ? m_ref : 0.f;  // (x - 0 folds: the MFMA produced s - m_ref)
+        exp_pack(cur_ref);
+        if (__builtin_expect(__any(!(ls <= REBASE_SUM)), 0)) {  // rebase (NaN-safe compare: inf sums rebase)
+          const float d = fmaxf(row_max() * SMUL - cur_ref, 0.f);
+          set_ref(m_ref + d);
+          const float alpha = __builtin_amdgcn_exp2f(-d);
+          l_run *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+          exp_pack(cur_ref + d);
+        }
       }
-    };
-    auto row_max = [&]() __attribute__((always_inline)) {
-      float mx = st[0][0];
+      l_run = add_s(l_run, ls);
+      // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[kb][r]);
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int s = 0; s < 2; ++s)
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
+      __syncthreads();
     };
-    if constexpr (FIRST) {
-      const float d = row_max() * SMUL;  // finite: the first tile always holds a valid key
-      set_ref(d);
-      exp_pack(d);
+
+    using T_ = std::integral_constant<bool, true>;
+    using F_ = std::integral_constant<bool, false>;
+    using S0 = std::integral_constant<int, 0>;
+    using S1 = std::integral_constant<int, 1>;
+    __syncthreads();
+    const bool tail_last = has_tail && k1 == nkt;
+    const int kf_end = tail_last ? k1 - 1 : k1;  // full tiles of this segment: [k0, kf_end)
+    if (kf_end == k0) {
+      tile(k0, T_(), T_(), S0());  // a one-tile segment on the partial last tile
     } else {
-      const float cur = ATTN_EXACT_SCALE ? m_ref : 0.f;  // (x - 0 folds: the MFMA already produced s - m_ref)
-      exp_pack(cur);
-      if (__builtin_expect(__any(!(ls <= REBASE_SUM)), 0)) {  // rebase (NaN-safe compare: inf sums rebase too)
-        const float d = fmaxf(row_max() * SMUL - cur, 0.f);
-        set_ref(m_ref + d);
-        const float alpha = __builtin_amdgcn_exp2f(-d);
-        l_run *= alpha;
+      tile(k0, T_(), F_(), S0());
+      int kt = k0 + 1;
+#pragma unroll 1
+      for (; kt + 1 < kf_end; kt += 2) {
+        tile(kt, F_(), F_(), S1());
+        tile(kt + 1, F_(), F_(), S0());
+      }
+      if (kt < kf_end) {
+        tile(kt, F_(), F_(), S1());
+        ++kt;
+      }
+      if (tail_last) {
+        if ((kt - k0) & 1) tile(kt, F_(), T_(), S1());
+        else tile(kt, F_(), T_(), S0());
+      }
+    }
+
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    const float inv = 1.f / l_tot;
+    if (k0 == 0 && k1 == nkt) {  // whole task in this workgroup: final output
+      if (qrow < p.seq_q) {
+        bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-        exp_pack(cur + d);
+          for (int gq = 0; gq < 4; ++gq) {
+            const int d = dt * 32 + 8 * gq + 4 * hl;
+            uint2 pk;
+            pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+            pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+            *reinterpret_cast<uint2*>(obase + d) = pk;
+          }
+        if (p.lse && hl == 0)
+          p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_ref + __log2f(l_tot)) * LN2;
       }
-    }
-    l_run = add_s(l_run, ls);
-    // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T (transposed LDS reads above)
+    } else {  // partial over tiles [k0, k1): normalised fp32 rows + LSE into this workgroup's slot
+      const int r = wave * 32 + l32;
+      float* po = sp.part_o + ((int64_t)slot * QBLK_WG + r) * 64;
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+      for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
-    __syncthreads();
-  };
-
-  using T_ = std::integral_constant<bool, true>;
-  using F_ = std::integral_constant<bool, false>;
-  using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
-  stage(0, 0);
-  __syncthreads();
-  if (nfull == 0) {
-    tile(0, T_(), T_(), S0());
-  } else {
-    tile(0, T_(), F_(), S0());
-    int kt = 1;
-    for (; kt + 1 < nfull; kt += 2) {
-      tile(kt, F_(), F_(), S1());
-      tile(kt + 1, F_(), F_(), S0());
-    }
-    if (kt < nfull) tile(kt, F_(), F_(), S1());
-    if (nfull < nkt) {
-      if (nfull & 1) tile(nfull, F_(), T_(), S1());
-      else tile(nfull, F_(), T_(), S0());
+        for (int gq = 0; gq < 4; ++gq) {
+          const int d = dt * 32 + 8 * gq + 4 * hl;
+          const f32x4 v = {o[dt][4 * gq] * inv, o[dt][4 * gq + 1] * inv, o[dt][4 * gq + 2] * inv,
+                           o[dt][4 * gq + 3] * inv};
+          *reinterpret_cast<f32x4*>(po + d) = v;
+        }
+      if (hl == 0) sp.part_lse[(int64_t)slot * QBLK_WG + r] = (m_ref + __log2f(l_tot)) * LN2;
     }
   }
+}
 
-  const float l_tot = ATTN_SUM_MFMA ? l_run : l_run + __shfl_xor(l_run, 32, 64);
-  if (qrow < p.seq_q) {
-    const float inv = 1.f / l_tot;
-    bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int d = dt * 32 + 8 * g + 4 * hl;
-        uint2 pk;
-        pk.x = pack_bf16x2(o[dt][4 * g + 0] * inv, o[dt][4 * g + 1] * inv);
-        pk.y = pack_bf16x2(o[dt][4 * g + 2] * inv, o[dt][4 * g + 3] * inv);
-        *reinterpret_cast<uint2*>(obase + d) = pk;
-      }
-    if (p.lse && hl == 0)
-      p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_ref + __log2f(l_tot)) * LN2;
+// Combines the K/V-chunk partials of the split tasks: one thread per (row, 4 columns) of a split task.
+template <int NW>
+__global__ void __launch_bounds__(256) attn_split_merge(AttnArgs p, SplitArgs sp, int nsplit_rows) {
+  constexpr int QBLK_WG = NW * 32;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= nsplit_rows * 16) return;
+  const int c4 = e & 15, rr = e >> 4;
+  const int tt = rr / QBLK_WG, r = rr % QBLK_WG;  // split-task index, row in the block
+  const int t = sp.n_dp + tt;
+  const int nqt = (p.seq_q + QBLK_WG - 1) / QBLK_WG;
+  const int qt = t % nqt, hb = t / nqt, h = hb % p.heads, b = hb / p.heads;
+  const int qrow = qt * QBLK_WG + r;
+  if (qrow >= p.seq_q) return;
+  const int s0 = tt * sp.chunks;
+  float mx = -INFINITY;
+  for (int c = 0; c < sp.chunks; ++c) mx = fmaxf(mx, sp.part_lse[(int64_t)(s0 + c) * QBLK_WG + r]);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float wsum = 0.f;
+  for (int c = 0; c < sp.chunks; ++c) {
+    const float w = __expf(sp.part_lse[(int64_t)(s0 + c) * QBLK_WG + r] - mx);
+    wsum += w;
+    acc += w * *reinterpret_cast<const f32x4*>(sp.part_o + ((int64_t)(s0 + c) * QBLK_WG + r) * 64 + c4 * 4);
   }
+  const float inv = 1.f / wsum;
+  uint2 pk;
+  pk.x = pack_bf16x2(acc[0] * inv, acc[1] * inv);
+  pk.y = pack_bf16x2(acc[2] * inv, acc[3] * inv);
+  *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64 + c4 * 4) = pk;
+  if (p.lse && c4 == 0) p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = mx + __logf(wsum);
 }
 
 // ------------------------------------------------------------------------------------------------ f32
@@ -571,6 +636,41 @@ extern "C" int mapa_attn_merge(const void* o_a, const float* lse_a, const void* 
   return 0;
 }
 
+namespace {
+constexpr int SK_NW = 4;  // waves per workgroup (4 x 32 query rows); 6/8-wave workgroups measured slower
+constexpr int SK_QBLK = SK_NW * 32;
+
+// Workgroups of attn_fwd_bf16 resident per CU: the 512-entry VGPR file over the kernel's allocation (one wave of
+// the 4-wave workgroup per SIMD), capped by LDS; MAPA_ATTN_WG_PER_CU overrides.  Cached per device.
+int sk_slots() {
+  static int cache[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (cache[dev]) return cache[dev];
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  hipFuncAttributes fa;
+  int per_cu = 2;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&attn_fwd_bf16<SK_NW, false>)) == hipSuccess &&
+      fa.numRegs > 0) {
+    const int alloc = (fa.numRegs + 7) / 8 * 8;
+    per_cu = 512 / alloc;
+    const int lds_cap = (160 * 1024) / (int)(fa.sharedSizeBytes > 0 ? fa.sharedSizeBytes : 32768);
+    if (lds_cap < per_cu) per_cu = lds_cap;
+    if (per_cu < 1) per_cu = 1;
+  }
+  if (const char* e = getenv("MAPA_ATTN_WG_PER_CU")) per_cu = atoi(e) > 0 ? atoi(e) : per_cu;
+  return cache[dev] = cus * per_cu;
+}
+
+int64_t sk_workspace_bytes(int slots) { return (int64_t)slots * SK_QBLK * (64 + 1) * sizeof(float); }
+}  // namespace
+
+extern "C" int64_t mapa_attention_workspace_bytes(const mapa_attn_desc* d) {
+  if (!d || d->dtype != MAPA_BF16) return 0;
+  return sk_workspace_bytes(sk_slots());
+}
+
 extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d != nullptr, "mapa_attention: null descriptor");
   MAPA_CHECK_ARG(d->batch > 0 && d->heads > 0 && d->seq_q > 0 && d->seq_kv > 0,
@@ -598,19 +698,40 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d->kv_nseg == 0 || tot == d->seq_kv, "mapa_attention: kv segments sum %lld != seq_kv %d",
                  (long long)tot, d->seq_kv);
   if (d->dtype == MAPA_BF16) {
-    // 4 waves x 32 query rows per workgroup, 3 workgroups per CU (6- and 8-wave workgroups measured slower:
-    // the per-tile barrier then spans more waves)
-    constexpr int nw = 4;
-    const int qblk = 32 * nw;
-    const int nblk = ((d->seq_q + qblk - 1) / qblk) * d->heads * d->batch;
+    const int ntask = ((d->seq_q + SK_QBLK - 1) / SK_QBLK) * d->heads * d->batch;
+    const int nkt = (d->seq_kv + KT - 1) / KT;
+    SplitArgs sp;
+    sp.part_o = nullptr;
+    sp.part_lse = nullptr;
+    sp.n_dp = ntask;
+    sp.chunks = 1;
+    // the remainder after the full waves of resident slots is cut into K/V chunks of >= 4 tiles (or not at all
+    // without a workspace)
+    const int slots = sk_slots();
+    const int rem = ntask % slots;
+    const int chunks = rem ? std::min(slots / rem, std::max(1, nkt / 4)) : 1;
+    if (chunks > 1 && d->workspace && d->workspace_bytes >= sk_workspace_bytes(slots) &&
+        getenv("MAPA_ATTN_NO_SPLIT") == nullptr) {
+      sp.n_dp = ntask - rem;
+      sp.chunks = chunks;
+      sp.part_o = reinterpret_cast<float*>(d->workspace);
+      sp.part_lse = sp.part_o + (int64_t)slots * SK_QBLK * 64;
+    }
+    const int grid = sp.n_dp + (ntask - sp.n_dp) * sp.chunks;
     if (a.nseg > 0)
-      hipLaunchKernelGGL((attn_fwd_bf16<nw, true>), dim3(nblk), dim3(nw * 64), 0, stream, a);
+      hipLaunchKernelGGL((attn_fwd_bf16<SK_NW, true>), dim3(grid), dim3(SK_NW * 64), 0, stream, a, sp);
     else
-      hipLaunchKernelGGL((attn_fwd_bf16<nw, false>), dim3(nblk), dim3(nw * 64), 0, stream, a);
-  } else {
-    const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
-    hipLaunchKernelGGL(attn_fwd_f32, dim3(nblk), dim3(NT), 0, stream, a);
+      hipLaunchKernelGGL((attn_fwd_bf16<SK_NW, false>), dim3(grid), dim3(SK_NW * 64), 0, stream, a, sp);
+    MAPA_CHECK_LAUNCH("mapa_attention");
+    if (sp.n_dp < ntask) {
+      const int rows = (ntask - sp.n_dp) * SK_QBLK;
+      hipLaunchKernelGGL((attn_split_merge<SK_NW>), dim3((rows * 16 + 255) / 256), dim3(256), 0, stream, a, sp, rows);
+      MAPA_CHECK_LAUNCH("mapa_attention (split merge)");
+    }
+    return 0;
   }
+  const int nblk = ((d->seq_q + QBLK - 1) / QBLK) * d->heads * d->batch;
+  hipLaunchKernelGGL(attn_fwd_f32, dim3(nblk), dim3(NT), 0, stream, a);
   MAPA_CHECK_LAUNCH("mapa_attention");
   return 0;
 }

@@ -23,7 +23,7 @@ ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_POST = 0, 1, 2, 3
 # Every extern "C" symbol declared in include/mapa.h (checked by tests/test_capi.py).
 EXPORTED = (
     "mapa_last_error", "mapa_version", "mapa_device_check", "mapa_gemm", "mapa_gemm_workspace_bytes",
-    "mapa_gemm_set_variant", "mapa_attention", "mapa_layernorm",
+    "mapa_gemm_set_variant", "mapa_attention", "mapa_attention_workspace_bytes", "mapa_layernorm",
     "mapa_patchify", "mapa_assemble_tokens", "mapa_add_rowvec", "mapa_bilinear_ac", "mapa_mean_tokens",
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
@@ -55,7 +55,7 @@ class AttnDesc(ctypes.Structure):
         ("k_bstride", ctypes.c_int64), ("k_rstride", ctypes.c_int64), ("v_bstride", ctypes.c_int64),
         ("v_rstride", ctypes.c_int64), ("o_bstride", ctypes.c_int64), ("o_rstride", ctypes.c_int64),
         ("lse", ctypes.c_void_p), ("kv_nseg", ctypes.c_int), ("kv_seg_start", ctypes.c_int * 16),
-        ("kv_seg_len", ctypes.c_int * 16),
+        ("kv_seg_len", ctypes.c_int * 16), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
     ]
 
 
@@ -86,6 +86,8 @@ def load_library(path: Optional[str] = None):
     L.mapa_gemm_workspace_bytes.restype = i64
     L.mapa_gemm_set_variant.argtypes = [i]
     L.mapa_attention.argtypes = [ctypes.POINTER(AttnDesc), vp]
+    L.mapa_attention_workspace_bytes.argtypes = [ctypes.POINTER(AttnDesc)]
+    L.mapa_attention_workspace_bytes.restype = i64
     L.mapa_layernorm.argtypes = [vp, i64, i, i, vp, vp, f, vp, vp, i, i64, i, i64, i, vp]
     L.mapa_patchify.argtypes = [vp, i, i, i, vp, i, i, vp]
     L.mapa_assemble_tokens.argtypes = [vp, vp, vp, i, i, i, vp, vp]
@@ -193,6 +195,7 @@ def _toc(tok, kind, flops=0.0):
 # ------------------------------------------------------------------------------------------------ wrappers
 _WS_NEED = {}
 _WS = {}
+_AWS = {}
 
 
 def gemm_workspace(nbytes: int) -> torch.Tensor:
@@ -205,6 +208,18 @@ def gemm_workspace(nbytes: int) -> torch.Tensor:
     if ws is None or ws.numel() < nbytes:
         ws = _WS[key] = torch.zeros(max(nbytes, 0 if ws is None else ws.numel()), dtype=torch.uint8,
                                     device="cuda")
+    return ws
+
+
+def attention_workspace(d) -> torch.Tensor:
+    """Scratch for the stream-K attention partials (fp32 rows + LSE of the tasks that a workgroup range cuts);
+    one buffer per device and stream, sized once by mapa_attention_workspace_bytes (it depends on the device's
+    resident workgroup count only).  Contents are never read across calls."""
+    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
+    ws = _AWS.get(key)
+    if ws is None:
+        need = int(lib().mapa_attention_workspace_bytes(ctypes.byref(d)))
+        ws = _AWS[key] = torch.empty(max(need, 16), dtype=torch.uint8, device="cuda")
     return ws
 
 
@@ -266,6 +281,9 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
     d.v_bstride, d.v_rstride = v_bstride, v_rstride
     d.o_bstride, d.o_rstride = o_bstride, o_rstride
     d.lse = None if lse is None else lse.data_ptr()
+    if d.dtype == BF16:
+        ws = attention_workspace(d)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if kv_segments:
         if len(kv_segments) > 16:
             raise NativeError("at most 16 K/V segments")

@@ -72,7 +72,10 @@ def main():
                       f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
             nat.gemm_set_variant(0)
     if what in ("attn", "all"):
-        for name, B, Hh, S in [("enc", V, 16, T + 1), ("frame", V, 12, T), ("global", 1, 12, L)]:
+        cases = [("enc", V, 16, T + 1), ("frame", V, 12, T), ("global", 1, 12, L)]
+        if os.environ.get("KB_ATTN_WIDE"):
+            cases += [("global1", 1, 12, T + 1), ("global32", 1, 12, 32 * T + 1)]
+        for name, B, Hh, S in cases:
             C = Hh * 64
             qkv = torch.randn(B * S, 3 * C, device="cuda").to(dt)
             o = torch.empty(B * S, C, device="cuda", dtype=dt)
