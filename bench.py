@@ -140,6 +140,14 @@ def main():
                         "per_kernel": {k: {"ms_per_step": v["ms"] / args.steps,
                                            "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["flops"] else None}
                                        for k, v in ktimes.items()}}
+        xattn = None
+        if ktimes.get("attention_global", {}).get("flops"):
+            # north_star target: >= 40 % MFMA utilisation in the cross-view (global AAT) attention kernel
+            v = ktimes["attention_global"]
+            tf = v["flops"] / (v["ms"] * 1e-3) / 1e12
+            xattn = {"kernel": "attn_fwd_bf16 (global AAT layers, L = V*1369+1 keys)", "achieved": tf,
+                     "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS, "target_frac": 0.40,
+                     "ms_per_step": v["ms"] / args.steps, "launches_per_step": v["count"] / args.steps}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.geometric:
             cpu = cpu_baseline(model, imgs, H, W)
@@ -159,6 +167,7 @@ def main():
                        "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else "single"},
             "tflops_effective": (gf_view * value) if gf_view else None,
             "roofline": roofline,
+            "cross_view_attention": xattn,
             "cpu_baseline": cpu,
             "hip_graphs": bool(model.hip_graphs and world == 1 and not args.geometric),
         }

@@ -86,6 +86,9 @@ __device__ __forceinline__ float add_s(float a, float b) { return a + b; }
 //    exp2(-d), P recomputed.  The first tile always takes the exact path (m_ref := its row max).
 // Exact softmax either way: O / l is invariant to the reference (the LSE output adds m_ref back).
 constexpr float REBASE_SUM = 256.f;
+#ifndef ATTN_PRIO
+#define ATTN_PRIO 0  // s_setprio experiments: 1 = around both MFMA blocks, 2 = around P.V, 3 = around the softmax
+#endif
 #ifndef ATTN_EXACT_SCALE
 #define ATTN_EXACT_SCALE 0
 #endif
@@ -255,6 +258,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
       }
       // S^T - m_ref = K Q^T + C, C = -m_ref (masked keys of the tail tile: -inf)
       f32x16 st[2];
+      if (ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         if constexpr (TAIL) {
@@ -271,6 +275,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         for (int kk = 1; kk < 4; ++kk)
           st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
       }
+      if (ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(0);
+      if (ATTN_PRIO == 3) __builtin_amdgcn_s_setprio(1);
       // V^T fragments (transposed LDS reads), then the next tile's DMA
       b8 vf[2][2][2];
       {
@@ -343,6 +349,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         }
       }
       l_run = add_s(l_run, ls);
+      if (ATTN_PRIO == 3) __builtin_amdgcn_s_setprio(0);
+      if (ATTN_PRIO == 1 || ATTN_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
@@ -351,6 +359,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 #pragma unroll
           for (int s = 0; s < 2; ++s)
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
+      if (ATTN_PRIO == 1 || ATTN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
       __syncthreads();
     };
 

@@ -270,8 +270,9 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
 
 
 def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, k_bstride, k_rstride,
-              v_bstride, v_rstride, o_bstride, o_rstride, lse=None, kv_segments=None):
-    """q/k/v/o are tensors whose data_ptr is the (b=0, h=0, i=0, d=0) element."""
+              v_bstride, v_rstride, o_bstride, o_rstride, lse=None, kv_segments=None, kind="attention"):
+    """q/k/v/o are tensors whose data_ptr is the (b=0, h=0, i=0, d=0) element.  `kind` labels the launch for the
+    per-kernel timing (bench.py: "attention_global" = the cross-view AAT layers)."""
     d = AttnDesc()
     d.dtype = dt_code(q.dtype)
     d.batch, d.heads, d.seq_q, d.seq_kv = batch, heads, seq_q, seq_kv
@@ -292,7 +293,7 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
             d.kv_seg_start[i], d.kv_seg_len[i] = st, ln
     tok = _tic()
     check(lib().mapa_attention(ctypes.byref(d), stream()), "mapa_attention")
-    _toc(tok, "attention", 4.0 * batch * heads * seq_q * seq_kv * 64)
+    _toc(tok, kind, 4.0 * batch * heads * seq_q * seq_kv * 64)
 
 
 def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, ldy=None, group=0,

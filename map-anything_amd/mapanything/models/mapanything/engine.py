@@ -260,14 +260,15 @@ class MapaEngine:
         return OH, OW
 
     # ------------------------------------------------------------------------------------ transformer block
-    def _block(self, x, xn, qkv, ao, hbuf, rows, dim, heads, p, *, attn_batch, attn_seq, gamma=True):
+    def _block(self, x, xn, qkv, ao, hbuf, rows, dim, heads, p, *, attn_batch, attn_seq, gamma=True,
+               attn_kind="attention"):
         lp = self.lp
         self._ln(x, rows, dim, p["n1w"], p["n1b"], y_lp=xn)
         nat.gemm(xn, p["qkv"], rows, 3 * dim, dim, bias=p["qkv_b"], out_lp=qkv)
         rs = 3 * dim
         nat.attention(qkv, qkv[:, dim:], qkv[:, 2 * dim:], ao, batch=attn_batch, heads=heads, seq_q=attn_seq,
                       seq_kv=attn_seq, q_bstride=attn_seq * rs, q_rstride=rs, k_bstride=attn_seq * rs, k_rstride=rs,
-                      v_bstride=attn_seq * rs, v_rstride=rs, o_bstride=attn_seq * dim, o_rstride=dim)
+                      v_bstride=attn_seq * rs, v_rstride=rs, o_bstride=attn_seq * dim, o_rstride=dim, kind=attn_kind)
         nat.gemm(ao, p["proj"], rows, dim, dim, bias=p["proj_b"], gamma=p.get("ls1") if gamma else None,
                  resid1=x, out_f32=x)
         self._ln(x, rows, dim, p["n2w"], p["n2b"], y_lp=xn)
@@ -452,7 +453,8 @@ class MapaEngine:
         for d, p in enumerate(w.aat):
             if d % 2 == 0:   # global attention over every view + the scale token
                 if shard is None:
-                    self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False)
+                    self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False,
+                                attn_kind="attention_global")
                 else:
                     self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm)
             else:            # frame attention inside each view; the scale token bypasses the block
@@ -493,7 +495,7 @@ class MapaEngine:
         if not overlap:
             comm.allgather_slots(kv_full, shard.max_rows)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
-                          kv_segments=shard.kv_segments(), **strides)
+                          kv_segments=shard.kv_segments(), kind="attention_global", **strides)
         else:
             handle = comm.allgather_slots_async(kv_full, shard.max_rows)
             segs = shard.kv_segments()
@@ -501,12 +503,12 @@ class MapaEngine:
             rest = [sg for r, sg in enumerate(segs) if r != shard.rank]
             lse_l = self._empty(AAT_HEADS, L, dtype=torch.float32)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=own[1], kv_segments=[own], lse=lse_l,
-                          **strides)
+                          kind="attention_global", **strides)
             handle.wait()
             ao_r = self._empty(L, C)
             lse_r = self._empty(AAT_HEADS, L, dtype=torch.float32)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao_r, seq_kv=sum(sg[1] for sg in rest), kv_segments=rest,
-                          lse=lse_r, **strides)
+                          lse=lse_r, kind="attention_global", **strides)
             nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, AAT_HEADS, C)
         nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
         self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)

@@ -17,6 +17,9 @@ GEMMS = [("enc.qkv", R, 3072, 1024), ("enc.proj", R, 1024, 1024), ("enc.fc1", R,
          ("aat.fc1", L, 3072, 768), ("aat.fc2", L, 768, 3072), ("pose.res", V * T, 784, 784)]
 if os.environ.get("KB_SQ"):
     GEMMS = [("sq4096", 4096, 4096, 4096), ("sq8192", 8192, 8192, 8192)]
+if os.environ.get("KB_SHAPES"):  # "M,N,K;M,N,K" ad-hoc GEMM shapes
+    GEMMS = [(f"{m}x{n}x{k}", int(m), int(n), int(k))
+             for m, n, k in (t.split(",") for t in os.environ["KB_SHAPES"].split(";"))]
 ONLY = os.environ.get("KB_ONLY")
 VARIANTS = [int(v) for v in os.environ.get("KB_VARIANTS", "0").split(",")]
 if ONLY:
