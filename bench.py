@@ -49,6 +49,8 @@ def main():
                     help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1", "pmc_traffic.json"),
                     help="HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_summary.py)")
+    ap.add_argument("--attn-pmc-json", default=os.path.join(REPO, "profiles", "r1", "attn_global_pmc.json"),
+                    help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,6 +150,11 @@ def main():
             xattn = {"kernel": "attn_fwd_bf16 (global AAT layers, L = V*1369+1 keys)", "achieved": tf,
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS, "target_frac": 0.40,
                      "ms_per_step": v["ms"] / args.steps, "launches_per_step": v["count"] / args.steps}
+            if os.path.exists(args.attn_pmc_json):
+                # MFMA-pipe busy fraction at the clock the chip really ran (rocprofv3 PMC pass, tools/attn_pmc.sh)
+                pj = json.load(open(args.attn_pmc_json))
+                xattn["pmc"] = {k: pj.get(k) for k in ("mfma_busy_frac", "clock_ghz", "valu_insts_per_mfma",
+                                                       "valu_coexec_frac_of_mfma_busy")}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.geometric:
             cpu = cpu_baseline(model, imgs, H, W)

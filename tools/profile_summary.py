@@ -2,6 +2,7 @@
 
   python tools/profile_summary.py stats <kernel_stats.csv> [bench.json]      -> per-group calls / avg / total
   python tools/profile_summary.py traffic <fetch_pmc.csv> <write_pmc.csv>    -> HBM bytes per launch per group
+  python tools/profile_summary.py mfma <kernel-regex> <pmc.csv>...           -> MFMA-pipe utilisation at the real clock
 
 Groups: "gemm" = dense GEMM instantiations (A mode 0), "conv3x3" = implicit-GEMM convs (A mode 1), "attention",
 "layernorm", "other".  FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB; on gfx950 FETCH_SIZE counts
@@ -66,8 +67,44 @@ def traffic(fetch_csv, write_csv):
     return out
 
 
+def mfma(pattern, paths):
+    """Per-dispatch MFMA-pipe busy fraction of the kernels matching `pattern`, at the clock the chip actually ran.
+
+    SQ counters are summed over the 32 shader engines: clock = SQ_CYCLES / 32 / duration.  SQ_VALU_MFMA_BUSY_CYCLES
+    sums busy cycles over all 1024 SIMDs (it equals SQ_INSTS_MFMA x 32 for v_mfma_f32_32x32x16_bf16), so
+    busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x clock x duration)."""
+    per = defaultdict(dict)  # (file, dispatch) -> counters
+    for path in paths:
+        for r in csv.DictReader(open(path)):
+            if not re.search(pattern, r["Kernel_Name"]):
+                continue
+            d = per[(path, r["Dispatch_Id"])]
+            d[r["Counter_Name"]] = float(r["Counter_Value"])
+            d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    agg = defaultdict(list)
+    for d in per.values():
+        for k, v in d.items():
+            agg[k].append(v)
+    mean = {k: sum(v) / len(v) for k, v in agg.items()}
+    out = {"dispatches_per_pass": len(per) // max(1, len(paths)), "counters_mean": mean}
+    if "SQ_CYCLES" in mean:
+        clk = mean["SQ_CYCLES"] / 32.0 / mean["dur_ns"]
+        out["clock_ghz"] = clk
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in mean:
+            out["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * clk * mean["dur_ns"])
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in mean and "SQ_VALU_MFMA_COEXEC_CYCLES" in mean:
+        out["valu_coexec_frac_of_mfma_busy"] = mean["SQ_VALU_MFMA_COEXEC_CYCLES"] / mean["SQ_VALU_MFMA_BUSY_CYCLES"]
+    if "SQ_INSTS_VALU" in mean and "SQ_INSTS_MFMA" in mean:
+        out["valu_insts_per_mfma"] = (mean["SQ_INSTS_VALU"] - mean["SQ_INSTS_MFMA"]) / mean["SQ_INSTS_MFMA"]
+    if "SQ_WAIT_INST_ANY" in mean and "SQ_WAVE_CYCLES" in mean:
+        out["wait_inst_frac_of_wave_cycles"] = mean["SQ_WAIT_INST_ANY"] / mean["SQ_WAVE_CYCLES"]
+    return out
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    if sys.argv[1] == "mfma":
+        print(json.dumps(mfma(sys.argv[2], sys.argv[3:]), indent=1))
+    elif sys.argv[1] == "stats":
         print(json.dumps(stats(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None), indent=1))
     else:
         print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
