@@ -86,16 +86,6 @@ __device__ __forceinline__ float add_s(float a, float b) { return a + b; }
 //    exp2(-d), P recomputed.  The first tile always takes the exact path (m_ref := its row max).
 // Exact softmax either way: O / l is invariant to the reference (the LSE output adds m_ref back).
 constexpr float REBASE_SUM = 256.f;
-#ifndef ATTN_PRIO
-#define ATTN_PRIO 0  // s_setprio experiments: 1 = around both MFMA blocks, 2 = around P.V, 3 = around the softmax
-#endif
-#ifndef ATTN_EXACT_SCALE
-#define ATTN_EXACT_SCALE 0
-#endif
-// scores leave the MFMA in the log2 domain (Q pre-scaled by log2(e)/8, one bf16 rounding) or, with
-// ATTN_EXACT_SCALE, in natural units (Q scaled by the exact 1/8) and enter exp2 through one fma by log2(e)
-// (measured 3 % slower; the same for summing P on the MFMA pipe with a ones operand: 5 % slower)
-constexpr float SMUL = ATTN_EXACT_SCALE ? LOG2E : 1.f;
 
 // Work split.  A task = (batch, head, 128-row query block).  The grid holds n_dp whole tasks (data-parallel, the
 // full waves of the device's resident workgroup slots) followed by the remaining tasks each cut into `chunks`
@@ -211,7 +201,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
         b8 sc;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E / SMUL));
+        for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E));
         qf[kk] = sc;
       }
     }
@@ -229,10 +219,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
     for (int r = 0; r < 16; ++r) csplat[r] = 0.f;
     auto set_ref = [&](float m) __attribute__((always_inline)) {
       m_ref = m;
-      if (!ATTN_EXACT_SCALE) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) csplat[r] = -m;
-      }
+      for (int r = 0; r < 16; ++r) csplat[r] = -m;
     };
 
     // One K/V tile: S^T = K Q^T, softmax, O^T += V^T P^T.  FIRST (a segment's first tile) sets m_ref; TAIL (the
@@ -258,7 +246,6 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
       }
       // S^T - m_ref = K Q^T + C, C = -m_ref (masked keys of the tail tile: -inf)
       f32x16 st[2];
-      if (ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         if constexpr (TAIL) {
@@ -275,8 +262,6 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         for (int kk = 1; kk < 4; ++kk)
           st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
       }
-      if (ATTN_PRIO == 1) __builtin_amdgcn_s_setprio(0);
-      if (ATTN_PRIO == 3) __builtin_amdgcn_s_setprio(1);
       // V^T fragments (transposed LDS reads), then the next tile's DMA
       b8 vf[2][2][2];
       {
@@ -312,7 +297,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
             b8 t;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const float e = __builtin_amdgcn_exp2f(__builtin_fmaf(st[kb][8 * s + j], SMUL, -shift));
+              const float e = __builtin_amdgcn_exp2f(st[kb][8 * s + j] - shift);
               a[j & 3] = add_s(a[j & 3], e);
               t[j] = (__bf16)e;
             }
@@ -330,14 +315,14 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
       };
       if constexpr (FIRST) {
-        const float d = row_max() * SMUL;  // finite: a segment's first tile always holds a valid key
+        const float d = row_max();  // finite: a segment's first tile always holds a valid key
         set_ref(d);
         exp_pack(d);
       } else {
-        const float cur_ref = ATTN_EXACT_SCALE ? m_ref : 0.f;  // (x - 0 folds: the MFMA produced s - m_ref)
+        const float cur_ref = 0.f;  // (x - 0 folds: the MFMA produced s - m_ref)
         exp_pack(cur_ref);
         if (__builtin_expect(__any(!(ls <= REBASE_SUM)), 0)) {  // rebase (NaN-safe compare: inf sums rebase)
-          const float d = fmaxf(row_max() * SMUL - cur_ref, 0.f);
+          const float d = fmaxf(row_max() - cur_ref, 0.f);
           set_ref(m_ref + d);
           const float alpha = __builtin_amdgcn_exp2f(-d);
           l_run *= alpha;
@@ -349,8 +334,6 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         }
       }
       l_run = add_s(l_run, ls);
-      if (ATTN_PRIO == 3) __builtin_amdgcn_s_setprio(0);
-      if (ATTN_PRIO == 1 || ATTN_PRIO == 2) __builtin_amdgcn_s_setprio(1);
       // O^T += V^T P^T : B = P^T straight from the S^T accumulator, A = V^T
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
@@ -359,7 +342,6 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 #pragma unroll
           for (int s = 0; s < 2; ++s)
             o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
-      if (ATTN_PRIO == 1 || ATTN_PRIO == 2) __builtin_amdgcn_s_setprio(0);
       __syncthreads();
     };
 
