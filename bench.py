@@ -49,6 +49,8 @@ def main():
                     help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1", "pmc_traffic.json"),
                     help="HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_summary.py)")
+    ap.add_argument("--mfma-pmc-json", default=os.path.join(REPO, "profiles", "r1", "pmc_mfma.json"),
+                    help="per-kernel-group MFMA busy fraction + clock from a rocprofv3 SQ pass (tools/gpu_pmc.sh)")
     ap.add_argument("--attn-pmc-json", default=os.path.join(REPO, "profiles", "r1", "attn_global_pmc.json"),
                     help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh)")
     args = ap.parse_args()
@@ -133,9 +135,14 @@ def main():
             if os.path.exists(args.traffic_json):
                 tj = json.load(open(args.traffic_json)).get(kind)
                 traffic = tj["hbm_bytes_per_launch"] if tj else None
+            mfma_pmc = None
+            if os.path.exists(args.mfma_pmc_json):
+                # MFMA-pipe busy fraction + clock of this kernel class from a rocprofv3 SQ-counter pass
+                mfma_pmc = json.load(open(args.mfma_pmc_json)).get(kind)
             roofline = {"kernel": kind, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                         "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
                         "traffic": traffic, "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)",
+                        "pmc": mfma_pmc,
                         "launches": kt["count"], "avg_launch_us": kt["ms"] * 1e3 / kt["count"],
                         "timing_pass": {"ms_per_step": instr_ms, "launch": "eager, event pair per native call",
                                         "note": "same K steps re-run after the timed region"},

@@ -3,6 +3,7 @@
   python tools/profile_summary.py stats <kernel_stats.csv> [bench.json]      -> per-group calls / avg / total
   python tools/profile_summary.py traffic <fetch_pmc.csv> <write_pmc.csv>    -> HBM bytes per launch per group
   python tools/profile_summary.py mfma <kernel-regex> <pmc.csv>...           -> MFMA-pipe utilisation at the real clock
+  python tools/profile_summary.py mfma_groups <pmc.csv>                      -> the same per kernel group (bench run)
 
 Groups: "gemm" = dense GEMM instantiations (A mode 0), "conv3x3" = implicit-GEMM convs (A mode 1), "attention",
 "layernorm", "other".  FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB; on gfx950 FETCH_SIZE counts
@@ -101,8 +102,36 @@ def mfma(pattern, paths):
     return out
 
 
+def mfma_groups(path):
+    """Per kernel group (as bench.py names them): time-weighted MFMA-pipe busy fraction and mean clock over every
+    dispatch of a PMC pass with SQ_CYCLES + SQ_VALU_MFMA_BUSY_CYCLES (see mfma())."""
+    per = defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        d = per[r["Dispatch_Id"]]
+        d["group"] = group(r["Kernel_Name"])
+        d[r["Counter_Name"]] = float(r["Counter_Value"])
+        d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    acc = defaultdict(lambda: {"launches": 0, "busy": 0.0, "simd_cycles": 0.0, "cycles": 0.0, "ns": 0.0})
+    for d in per.values():
+        if "SQ_CYCLES" not in d or "SQ_VALU_MFMA_BUSY_CYCLES" not in d or d["dur_ns"] <= 0:
+            continue
+        a = acc[d["group"]]
+        clk = d["SQ_CYCLES"] / 32.0 / d["dur_ns"]
+        a["launches"] += 1
+        a["busy"] += d["SQ_VALU_MFMA_BUSY_CYCLES"]
+        a["simd_cycles"] += 1024.0 * clk * d["dur_ns"]
+        a["cycles"] += d["SQ_CYCLES"] / 32.0
+        a["ns"] += d["dur_ns"]
+    return {k: {"launches": v["launches"], "mfma_busy_frac": v["busy"] / v["simd_cycles"],
+                "clock_ghz": v["cycles"] / v["ns"],
+                "note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x SQ_CYCLES/32 per dispatch), summed over launches"}
+            for k, v in acc.items() if v["simd_cycles"] > 0}
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "mfma":
+    if sys.argv[1] == "mfma_groups":
+        print(json.dumps(mfma_groups(sys.argv[2]), indent=1))
+    elif sys.argv[1] == "mfma":
         print(json.dumps(mfma(sys.argv[2], sys.argv[3:]), indent=1))
     elif sys.argv[1] == "stats":
         print(json.dumps(stats(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None), indent=1))
