@@ -160,7 +160,8 @@ def main():
             if os.path.exists(args.attn_pmc_json):
                 # MFMA-pipe busy fraction at the clock the chip really ran (rocprofv3 PMC pass, tools/attn_pmc.sh)
                 pj = json.load(open(args.attn_pmc_json))
-                xattn["pmc"] = {k: pj.get(k) for k in ("mfma_busy_frac", "clock_ghz", "valu_insts_per_mfma",
+                xattn["pmc"] = {k: pj.get(k) for k in ("mfma_busy_frac", "mfma_busy_frac_lower", "clock_ghz",
+                                                       "clock_ghz_upper", "valu_insts_per_mfma",
                                                        "valu_coexec_frac_of_mfma_busy")}
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.geometric:

@@ -300,7 +300,7 @@ static int forced_variant() {
 // Stream-K variants (2580 + v) are chosen only when the caller passes a workspace; 0 = none.
 int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   const int f = forced_variant();
-  if (f) return f >= 2580 && f <= 2581 ? f : 0;
+  if (f) return f >= 2580 && f <= 2582 ? f : 0;
   (void)dtype; (void)conv; (void)M; (void)N; (void)K;
   return 0;
 }
@@ -376,7 +376,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2574) || variant == 2580 || variant == 2581,
+                     (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582),
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;

@@ -11,6 +11,8 @@
 //    applied on the per-lane SOURCE address -> conflict-free ds_read_b128 fragment reads).
 //  * K tile t+1 is DMA'd into the other stage while tile t is multiplied; one barrier per K tile.
 //  * Epilogue: each wave stages 32 x 64 fp32 of its accumulators through LDS and stores 16-B row segments.
+#include <algorithm>
+
 #include "gemm_internal.h"
 
 namespace mapa_gemm_impl {
@@ -773,8 +775,8 @@ static int sk_cus() {
 }
 
 static void sk_shape(int variant, int& bn, int& per_cu) {
-  bn = variant == 0 ? 128 : 256;
-  per_cu = variant == 0 ? 2 : 1;
+  bn = variant == 1 ? 256 : 128;
+  per_cu = variant == 1 ? 1 : 2;
 }
 
 // Ticket words live in a fixed-size head shared by every shape (a shape-dependent split would let one shape's slabs
@@ -782,7 +784,7 @@ static void sk_shape(int variant, int& bn, int& per_cu) {
 constexpr int64_t SK_MAX_TILES = 65536, SK_TICKET_BYTES = SK_MAX_TILES * 4;
 
 int64_t streamk_workspace_bytes(int M, int N, int variant) {
-  if (variant < 0 || variant > 1) return 0;
+  if (variant < 0 || variant > 2) return 0;
   int bn, per_cu;
   sk_shape(variant, bn, per_cu);
   const int64_t tiles = (int64_t)((M + BBM - 1) / BBM) * ((N + bn - 1) / bn);
@@ -792,7 +794,7 @@ int64_t streamk_workspace_bytes(int M, int N, int variant) {
 }
 
 bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
-  if (variant < 0 || variant > 1 || !ws) return false;
+  if (variant < 0 || variant > 2 || !ws) return false;
   const int64_t need = streamk_workspace_bytes(a.M, a.N, variant);
   if (need == 0 || ws_bytes < need) return false;
   int bn, per_cu;
@@ -807,17 +809,30 @@ bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, in
   const int g = sk_cus() * per_cu;
   // Data-parallel whole tiles for all but the last one-to-two waves; stream-K spreads the rest evenly, so at most
   // ~one tile per block is split (each split costs a 128-256 KB slab write + read).
-  static const int dp_env = getenv("MAPA_SK_DP") ? atoi(getenv("MAPA_SK_DP")) : 1;  // tuning: 0 = pure stream-K
-  s.dp_tiles = (dp_env && tiles >= 2 * g) ? (int)((tiles / g - 1) * g) : 0;
-  s.base = s.dp_tiles * s.nk;
-  s.per = (s.total - s.base + g - 1) / g;
-  static const int per_env = getenv("MAPA_SK_PER") ? atoi(getenv("MAPA_SK_PER")) : 0;  // tuning: iterations/block
-  if (per_env > s.per) s.per = per_env;  // only coarser: G stays within the workspace's slab count
-  const int G = (s.total - s.base + s.per - 1) / s.per;
+  int G;
+  if (variant == 2) {
+    // tail-only stream-K: every full wave of resident tiles runs data-parallel; only the iterations of the last,
+    // partial wave are spread (in chunks of >= nk/4 K-steps, so a split tile has at most 4 contributors)
+    s.dp_tiles = (int)((tiles / g) * g);
+    s.base = s.dp_tiles * s.nk;
+    const int rem = s.total - s.base;
+    s.per = std::max((rem + g - 1) / g, std::max(1, s.nk / 4));
+    G = g;  // blocks past the stream-K ranges only take data-parallel tiles
+  } else {
+    // Data-parallel whole tiles for all but the last one-to-two waves; stream-K spreads the rest evenly, so at most
+    // ~one tile per block is split (each split costs a 128-256 KB slab write + read).
+    static const int dp_env = getenv("MAPA_SK_DP") ? atoi(getenv("MAPA_SK_DP")) : 1;  // tuning: 0 = pure stream-K
+    s.dp_tiles = (dp_env && tiles >= 2 * g) ? (int)((tiles / g - 1) * g) : 0;
+    s.base = s.dp_tiles * s.nk;
+    s.per = (s.total - s.base + g - 1) / g;
+    static const int per_env = getenv("MAPA_SK_PER") ? atoi(getenv("MAPA_SK_PER")) : 0;  // tuning: iterations/block
+    if (per_env > s.per) s.per = per_env;  // only coarser: G stays within the workspace's slab count
+    G = (s.total - s.base + s.per - 1) / s.per;
+  }
   s.tickets = reinterpret_cast<int*>(ws);
   s.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + SK_TICKET_BYTES);
   void (*k)(GemmArgs, SkArgs);
-  if (variant == 0) k = conv ? gemm_sk_kernel<1, 128, 64, 3, 1, 4> : gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
+  if (variant != 1) k = conv ? gemm_sk_kernel<1, 128, 64, 3, 1, 4> : gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
   else k = conv ? gemm_sk_kernel<1, 256, 64, 3, 1, 1> : gemm_sk_kernel<0, 256, 64, 3, 1, 1>;
   hipLaunchKernelGGL(k, dim3(G), dim3(BTHREADS), 0, stream, a, s);
   return true;

@@ -71,9 +71,11 @@ def traffic(fetch_csv, write_csv):
 def mfma(pattern, paths):
     """Per-dispatch MFMA-pipe busy fraction of the kernels matching `pattern`, at the clock the chip actually ran.
 
-    SQ counters are summed over the 32 shader engines: clock = SQ_CYCLES / 32 / duration.  SQ_VALU_MFMA_BUSY_CYCLES
-    sums busy cycles over all 1024 SIMDs (it equals SQ_INSTS_MFMA x 32 for v_mfma_f32_32x32x16_bf16), so
-    busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x clock x duration)."""
+    SQ counters are summed over the 32 shader engines.  SQ_VALU_MFMA_BUSY_CYCLES sums busy cycles over all 1024
+    SIMDs (it equals SQ_INSTS_MFMA x 32 for v_mfma_f32_32x32x16_bf16), so the busy fraction over the cycles the
+    sequencers had work = SQ_VALU_MFMA_BUSY_CYCLES / (1024 x SQ_BUSY_CYCLES / 32), and the clock = SQ_BUSY_CYCLES / 32
+    / duration.  (SQ_CYCLES / 32 / duration reads above the 2.4 GHz maximum on short kernels — its window is wider
+    than the dispatch timestamps — so it is reported only as an upper-bound clock.)"""
     per = defaultdict(dict)  # (file, dispatch) -> counters
     for path in paths:
         for r in csv.DictReader(open(path)):
@@ -88,11 +90,14 @@ def mfma(pattern, paths):
             agg[k].append(v)
     mean = {k: sum(v) / len(v) for k, v in agg.items()}
     out = {"dispatches_per_pass": len(per) // max(1, len(paths)), "counters_mean": mean}
-    if "SQ_CYCLES" in mean:
-        clk = mean["SQ_CYCLES"] / 32.0 / mean["dur_ns"]
-        out["clock_ghz"] = clk
+    if "SQ_BUSY_CYCLES" in mean:
+        out["clock_ghz"] = mean["SQ_BUSY_CYCLES"] / 32.0 / mean["dur_ns"]
         if "SQ_VALU_MFMA_BUSY_CYCLES" in mean:
-            out["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * clk * mean["dur_ns"])
+            out["mfma_busy_frac"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * mean["SQ_BUSY_CYCLES"] / 32.0)
+    if "SQ_CYCLES" in mean:
+        out["clock_ghz_upper"] = mean["SQ_CYCLES"] / 32.0 / mean["dur_ns"]
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in mean:
+            out["mfma_busy_frac_lower"] = mean["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024.0 * mean["SQ_CYCLES"] / 32.0)
     if "SQ_VALU_MFMA_BUSY_CYCLES" in mean and "SQ_VALU_MFMA_COEXEC_CYCLES" in mean:
         out["valu_coexec_frac_of_mfma_busy"] = mean["SQ_VALU_MFMA_COEXEC_CYCLES"] / mean["SQ_VALU_MFMA_BUSY_CYCLES"]
     if "SQ_INSTS_VALU" in mean and "SQ_INSTS_MFMA" in mean:
@@ -103,29 +108,28 @@ def mfma(pattern, paths):
 
 
 def mfma_groups(path):
-    """Per kernel group (as bench.py names them): time-weighted MFMA-pipe busy fraction and mean clock over every
-    dispatch of a PMC pass with SQ_CYCLES + SQ_VALU_MFMA_BUSY_CYCLES (see mfma())."""
+    """Per kernel group (as bench.py names them): MFMA-pipe busy fraction over the sequencer-busy cycles and the
+    clock (see mfma()), time-weighted over every dispatch of a PMC pass with SQ_BUSY_CYCLES +
+    SQ_VALU_MFMA_BUSY_CYCLES."""
     per = defaultdict(dict)
     for r in csv.DictReader(open(path)):
         d = per[r["Dispatch_Id"]]
         d["group"] = group(r["Kernel_Name"])
         d[r["Counter_Name"]] = float(r["Counter_Value"])
         d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    acc = defaultdict(lambda: {"launches": 0, "busy": 0.0, "simd_cycles": 0.0, "cycles": 0.0, "ns": 0.0})
+    acc = defaultdict(lambda: {"launches": 0, "busy": 0.0, "sq_busy": 0.0, "ns": 0.0})
     for d in per.values():
-        if "SQ_CYCLES" not in d or "SQ_VALU_MFMA_BUSY_CYCLES" not in d or d["dur_ns"] <= 0:
+        if "SQ_BUSY_CYCLES" not in d or "SQ_VALU_MFMA_BUSY_CYCLES" not in d or d["dur_ns"] <= 0:
             continue
         a = acc[d["group"]]
-        clk = d["SQ_CYCLES"] / 32.0 / d["dur_ns"]
         a["launches"] += 1
         a["busy"] += d["SQ_VALU_MFMA_BUSY_CYCLES"]
-        a["simd_cycles"] += 1024.0 * clk * d["dur_ns"]
-        a["cycles"] += d["SQ_CYCLES"] / 32.0
+        a["sq_busy"] += d["SQ_BUSY_CYCLES"] / 32.0
         a["ns"] += d["dur_ns"]
-    return {k: {"launches": v["launches"], "mfma_busy_frac": v["busy"] / v["simd_cycles"],
-                "clock_ghz": v["cycles"] / v["ns"],
-                "note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x SQ_CYCLES/32 per dispatch), summed over launches"}
-            for k, v in acc.items() if v["simd_cycles"] > 0}
+    return {k: {"launches": v["launches"], "mfma_busy_frac": v["busy"] / (1024.0 * v["sq_busy"]),
+                "clock_ghz": v["sq_busy"] / v["ns"],
+                "note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x SQ_BUSY_CYCLES / 32 SEs), summed over launches"}
+            for k, v in acc.items() if v["sq_busy"] > 0}
 
 
 if __name__ == "__main__":
