@@ -297,7 +297,10 @@ static int forced_variant() {
   return g_forced;
 }
 
-// Stream-K variants (2580 + v) are chosen only when the caller passes a workspace; 0 = none.
+// Stream-K variants (2580 + v) are chosen only when the caller passes a workspace; 0 = none.  None is picked
+// automatically: on the path shapes the data-parallel kernels measured faster (2580/2581), or equal within noise at
+// the bench level (2582, tail-only stream-K: every full wave of 256x128 tiles data-parallel, only the last partial
+// wave split; enc.qkv 108 -> 97 us and aat.fc1 77 -> 75 us in isolation, 266 vs 266 views/s in the bench).
 int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   const int f = forced_variant();
   if (f) return f >= 2580 && f <= 2582 ? f : 0;

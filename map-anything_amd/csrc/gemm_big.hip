@@ -779,6 +779,12 @@ static void sk_shape(int variant, int& bn, int& per_cu) {
   per_cu = variant == 1 ? 1 : 2;
 }
 
+int gemm_streamk_slots(int variant) {
+  int bn, per_cu;
+  sk_shape(variant, bn, per_cu);
+  return sk_cus() * per_cu;
+}
+
 // Ticket words live in a fixed-size head shared by every shape (a shape-dependent split would let one shape's slabs
 // overwrite another's tickets, which must stay zero between calls); shapes with more tiles use the DP schedule.
 constexpr int64_t SK_MAX_TILES = 65536, SK_TICKET_BYTES = SK_MAX_TILES * 4;

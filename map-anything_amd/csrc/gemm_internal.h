@@ -158,6 +158,7 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
 // streamk_workspace_bytes: bytes the launch needs (ticket words + partial-sum slabs); launch returns false if
 // the workspace is missing or too small.
 int64_t streamk_workspace_bytes(int M, int N, int variant);
+int gemm_streamk_slots(int variant);  // persistent workgroups of a stream-K variant on this device
 bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 }  // namespace mapa_gemm_impl

@@ -326,7 +326,9 @@ class MapAnything:
                     eng.run(static_in)
                 torch.cuda.current_stream(imgs.device).wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graph):
+                # captured on the warm-up stream: the per-stream GEMM / attention workspaces made in the warm-up
+                # are the ones the graph uses (no allocation or zero-fill inside the capture)
+                with torch.cuda.graph(graph, stream=side):
                     static_out = eng.run(static_in)
                 entry = (graph, static_in, static_out)
                 self._graphs[key] = entry
