@@ -81,7 +81,7 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
 int mapa_gemm_set_variant(int variant);
 
 /* ---------------------------------------------------------------------------------------------------------
- * Flash attention forward, head_dim 64, non-causal, softmax scale 1/8 (F.scaled_dot_product_attention at
+ * Flash attention forward, head_dim 64, non-causal, softmax scale `scale` (default 1/8; F.scaled_dot_product_attention at
  * dinov2.py:136 and transformer_blocks.py:198-201).  Element (b, h, i, d) of Q lives at
  *   q + b*q_bstride + i*q_rstride + h*64 + d   (same for k, v, o), so the packed qkv GEMM output is read in place.
  * Q rows [0, seq_q) attend to K/V rows [0, seq_kv) of the same batch; o receives the per-head outputs.
@@ -108,6 +108,9 @@ typedef struct {
    * without it one workgroup per block */
   void* workspace;
   int64_t workspace_bytes;
+  /* softmax scale on q.k (0 = 1/sqrt(64), SDPA's default); variants fold their logit scaling into it
+   * (entropy scaling / scalable softmax, transformer_blocks.py:185-196) */
+  float scale;
 } mapa_attn_desc;
 
 int mapa_attention(const mapa_attn_desc* d, mapa_stream_t stream);

@@ -38,6 +38,7 @@ struct AttnArgs {
   float* lse;
   int64_t qb, qr, kb, kr, vb, vr, ob, orr;
   int batch, heads, seq_q, seq_kv;
+  float qscale;  // softmax scale on q.k (natural units; the bf16 kernel multiplies by log2(e) as well)
   int nseg;
   int seg_start[MAPA_MAX_KV_SEGMENTS];
   int seg_len[MAPA_MAX_KV_SEGMENTS];
@@ -201,7 +202,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
         b8 sc;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (0.125f * LOG2E));
+        for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (p.qscale * LOG2E));
         qf[kk] = sc;
       }
     }
@@ -460,7 +461,7 @@ __global__ void __launch_bounds__(NT, 1) attn_fwd_f32(AttnArgs p) {
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     qf[c] = *reinterpret_cast<const f32x4*>(qbase + (int64_t)qrow_c * p.qr + (2 * c + hl) * 4);
-    qf[c] *= 0.125f;
+    qf[c] *= p.qscale;
   }
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const int nkt = (p.seq_kv + KT - 1) / KT;
@@ -677,6 +678,8 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   a.qb = d->q_bstride; a.qr = d->q_rstride; a.kb = d->k_bstride; a.kr = d->k_rstride;
   a.vb = d->v_bstride; a.vr = d->v_rstride; a.ob = d->o_bstride; a.orr = d->o_rstride;
   a.batch = d->batch; a.heads = d->heads; a.seq_q = d->seq_q; a.seq_kv = d->seq_kv;
+  MAPA_CHECK_ARG(d->scale >= 0.f && d->scale < 1e30f, "mapa_attention: bad scale %g", (double)d->scale);
+  a.qscale = d->scale > 0.f ? d->scale : 0.125f;
   MAPA_CHECK_ARG(d->kv_nseg >= 0 && d->kv_nseg <= MAPA_MAX_KV_SEGMENTS, "mapa_attention: kv_nseg out of range");
   a.nseg = d->kv_nseg;
   int64_t tot = 0;

@@ -56,6 +56,7 @@ class AttnDesc(ctypes.Structure):
         ("v_rstride", ctypes.c_int64), ("o_bstride", ctypes.c_int64), ("o_rstride", ctypes.c_int64),
         ("lse", ctypes.c_void_p), ("kv_nseg", ctypes.c_int), ("kv_seg_start", ctypes.c_int * 16),
         ("kv_seg_len", ctypes.c_int * 16), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
+        ("scale", ctypes.c_float),
     ]
 
 
@@ -270,7 +271,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
 
 
 def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, k_bstride, k_rstride,
-              v_bstride, v_rstride, o_bstride, o_rstride, lse=None, kv_segments=None, kind="attention"):
+              v_bstride, v_rstride, o_bstride, o_rstride, lse=None, kv_segments=None, kind="attention", scale=None):
     """q/k/v/o are tensors whose data_ptr is the (b=0, h=0, i=0, d=0) element.  `kind` labels the launch for the
     per-kernel timing (bench.py: "attention_global" = the cross-view AAT layers)."""
     d = AttnDesc()
@@ -282,6 +283,7 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
     d.v_bstride, d.v_rstride = v_bstride, v_rstride
     d.o_bstride, d.o_rstride = o_bstride, o_rstride
     d.lse = None if lse is None else lse.data_ptr()
+    d.scale = 0.0 if scale is None else float(scale)  # 0 -> 1/sqrt(64)
     if d.dtype == BF16:
         ws = attention_workspace(d)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()

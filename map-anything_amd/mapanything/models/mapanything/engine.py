@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import _native as nat
+from .spec import RELEASED_INFO, InfoSharingSpec
 
 ENC_DIM, ENC_HEADS, PATCH, KPAD = 1024, 16, 14, 640
 AAT_DIM, AAT_HEADS = 768, 12
@@ -67,7 +68,7 @@ class GeoInputs:
 class PackedWeights:
     """Canonical state dict -> device buffers in kernel layout (done once at load)."""
 
-    def __init__(self, sd: Dict[str, object], device, lp_dtype: torch.dtype):
+    def __init__(self, sd: Dict[str, object], device, lp_dtype: torch.dtype, info: InfoSharingSpec = RELEASED_INFO):
         self.device = device
         self.lp = lp_dtype
         self.sd = sd
@@ -117,9 +118,11 @@ class PackedWeights:
         # AAT
         self.pe_proj = lin("info_sharing.proj_embed")
         self.pe_proj_b = f32("info_sharing.proj_embed.bias")
-        self.view_pe = f32("info_sharing.view_pos_table").reshape(-1)[:AAT_DIM].contiguous()
+        # sinusoid view PE table (pe_rows x 768): row 0 = the reference view's, rows 1.. the other views'
+        self.view_pos = f32("info_sharing.view_pos_table").reshape(-1, AAT_DIM) if info.ref_pe else None
+        self.view_pe = self.view_pos[0].contiguous() if info.ref_pe else None
         self.aat = []
-        for b in range(24):
+        for b in range(info.depth):
             p = f"info_sharing.self_attention_blocks.{b}"
             self.aat.append(dict(
                 n1w=f32(f"{p}.norm1.weight"), n1b=f32(f"{p}.norm1.bias"),
@@ -228,7 +231,8 @@ class PackedWeights:
 
 
 class MapaEngine:
-    def __init__(self, sd: Dict[str, object], device=None, precision: str = "bf16"):
+    def __init__(self, sd: Dict[str, object], device=None, precision: str = "bf16",
+                 info: InfoSharingSpec = RELEASED_INFO):
         if precision not in ("bf16", "fp32"):
             raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision}")
         nat.lib()  # fail loudly without the HIP library / a gfx950 device
@@ -236,8 +240,9 @@ class MapaEngine:
         self.precision = precision
         self.lp = torch.bfloat16 if precision == "bf16" else torch.float32
         self._sd = sd  # host state dict: the geometric encoders are packed on first use
+        self.info = info
         with torch.cuda.device(self.device):
-            self.w = PackedWeights(sd, self.device, self.lp)
+            self.w = PackedWeights(sd, self.device, self.lp, info)
 
     # ---------------------------------------------------------------------------------------- profiling
     def enable_kernel_timing(self):
@@ -261,14 +266,15 @@ class MapaEngine:
 
     # ------------------------------------------------------------------------------------ transformer block
     def _block(self, x, xn, qkv, ao, hbuf, rows, dim, heads, p, *, attn_batch, attn_seq, gamma=True,
-               attn_kind="attention"):
+               attn_kind="attention", attn_scale=None):
         lp = self.lp
         self._ln(x, rows, dim, p["n1w"], p["n1b"], y_lp=xn)
         nat.gemm(xn, p["qkv"], rows, 3 * dim, dim, bias=p["qkv_b"], out_lp=qkv)
         rs = 3 * dim
         nat.attention(qkv, qkv[:, dim:], qkv[:, 2 * dim:], ao, batch=attn_batch, heads=heads, seq_q=attn_seq,
                       seq_kv=attn_seq, q_bstride=attn_seq * rs, q_rstride=rs, k_bstride=attn_seq * rs, k_rstride=rs,
-                      v_bstride=attn_seq * rs, v_rstride=rs, o_bstride=attn_seq * dim, o_rstride=dim, kind=attn_kind)
+                      v_bstride=attn_seq * rs, v_rstride=rs, o_bstride=attn_seq * dim, o_rstride=dim, kind=attn_kind,
+                      scale=attn_scale)
         nat.gemm(ao, p["proj"], rows, dim, dim, bias=p["proj_b"], gamma=p.get("ls1") if gamma else None,
                  resid1=x, out_f32=x)
         self._ln(x, rows, dim, p["n2w"], p["n2b"], y_lp=xn)
@@ -434,33 +440,44 @@ class MapaEngine:
         return y
 
     # ----------------------------------------------------------------------------------------------- AAT
-    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None):
-        """alternating_attention_transformer.py:530-771 (IFR [11, 17]).  Returns l11, l17, final (lp, VB*T rows)
-        and the final scale-token feature (f32, 768).  With `shard` (parallel.ShardPlan) this rank holds only its
-        views (+ the scale-token replica) and the global layers all-gather K/V through `comm`."""
-        w = self.w
+    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None, pe_idx=None):
+        """The multi-view transformer with intermediate-feature return: AAT (alternating_attention_transformer.py:
+        530-771; released config: 24 blocks, taps after 11 and 17) or GAT (global_attention_transformer.py:458-640:
+        every block global), per self.info.  Returns the two taps and the final features (lp, VB*T rows) and the final
+        scale-token feature (f32, 768).  pe_idx: (V_total,) int64 device tensor of view-PE table rows (row 0 for the
+        reference view) when the variant encodes non-reference views too.  With `shard` (parallel.ShardPlan) this
+        rank holds only its views (+ the scale-token replica) and the global layers all-gather K/V through `comm`."""
+        w, info = self.w, self.info
         L = VB * T + 1
         y = self._empty(L, AAT_DIM, dtype=torch.float32)
         nat.gemm(fused_lp, w.pe_proj, L, AAT_DIM, ENC_DIM, bias=w.pe_proj_b, out_f32=y)
-        if shard is None or shard.rank == 0:  # reference-view PE on view 0 only
+        first = 0 if shard is None else shard.starts[shard.rank]  # global index of this rank's first view
+        if info.nonref_pe:  # view PE on every view: table rows pe_idx (row 0 on the reference view)
+            vecs = w.view_pos.index_select(0, pe_idx[first:first + VB]).contiguous()
+            nat.add_view_vectors(y, T, AAT_DIM, VB, vecs, self._ones(VB), 1)
+        elif info.ref_pe and first == 0:  # reference-view PE on view 0 only
             nat.add_rowvec(y, AAT_DIM, 0, T, AAT_DIM, w.view_pe)
         yn, qkv, ao = self._empty(L, AAT_DIM), self._empty(L, 3 * AAT_DIM), self._empty(L, AAT_DIM)
         hbuf = self._empty(L, 4 * AAT_DIM)
+        L_all = L if shard is None else shard.total_kv  # tokens of a global block (every view + the scale token)
+        g_scale = 0.125 * info.q_scale(L_all) if (info.scalable_softmax or info.entropy_scaling) else None
+        f_scale = 0.125 * info.q_scale(T) if (info.scalable_softmax or info.entropy_scaling) else None
         if shard is not None:
             kv_full = self._empty(shard.world * shard.max_rows, 2 * AAT_DIM)
             q_loc = self._empty(L, AAT_DIM)
         inter = {}
+        i0, i1 = info.indices
         for d, p in enumerate(w.aat):
-            if d % 2 == 0:   # global attention over every view + the scale token
+            if info.is_global(d):   # global attention over every view + the scale token
                 if shard is None:
                     self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False,
-                                attn_kind="attention_global")
+                                attn_kind="attention_global", attn_scale=g_scale)
                 else:
-                    self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm)
-            else:            # frame attention inside each view; the scale token bypasses the block
+                    self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, g_scale)
+            else:                   # frame attention inside each view; the scale token bypasses the block
                 self._block(y, yn, qkv, ao, hbuf, VB * T, AAT_DIM, AAT_HEADS, p, attn_batch=VB, attn_seq=T,
-                            gamma=False)
-            if d in (11, 17):
+                            gamma=False, attn_scale=f_scale)
+            if d in (i0, i1):
                 t_lp = self._empty(VB * T, AAT_DIM)
                 t_f = self._empty(VB * T, AAT_DIM, dtype=torch.float32) if taps is not None else None
                 self._ln(y, VB * T, AAT_DIM, w.aat_nw, w.aat_nb, y_lp=t_lp, y_f32=t_f)
@@ -477,9 +494,15 @@ class MapaEngine:
         if taps is not None:
             taps["aat_final"] = fin_f32[:VB * T]
             taps["scale_token"] = fin_f32[VB * T]
-        return inter[11], inter[17], fin_lp, fin_f32[VB * T:]
+        return inter[i0], inter[i1], fin_lp, fin_f32[VB * T:]
 
-    def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm):
+    def _ones(self, n):
+        o = getattr(self, "_ones_buf", None)
+        if o is None or o.numel() < n:
+            o = self._ones_buf = torch.ones(max(n, 64), dtype=torch.float32, device=self.device)
+        return o
+
+    def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, scale=None):
         """Global SelfAttentionBlock on a view shard: Q for the local rows, K/V of all ranks (one all-gather).
         The all-gather runs on the communicator's stream while the local queries attend to this rank's own keys;
         the remote-key partial follows the gather and the two partials are merged through their LSEs
@@ -490,7 +513,7 @@ class MapaEngine:
         slot = kv_full[shard.rank * shard.max_rows:]
         nat.gemm(yn, p["qkv"][C:], L, 2 * C, C, bias=p["qkv_b"][C:], out_lp=slot, ldo=2 * C)
         strides = dict(batch=1, heads=AAT_HEADS, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
-                       v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C)
+                       v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C, scale=scale)
         overlap = hasattr(comm, "allgather_slots_async") and os.environ.get("MAPA_KV_OVERLAP", "1") != "0"
         if not overlap:
             comm.allgather_slots(kv_full, shard.max_rows)
@@ -680,7 +703,8 @@ class MapaEngine:
     # ----------------------------------------------------------------------------------------------- run
     @torch.no_grad()
     def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None,
-            geo: Optional[GeoInputs] = None, dpt_chunk: Optional[int] = None) -> Dict[str, torch.Tensor]:
+            geo: Optional[GeoInputs] = None, dpt_chunk: Optional[int] = None,
+            pe_idx: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
         """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
         per-pixel / per-view outputs of MapAnything.forward, view-major.  With `shard`/`comm`, imgs are this
         rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'.  `geo` carries the
@@ -697,7 +721,9 @@ class MapaEngine:
             T = hp * wp
             if shard is not None and (shard.counts[shard.rank] != VB or shard.tokens_per_view != T):
                 raise AssertionError("shard plan does not match the local views")
-            l11, l17, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm)
+            if self.info.nonref_pe and pe_idx is None:
+                raise ValueError("this info-sharing variant encodes every view's index: pass pe_idx")
+            l11, l17, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx)
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)

@@ -27,11 +27,11 @@ import torch
 from ... import _native as nat
 from ...utils.inference import (postprocess_outputs, preprocess_input_views_for_inference,
                                 validate_input_views_for_inference)
-from .spec import aliases, canonical_spec
+from .spec import InfoSharingSpec, aliases, canonical_spec
 
 SUPPORTED = dict(
-    encoder="dinov2", size="large", info_sharing="alternating_attention", return_type="intermediate_features",
-    pred_head="dpt+pose", adaptor="raydirs+depth+pose+confidence+mask",
+    encoder="dinov2", size="large", info_sharing=("alternating_attention", "global_attention"),
+    return_type="intermediate_features", pred_head="dpt+pose", adaptor="raydirs+depth+pose+confidence+mask",
 )
 
 
@@ -41,13 +41,23 @@ def _check_config(encoder_config, info_sharing_config, pred_head_config):
         problems.append(f"encoder {encoder_config.get('encoder_str')}/{encoder_config.get('size')}")
     if encoder_config.get("with_registers", False):
         problems.append("dinov2 with registers")
-    if info_sharing_config.get("model_type") != SUPPORTED["info_sharing"]:
+    if info_sharing_config.get("model_type") not in SUPPORTED["info_sharing"]:
         problems.append(f"info_sharing {info_sharing_config.get('model_type')}")
     if info_sharing_config.get("model_return_type") != SUPPORTED["return_type"]:
         problems.append(f"return type {info_sharing_config.get('model_return_type')}")
     args = info_sharing_config.get("module_args", {})
-    if list(args.get("indices", [11, 17])) != [11, 17] or args.get("depth", 24) != 24:
-        problems.append("AAT depth/indices")
+    depth = int(args.get("depth", 12))
+    idx = list(args.get("indices", []))
+    if len(idx) != 2 or not all(0 <= int(i) < depth for i in idx) or int(idx[0]) >= int(idx[1]):
+        # 3 indices (model.py:322-330: DPT on info-sharing taps only) is not part of this engine
+        problems.append(f"info-sharing intermediate indices {idx} (two increasing block indices < depth)")
+    if (info_sharing_config.get("custom_positional_encoding") is not None
+            or args.get("custom_positional_encoding") is not None):
+        # RoPE-2D: with MapAnything's scale token the reference adds a list of None positions to the position
+        # tensor (alternating_attention_transformer.py:294, global_attention_transformer.py:541) and fails
+        problems.append("custom positional encoding (RoPE)")
+    if args.get("qk_norm", False):
+        problems.append("qk_norm")
     if pred_head_config.get("type") != SUPPORTED["pred_head"]:
         problems.append(f"pred head {pred_head_config.get('type')}")
     if pred_head_config.get("adaptor_type") != SUPPORTED["adaptor"]:
@@ -65,6 +75,7 @@ class MapAnything:
                  load_specific_pretrained_submodules: bool = False, specific_pretrained_submodules: list = None,
                  torch_hub_force_reload: bool = False, precision: str = "bf16", hip_graphs: bool = True):
         _check_config(encoder_config, info_sharing_config, pred_head_config)
+        self.info = InfoSharingSpec.from_config(info_sharing_config)
         self.name = name
         self.encoder_config = encoder_config
         self.info_sharing_config = info_sharing_config
@@ -124,8 +135,8 @@ class MapAnything:
         self.load_state_dict(ckpt["model"] if "model" in ckpt else ckpt)
 
     def load_state_dict(self, state_dict: Dict[str, Any], strict: bool = True):
-        canon = dict(canonical_spec())
-        al = aliases()
+        canon = dict(canonical_spec(self.info))
+        al = aliases(self.info)
         sd: Dict[str, np.ndarray] = {}
         for k, v in state_dict.items():
             arr = v.detach().float().cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v, np.float32)
@@ -150,7 +161,7 @@ class MapAnything:
         """Named-PRNG synthetic checkpoint (mapanything/utils/synthetic.py) — bench/tests only."""
         from ...utils.synthetic import synthetic_state_dict
 
-        self._sd = synthetic_state_dict(canonical_spec())
+        self._sd = synthetic_state_dict(canonical_spec(self.info))
         self._engines.clear()
         self._graphs.clear()
         self._modules.clear()
@@ -225,7 +236,7 @@ class MapAnything:
         key = (str(self._device), prec)
         if key not in self._engines:
             from .engine import MapaEngine
-            self._engines[key] = MapaEngine(self._sd, self._device, prec)
+            self._engines[key] = MapaEngine(self._sd, self._device, prec, self.info)
         return self._engines[key]
 
     def enable_view_sharding(self, group=None, comm=None):
@@ -307,37 +318,56 @@ class MapAnything:
 
     _MAX_GRAPHS = 4
 
+    def _view_pe_rows(self, num_views: int) -> Optional[torch.Tensor]:
+        """View-PE table rows of this forward (None when only the reference view is encoded): 0 for the reference
+        view, then torch.randint(1, rows, (V-1,)) from the global CPU generator, the same draw the reference makes
+        per forward (alternating_attention_transformer.py:608-611, global_attention_transformer.py:551-554), or
+        1..V-1 without random indices."""
+        if not self.info.nonref_pe:
+            return None
+        if self.info.rand_idx:
+            rest = torch.randint(low=1, high=self.info.pe_rows, size=(num_views - 1,))
+        else:
+            if num_views > self.info.pe_rows:
+                raise ValueError(f"{num_views} views exceed the {self.info.pe_rows}-row view positional table")
+            rest = torch.arange(1, num_views)
+        return torch.cat([torch.zeros(1, dtype=torch.int64), rest.to(torch.int64)]).to(self._device)
+
     def _run_engine(self, eng, imgs, plan, geo, dpt_chunk):
         """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: one device, no
         geometric inputs, no chunked dense head, no per-launch kernel timing.  The graph is keyed on the image
         batch shape and precision; inputs are copied into its static buffer and outputs cloned out of it, so
         results never alias a later call's."""
+        pe_idx = self._view_pe_rows(plan.num_views if plan is not None else imgs.shape[0])
         if (not self.hip_graphs or plan is not None or geo is not None or dpt_chunk is not None
                 or nat._timing is not None or imgs.device.type != "cuda"):
-            return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk)
+            return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx)
         key = (eng.precision, tuple(imgs.shape), imgs.device.index)
         with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
             entry = self._graphs.get(key)
             if entry is None:
                 static_in = imgs.clone()
+                static_pe = None if pe_idx is None else pe_idx.clone()  # refreshed before every replay
                 side = torch.cuda.Stream(imgs.device)
                 side.wait_stream(torch.cuda.current_stream(imgs.device))
                 with torch.cuda.stream(side):  # eager warm-up: lazy packing, pos-embed caches
-                    eng.run(static_in)
+                    eng.run(static_in, pe_idx=static_pe)
                 torch.cuda.current_stream(imgs.device).wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
                 # captured on the warm-up stream: the per-stream GEMM / attention workspaces made in the warm-up
                 # are the ones the graph uses (no allocation or zero-fill inside the capture)
                 with torch.cuda.graph(graph, stream=side):
-                    static_out = eng.run(static_in)
-                entry = (graph, static_in, static_out)
+                    static_out = eng.run(static_in, pe_idx=static_pe)
+                entry = (graph, static_in, static_out, static_pe)
                 self._graphs[key] = entry
                 while len(self._graphs) > self._MAX_GRAPHS:
                     self._graphs.popitem(last=False)
             else:
                 self._graphs.move_to_end(key)
-            graph, static_in, static_out = entry
+            graph, static_in, static_out, static_pe = entry
             static_in.copy_(imgs)
+            if static_pe is not None:
+                static_pe.copy_(pe_idx)
             graph.replay()
         return {k: v.clone() for k, v in static_out.items()}
 

@@ -77,10 +77,15 @@ class DINOv2Encoder(_EngineModule):
 
 
 class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
-    """uniception/models/info_sharing/alternating_attention_transformer.py:530-771 (depth 24, dim 768, IFR
-    indices [11, 17], intermediates normed).  Exactly one additional input token (MapAnything's scale token)."""
+    """uniception/models/info_sharing/alternating_attention_transformer.py:530-771 (released config: depth 24,
+    dim 768, IFR indices [11, 17], intermediates normed) — or, for a global_attention config, the GAT of
+    global_attention_transformer.py:458-640 (the engine follows model.info).  Exactly one additional input token
+    (MapAnything's scale token)."""
     dim = AAT_DIM
-    indices = (11, 17)
+
+    @property
+    def indices(self):
+        return self._model.info.indices
 
     @torch.no_grad()
     def forward(self, model_input):
@@ -95,6 +100,7 @@ class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
             raise AssertionError("every view's features must be (B, 1024, h, w)")
         T = h * w
         eng = self._eng()
+        i0, i1 = self._model.info.indices
         final, l11, l17 = ([None] * B for _ in range(3))
         final_tok, tok11, tok17 = [None] * B, [None] * B, [None] * B
         with torch.cuda.device(eng.device):
@@ -103,11 +109,12 @@ class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
                 fused[:V * T] = _rows(torch.stack([self._dev(f[b]) for f in feats], 0), eng.lp)
                 fused[V * T] = self._dev(tok[b, :, 0], eng.lp)
                 taps = {}
-                eng.aat(fused, V, T, taps)
+                eng.aat(fused, V, T, taps, pe_idx=self._model._view_pe_rows(V))
                 final[b] = taps["aat_final"].reshape(V, h, w, AAT_DIM)
-                l11[b] = taps["aat_l11"].reshape(V, h, w, AAT_DIM)
-                l17[b] = taps["aat_l17"].reshape(V, h, w, AAT_DIM)
-                final_tok[b], tok11[b], tok17[b] = taps["scale_token"], taps["aat_l11_token"], taps["aat_l17_token"]
+                l11[b] = taps[f"aat_l{i0}"].reshape(V, h, w, AAT_DIM)
+                l17[b] = taps[f"aat_l{i1}"].reshape(V, h, w, AAT_DIM)
+                final_tok[b], tok11[b], tok17[b] = (taps["scale_token"], taps[f"aat_l{i0}_token"],
+                                                    taps[f"aat_l{i1}_token"])
 
         def pack(per_b, toks):
             views = [torch.stack([per_b[b][v] for b in range(B)], 0).permute(0, 3, 1, 2).contiguous()
@@ -117,6 +124,9 @@ class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
                                                   [t.reshape(AAT_DIM, 1) for t in toks], 0))
 
         return pack(final, final_tok), [pack(l11, tok11), pack(l17, tok17)]
+
+
+MultiViewGlobalAttentionTransformerIFR = MultiViewAlternatingAttentionTransformerIFR  # same engine entry
 
 
 class DPTFeature(_EngineModule):

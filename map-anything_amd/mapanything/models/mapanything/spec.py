@@ -11,7 +11,9 @@ canonical tensor (`dense_head.0/1.*`, `scratch.layer_rn.N`, `input_process.N.1`)
 reference can be read either way.
 """
 
-from typing import Dict, List, Tuple
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
 
 Spec = List[Tuple[str, Tuple[int, ...]]]
 
@@ -25,6 +27,70 @@ AAT_MLP = 3072
 DPT_LAYER_DIMS = (96, 192, 384, 768)
 DPT_FEAT = 256
 POSE_DIM = 4 * PATCH * PATCH  # 784
+
+
+@dataclass(frozen=True)
+class InfoSharingSpec:
+    """The multi-view transformer variant of an info_sharing_config (model.py:240-330 picks the class):
+
+    * kind "alternating" = MultiViewAlternatingAttentionTransformerIFR (alternating_attention_transformer.py:386-771:
+      even blocks attend over every view + the additional tokens, odd blocks inside each view without them);
+      "global" = MultiViewGlobalAttentionTransformerIFR (global_attention_transformer.py:347-640: every block global).
+    * view positional encoding from the sinusoid `view_pos_table` (pe_rows rows): row 0 on the reference view when
+      ref_pe; rows 1.. (sequential, or torch.randint(1, pe_rows) per forward when rand_idx) on the other views when
+      nonref_pe.  AAT: ref_pe = distinguish_ref_and_non_ref_views, nonref_pe = that and use_pe_for_non_reference_views,
+      table rows max_num_views_for_pe if nonref_pe else 1 (alternating_attention_transformer.py:159-172, 594-620);
+      GAT: both always, max_num_views rows (global_attention_transformer.py:160-167, 543-563).
+    * attention logit scaling (transformer_blocks.py:185-196), applied to q per block with N = that block's tokens:
+      scalable softmax x ln N; entropy scaling x sqrt(growth * ln N / ln base).
+    """
+    kind: str = "alternating"
+    depth: int = 24
+    indices: Tuple[int, int] = (11, 17)
+    ref_pe: bool = True
+    nonref_pe: bool = False
+    rand_idx: bool = True
+    pe_rows: int = 1
+    scalable_softmax: bool = False
+    entropy_scaling: bool = False
+    entropy_base: int = 444
+    entropy_growth: float = 1.4
+
+    @staticmethod
+    def from_config(info_sharing_config: Optional[Dict]) -> "InfoSharingSpec":
+        if not info_sharing_config:
+            return InfoSharingSpec()
+        a = info_sharing_config.get("module_args", {})
+        kind = "global" if info_sharing_config.get("model_type") == "global_attention" else "alternating"
+        common = dict(depth=int(a.get("depth", 12)), indices=tuple(int(i) for i in a.get("indices", (11, 17))),
+                      scalable_softmax=bool(a.get("use_scalable_softmax", False)),
+                      entropy_scaling=bool(a.get("use_entropy_scaling", False)),
+                      entropy_base=int(a.get("base_token_count_for_entropy_scaling", 444)),
+                      entropy_growth=float(a.get("entropy_scaling_growth_factor", 1.4)))
+        if kind == "global":
+            return InfoSharingSpec(kind=kind, ref_pe=True, nonref_pe=True,
+                                   rand_idx=bool(a["use_rand_idx_pe_for_non_reference_views"]),
+                                   pe_rows=int(a["max_num_views"]), **common)
+        ref = bool(a.get("distinguish_ref_and_non_ref_views", True))
+        nonref = ref and bool(a.get("use_pe_for_non_reference_views", False))
+        return InfoSharingSpec(kind=kind, ref_pe=ref, nonref_pe=nonref,
+                               rand_idx=bool(a.get("use_rand_idx_pe_for_non_reference_views", True)),
+                               pe_rows=int(a.get("max_num_views_for_pe", 1000)) if nonref else 1, **common)
+
+    def is_global(self, d: int) -> bool:
+        return self.kind == "global" or d % 2 == 0
+
+    def q_scale(self, n_tokens: int) -> float:
+        """Multiplier on q (on top of SDPA's head_dim^-0.5) for a block over n_tokens tokens."""
+        f = 1.0
+        if self.scalable_softmax:
+            f *= math.log(n_tokens)
+        if self.entropy_scaling:
+            f *= math.sqrt(self.entropy_growth * math.log(n_tokens) / math.log(self.entropy_base))
+        return f
+
+
+RELEASED_INFO = InfoSharingSpec()
 
 
 def _linear(spec: Spec, name: str, out_f: int, in_f: int, bias: bool = True):
@@ -68,7 +134,7 @@ def _rcu(spec: Spec, name: str):
     _conv(spec, f"{name}.conv2", DPT_FEAT, DPT_FEAT, 3)
 
 
-def canonical_spec() -> Spec:
+def canonical_spec(info: InfoSharingSpec = RELEASED_INFO) -> Spec:
     s: Spec = []
     s.append(("scale_token", (ENC_DIM,)))
     # DINOv2 ViT-L/14
@@ -95,9 +161,10 @@ def canonical_spec() -> Spec:
     _global_rep_encoder(s, "cam_trans_scale_encoder", 1)
     _ln(s, "fusion_norm_layer", ENC_DIM)
     # AAT
-    s.append(("info_sharing.view_pos_table", (1, AAT_DIM)))
+    if info.ref_pe:
+        s.append(("info_sharing.view_pos_table", (info.pe_rows, AAT_DIM)))
     _linear(s, "info_sharing.proj_embed", AAT_DIM, ENC_DIM)
-    for b in range(AAT_DEPTH):
+    for b in range(info.depth):
         p = f"info_sharing.self_attention_blocks.{b}"
         _ln(s, f"{p}.norm1", AAT_DIM)
         _linear(s, f"{p}.attn.qkv", 3 * AAT_DIM, AAT_DIM)
@@ -146,7 +213,7 @@ def canonical_spec() -> Spec:
     return s
 
 
-def aliases() -> Dict[str, str]:
+def aliases(info: InfoSharingSpec = RELEASED_INFO) -> Dict[str, str]:
     """alias key -> canonical key (tensors that share storage in the reference's state dict)."""
     out: Dict[str, str] = {}
     h = "dpt_feature_head"
@@ -157,7 +224,7 @@ def aliases() -> Dict[str, str]:
     for a, c in feat_alias.items():
         out[f"{h}.{a}"] = f"{h}.{c}"
         out[f"dense_head.0.{a}"] = f"{h}.{c}"
-    for n, _ in canonical_spec():
+    for n, _ in canonical_spec(info):
         if n.startswith(h + "."):
             out["dense_head.0." + n[len(h) + 1:]] = n
         elif n.startswith("dpt_regressor_head."):
@@ -165,8 +232,8 @@ def aliases() -> Dict[str, str]:
     return out
 
 
-def full_spec() -> Spec:
+def full_spec(info: InfoSharingSpec = RELEASED_INFO) -> Spec:
     """Every key of the reference's state_dict (canonical + aliases)."""
-    canon = canonical_spec()
+    canon = canonical_spec(info)
     shapes = dict(canon)
-    return canon + [(a, shapes[c]) for a, c in aliases().items()]
+    return canon + [(a, shapes[c]) for a, c in aliases(info).items()]

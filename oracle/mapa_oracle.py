@@ -50,9 +50,12 @@ def _t(x):
 class MapAnythingOracle:
     """fp32 CPU restatement. `sd` = canonical state dict (names of spec.canonical_spec())."""
 
-    def __init__(self, sd: Dict[str, object]):
+    def __init__(self, sd: Dict[str, object], info=None):
+        """info: the multi-view transformer variant (mapanything.models.mapanything.spec.InfoSharingSpec or any
+        object with its fields); None = the released AAT (24 blocks, taps 11/17, reference-view PE only)."""
         self.sd = {k: _t(v).float() for k, v in sd.items()}
         self.taps: Dict[str, torch.Tensor] = {}
+        self.info = info
 
     def p(self, name):
         return self.sd[name]
@@ -67,11 +70,14 @@ class MapAnythingOracle:
     def conv(self, x, name, stride=1, padding=0):
         return F.conv2d(x, self.p(f"{name}.weight"), self.sd.get(f"{name}.bias"), stride=stride, padding=padding)
 
-    def attention(self, x, name, heads):
-        """transformer_blocks.py:163-212 / dinov2.py:125-141: qkv -> SDPA (scale hd^-0.5) -> proj."""
+    def attention(self, x, name, heads, qmul=None):
+        """transformer_blocks.py:163-212 / dinov2.py:125-141: qkv -> [q * qmul(N), the logit scaling of :185-196]
+        -> SDPA (scale hd^-0.5) -> proj."""
         B, N, C = x.shape
         qkv = self.lin(x, f"{name}.qkv").reshape(B, N, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
+        if qmul is not None:
+            q = q * qmul(N)
         o = F.scaled_dot_product_attention(q, k, v)
         o = o.transpose(1, 2).reshape(B, N, C)
         return self.lin(o, f"{name}.proj")
@@ -85,9 +91,9 @@ class MapAnythingOracle:
         x = x + self.p(f"{name}.ls2.gamma") * self.mlp(self.ln(x, f"{name}.norm2"), f"{name}.mlp")
         return x
 
-    def aat_block(self, x, name):
+    def aat_block(self, x, name, qmul=None):
         """transformer_blocks.py:452-469 (init_values=None -> no LayerScale, eval -> no drop path)."""
-        x = x + self.attention(self.ln(x, f"{name}.norm1"), f"{name}.attn", AAT_HEADS)
+        x = x + self.attention(self.ln(x, f"{name}.norm1"), f"{name}.attn", AAT_HEADS, qmul)
         x = x + self.mlp(self.ln(x, f"{name}.norm2"), f"{name}.mlp")
         return x
 
@@ -221,27 +227,54 @@ class MapAnythingOracle:
         return out
 
     # ------------------------------------------------------------------------------------------------- AAT
-    def aat(self, feats: List[torch.Tensor], scale_token: torch.Tensor):
-        """alternating_attention_transformer.py:530-771 (IFR, indices [11, 17], norm_intermediate)."""
+    def aat(self, feats: List[torch.Tensor], scale_token: torch.Tensor, pe_rows=None):
+        """The multi-view transformer with intermediate returns: AAT (alternating_attention_transformer.py:530-771)
+        or GAT (global_attention_transformer.py:458-640) per self.info.  View PE (AAT :594-620, GAT :543-563):
+        table row 0 on the reference view; rows pe_rows[1:] (default 1..V-1) on the others when the variant encodes
+        them.  Logit scaling per block with its own token count N (transformer_blocks.py:185-196)."""
+        info = self.info
+        kind = getattr(info, "kind", "alternating")
+        depth = getattr(info, "depth", 24)
+        i0, i1 = getattr(info, "indices", (11, 17))
+        ref_pe, nonref_pe = getattr(info, "ref_pe", True), getattr(info, "nonref_pe", False)
+        qmul = None
+        if info is not None and (info.scalable_softmax or info.entropy_scaling):
+            def qmul(n):
+                f = 1.0
+                if info.scalable_softmax:
+                    f *= math.log(n)
+                if info.entropy_scaling:
+                    f *= math.sqrt(info.entropy_growth * math.log(n) / math.log(info.entropy_base))
+                return f
         V = len(feats)
         B, C, h, w = feats[0].shape
         T = h * w
         x = torch.stack(feats, 1).permute(0, 1, 3, 4, 2).reshape(B, V * T, C)
         x = torch.cat([x, scale_token.permute(0, 2, 1)], 1)
         x = self.lin(x, "info_sharing.proj_embed")
-        pe = self.p("info_sharing.view_pos_table")[0].reshape(1, 1, AAT_DIM)
-        x = torch.cat([x[:, :T] + pe, x[:, T:V * T], x[:, V * T:]], 1)
+        if ref_pe:
+            table = self.p("info_sharing.view_pos_table")
+            rows = list(pe_rows) if pe_rows is not None else list(range(V))
+            parts = []
+            for v in range(V):
+                xv = x[:, v * T:(v + 1) * T]
+                if v == 0:
+                    xv = xv + table[0].reshape(1, 1, AAT_DIM)
+                elif nonref_pe:
+                    xv = xv + table[rows[v]].reshape(1, 1, AAT_DIM)
+                parts.append(xv)
+            x = torch.cat(parts + [x[:, V * T:]], 1)
         inter = []
-        for d in range(24):
+        for d in range(depth):
             name = f"info_sharing.self_attention_blocks.{d}"
-            if d % 2 == 0:
-                x = self.aat_block(x, name)
+            if kind == "global" or d % 2 == 0:
+                x = self.aat_block(x, name, qmul)
             else:
                 extra = x[:, V * T:]
                 xv = x[:, :V * T].reshape(B * V, T, AAT_DIM)
-                xv = self.aat_block(xv, name).reshape(B, V * T, AAT_DIM)
+                xv = self.aat_block(xv, name, qmul).reshape(B, V * T, AAT_DIM)
                 x = torch.cat([xv, extra], 1)
-            if d in (11, 17):
+            if d in (i0, i1):
                 inter.append(self.ln(x, "info_sharing.norm"))
         out = self.ln(x, "info_sharing.norm")
 

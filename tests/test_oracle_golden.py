@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from conftest import GOLDEN, rel_l2
-from tests_helpers import CASES, make_views
+from tests_helpers import CASES, VARIANT_CASES, make_views, variant_config
 
 TOL = 2e-5
 
@@ -27,12 +27,26 @@ def _steps(name):
     return meta[name]["steps_out_tap_dpt"]
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "mixed_224", "ns_280x392", "one_224", "v2_518"])
+def _oracle_for(name, oracle):
+    if name not in VARIANT_CASES:
+        return oracle, CASES[name]
+    from mapanything.models.mapanything.spec import InfoSharingSpec, canonical_spec
+    from mapanything.utils.synthetic import synthetic_state_dict
+    from oracle.mapa_oracle import MapAnythingOracle
+
+    cfg, case = variant_config(name)
+    info = InfoSharingSpec.from_config(cfg["info_sharing_config"])
+    return MapAnythingOracle(synthetic_state_dict(canonical_spec(info)), info), case
+
+
+@pytest.mark.parametrize("name", ["cfg1_224", "mm_224", "mixed_224", "ns_280x392", "one_224", "v2_518",
+                                  *VARIANT_CASES])
 def test_oracle_matches_reference(oracle, golden, name):
     g = golden(name)
     out_step, tap_step, dpt_step = _steps(name)
+    oracle, case = _oracle_for(name, oracle)
     with torch.no_grad():
-        preds = oracle.infer(make_views(CASES[name]))
+        preds = oracle.infer(make_views(case))
     taps = oracle.taps
     checked = 0
     for key, ref in g.items():

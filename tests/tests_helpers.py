@@ -23,6 +23,20 @@ CASES = {
 }
 
 
+# Info-sharing variants (make_golden.py VARIANTS): the reference rebuilt with these info_sharing_configs
+VARIANT_CASES = ("gat_224", "aatpe_224", "aatnoref_224")
+
+
+def variant_config(name):
+    """(full model config, case) of a variant fixture: the released config with the info_sharing_config the
+    reference was built with (recorded in golden_meta.json)."""
+    meta = json.load(open(os.path.join(HERE, "golden", "golden_meta.json")))[name]
+    cfg = released_config()
+    cfg["info_sharing_config"] = meta["info_sharing_config"]
+    case = {k: meta[k] for k in ("views", "h", "w", "seed")}
+    return cfg, case
+
+
 def make_views(case):
     """Seeded reference-format views: images (+ intrinsics / sparse depth_z / 4x4 poses / is_metric_scale)."""
     import torch
