@@ -106,3 +106,48 @@ def test_sharded_geometric_inputs_equal_single(precision, tol):
             for k in ("pts3d", "conf", "cam_quats", "cam_trans", "metric_scaling_factor"):
                 e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
                 assert e < tol, (r, v, k, e)
+
+
+@pytest.mark.parametrize("variant", ["gat_224", "aatpe_224"])
+def test_sharded_variants_equal_single(variant):
+    """Info-sharing variants on the sharded path: GAT (every block global, view PE on every view: each rank adds
+    the rows of its own views) and AAT with non-reference PE + scalable softmax (scale from the global token count
+    on every rank), fp32, 2 ranks over 3 views."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ThreadComm
+    from tests_helpers import variant_config
+
+    cfg, _ = variant_config(variant)
+    world, V = 2, 3
+    views = _views(V, 224, 224, seed=12)
+    ref_model = MapAnything(**cfg, precision="fp32").load_synthetic_weights().to("cuda")
+    ref = ref_model.forward(views)
+    comm = ThreadComm(world)
+    model = MapAnything(**cfg, precision="fp32").to("cuda")
+    model._sd = ref_model._sd
+    model.enable_view_sharding(comm=comm)
+    model.engine()
+    outs, errs = [None] * world, []
+
+    def run(rank):
+        try:
+            comm.bind(rank)
+            outs[rank] = model.forward(views)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            raise
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for r in range(world):
+        for v, o in enumerate(outs[r]):
+            if o is None:
+                continue
+            for k in ("pts3d", "conf", "cam_quats", "cam_trans", "metric_scaling_factor"):
+                e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
+                assert e < 2e-5, (variant, r, v, k, e)
