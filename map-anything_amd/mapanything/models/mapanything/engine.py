@@ -31,7 +31,7 @@ from ... import _native as nat
 from .spec import RELEASED_INFO, InfoSharingSpec
 
 ENC_DIM, ENC_HEADS, PATCH, KPAD = 1024, 16, 14, 640
-AAT_DIM, AAT_HEADS = 768, 12
+AAT_DIM, AAT_HEADS = 768, 12  # the released transformer; variants carry their own (InfoSharingSpec)
 POSE_DIM = 784
 LN_EPS = 1e-6
 DINOV2_MEAN = (0.485, 0.456, 0.406)
@@ -116,10 +116,12 @@ class PackedWeights:
         self.fus_w, self.fus_b = f32("fusion_norm_layer.weight"), f32("fusion_norm_layer.bias")
         self.scale_token = f32("scale_token")
         # AAT
-        self.pe_proj = lin("info_sharing.proj_embed")
-        self.pe_proj_b = f32("info_sharing.proj_embed.bias")
-        # sinusoid view PE table (pe_rows x 768): row 0 = the reference view's, rows 1.. the other views'
-        self.view_pos = f32("info_sharing.view_pos_table").reshape(-1, AAT_DIM) if info.ref_pe else None
+        # proj_embed is nn.Identity when the transformer is as wide as the encoder (alternating_attention_
+        # transformer.py:121-124; the 48-layer configs)
+        self.pe_proj = lin("info_sharing.proj_embed") if info.dim != ENC_DIM else None
+        self.pe_proj_b = f32("info_sharing.proj_embed.bias") if info.dim != ENC_DIM else None
+        # sinusoid view PE table (pe_rows x dim): row 0 = the reference view's, rows 1.. the other views'
+        self.view_pos = f32("info_sharing.view_pos_table").reshape(-1, info.dim) if info.ref_pe else None
         self.view_pe = self.view_pos[0].contiguous() if info.ref_pe else None
         self.aat = []
         for b in range(info.depth):
@@ -285,7 +287,8 @@ class MapaEngine:
     # ------------------------------------------------------------------------------------------- encoder
     def encode(self, imgs, taps=None, geo: Optional[GeoInputs] = None):
         """DINOv2 ViT-L/14 + final norm [+ geometric-input features] + fusion LayerNorm.  Returns fused_lp
-        [VB*T+1][1024] (last row reserved for the scale token) and fused f32 if taps is not None."""
+        [VB*T+1][1024] (last row = the scale token), the same rows in f32 if taps is not None or the transformer
+        has no input projection (else None), and the token grid."""
         w = self.w
         VB, _, H, W = imgs.shape
         hp, wp = H // PATCH, W // PATCH
@@ -296,12 +299,15 @@ class MapaEngine:
         if geo is not None and not geo.empty():
             self.geometric(enc, geo, VB, H, W)
         fused_lp = self._empty(VB * T + 1, ENC_DIM)
-        fused_f32 = self._empty(VB * T, ENC_DIM, dtype=torch.float32) if taps is not None else None
+        identity = w.pe_proj is None  # the transformer reads the fp32 fused rows directly
+        fused_f32 = self._empty(VB * T + 1, ENC_DIM, dtype=torch.float32) if taps is not None or identity else None
         self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
         nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
+        if fused_f32 is not None:
+            fused_f32[VB * T].copy_(w.scale_token)
         if taps is not None:
-            taps["fused"] = fused_f32
-        return fused_lp, (hp, wp)
+            taps["fused"] = fused_f32[:VB * T]
+        return fused_lp, fused_f32, (hp, wp)
 
     def encoder_features(self, imgs):
         """DINOv2Encoder.forward (dinov2.py:146-178): patch embed + cls + pos-embed, 24 blocks, final norm.
@@ -440,61 +446,67 @@ class MapaEngine:
         return y
 
     # ----------------------------------------------------------------------------------------------- AAT
-    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None, pe_idx=None):
+    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None, pe_idx=None, fused_f32=None):
         """The multi-view transformer with intermediate-feature return: AAT (alternating_attention_transformer.py:
         530-771; released config: 24 blocks, taps after 11 and 17) or GAT (global_attention_transformer.py:458-640:
-        every block global), per self.info.  Returns the two taps and the final features (lp, VB*T rows) and the final
-        scale-token feature (f32, 768).  pe_idx: (V_total,) int64 device tensor of view-PE table rows (row 0 for the
+        every block global), per self.info.  Returns the list of normed taps (2 or 3, lp, VB*T rows), the final
+        features (lp) and the final scale-token feature (f32, dim).  fused_f32: the fp32 fused rows (with the scale token), needed
+        when proj_embed is the identity.  pe_idx: (V_total,) int64 device tensor of view-PE table rows (row 0 for the
         reference view) when the variant encodes non-reference views too.  With `shard` (parallel.ShardPlan) this
         rank holds only its views (+ the scale-token replica) and the global layers all-gather K/V through `comm`."""
         w, info = self.w, self.info
+        D, NH = info.dim, info.heads
         L = VB * T + 1
-        y = self._empty(L, AAT_DIM, dtype=torch.float32)
-        nat.gemm(fused_lp, w.pe_proj, L, AAT_DIM, ENC_DIM, bias=w.pe_proj_b, out_f32=y)
+        if w.pe_proj is None:  # identity projection: the residual stream starts from the fp32 fused features
+            if fused_f32 is None:
+                raise ValueError("this info-sharing variant has no input projection: pass fused_f32")
+            y = fused_f32.clone() if taps is not None else fused_f32
+        else:
+            y = self._empty(L, D, dtype=torch.float32)
+            nat.gemm(fused_lp, w.pe_proj, L, D, ENC_DIM, bias=w.pe_proj_b, out_f32=y)
         first = 0 if shard is None else shard.starts[shard.rank]  # global index of this rank's first view
         if info.nonref_pe:  # view PE on every view: table rows pe_idx (row 0 on the reference view)
             vecs = w.view_pos.index_select(0, pe_idx[first:first + VB]).contiguous()
-            nat.add_view_vectors(y, T, AAT_DIM, VB, vecs, self._ones(VB), 1)
+            nat.add_view_vectors(y, T, D, VB, vecs, self._ones(VB), 1)
         elif info.ref_pe and first == 0:  # reference-view PE on view 0 only
-            nat.add_rowvec(y, AAT_DIM, 0, T, AAT_DIM, w.view_pe)
-        yn, qkv, ao = self._empty(L, AAT_DIM), self._empty(L, 3 * AAT_DIM), self._empty(L, AAT_DIM)
-        hbuf = self._empty(L, 4 * AAT_DIM)
+            nat.add_rowvec(y, D, 0, T, D, w.view_pe)
+        yn, qkv, ao = self._empty(L, D), self._empty(L, 3 * D), self._empty(L, D)
+        hbuf = self._empty(L, 4 * D)
         L_all = L if shard is None else shard.total_kv  # tokens of a global block (every view + the scale token)
         g_scale = 0.125 * info.q_scale(L_all) if (info.scalable_softmax or info.entropy_scaling) else None
         f_scale = 0.125 * info.q_scale(T) if (info.scalable_softmax or info.entropy_scaling) else None
         if shard is not None:
-            kv_full = self._empty(shard.world * shard.max_rows, 2 * AAT_DIM)
-            q_loc = self._empty(L, AAT_DIM)
+            kv_full = self._empty(shard.world * shard.max_rows, 2 * D)
+            q_loc = self._empty(L, D)
         inter = {}
-        i0, i1 = info.indices
         for d, p in enumerate(w.aat):
             if info.is_global(d):   # global attention over every view + the scale token
                 if shard is None:
-                    self._block(y, yn, qkv, ao, hbuf, L, AAT_DIM, AAT_HEADS, p, attn_batch=1, attn_seq=L, gamma=False,
+                    self._block(y, yn, qkv, ao, hbuf, L, D, NH, p, attn_batch=1, attn_seq=L, gamma=False,
                                 attn_kind="attention_global", attn_scale=g_scale)
                 else:
                     self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, g_scale)
             else:                   # frame attention inside each view; the scale token bypasses the block
-                self._block(y, yn, qkv, ao, hbuf, VB * T, AAT_DIM, AAT_HEADS, p, attn_batch=VB, attn_seq=T,
+                self._block(y, yn, qkv, ao, hbuf, VB * T, D, NH, p, attn_batch=VB, attn_seq=T,
                             gamma=False, attn_scale=f_scale)
-            if d in (i0, i1):
-                t_lp = self._empty(VB * T, AAT_DIM)
-                t_f = self._empty(VB * T, AAT_DIM, dtype=torch.float32) if taps is not None else None
-                self._ln(y, VB * T, AAT_DIM, w.aat_nw, w.aat_nb, y_lp=t_lp, y_f32=t_f)
+            if d in info.indices:
+                t_lp = self._empty(VB * T, D)
+                t_f = self._empty(VB * T, D, dtype=torch.float32) if taps is not None else None
+                self._ln(y, VB * T, D, w.aat_nw, w.aat_nb, y_lp=t_lp, y_f32=t_f)
                 inter[d] = t_lp
                 if taps is not None:
                     taps[f"aat_l{d}"] = t_f
-                    tk = self._empty(1, AAT_DIM, dtype=torch.float32)  # the scale token, normed as well
-                    self._ln(y[VB * T:], 1, AAT_DIM, w.aat_nw, w.aat_nb, y_f32=tk)
+                    tk = self._empty(1, D, dtype=torch.float32)  # the scale token, normed as well
+                    self._ln(y[VB * T:], 1, D, w.aat_nw, w.aat_nb, y_f32=tk)
                     taps[f"aat_l{d}_token"] = tk
         del yn, qkv, ao, hbuf
-        fin_lp = self._empty(L, AAT_DIM)
-        fin_f32 = self._empty(L, AAT_DIM, dtype=torch.float32)
-        self._ln(y, L, AAT_DIM, w.aat_nw, w.aat_nb, y_lp=fin_lp, y_f32=fin_f32)
+        fin_lp = self._empty(L, D)
+        fin_f32 = self._empty(L, D, dtype=torch.float32)
+        self._ln(y, L, D, w.aat_nw, w.aat_nb, y_lp=fin_lp, y_f32=fin_f32)
         if taps is not None:
             taps["aat_final"] = fin_f32[:VB * T]
             taps["scale_token"] = fin_f32[VB * T]
-        return inter[i0], inter[i1], fin_lp, fin_f32[VB * T:]
+        return [inter[i] for i in info.indices], fin_lp, fin_f32[VB * T:]
 
     def _ones(self, n):
         o = getattr(self, "_ones_buf", None)
@@ -507,12 +519,12 @@ class MapaEngine:
         The all-gather runs on the communicator's stream while the local queries attend to this rank's own keys;
         the remote-key partial follows the gather and the two partials are merged through their LSEs
         (MAPA_KV_OVERLAP=0: gather first, one attention over every key)."""
-        C = AAT_DIM
+        C, NH = self.info.dim, self.info.heads
         self._ln(y, L, C, p["n1w"], p["n1b"], y_lp=yn)
         nat.gemm(yn, p["qkv"][:C], L, C, C, bias=p["qkv_b"][:C], out_lp=q_loc)
         slot = kv_full[shard.rank * shard.max_rows:]
         nat.gemm(yn, p["qkv"][C:], L, 2 * C, C, bias=p["qkv_b"][C:], out_lp=slot, ldo=2 * C)
-        strides = dict(batch=1, heads=AAT_HEADS, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
+        strides = dict(batch=1, heads=NH, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
                        v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C, scale=scale)
         overlap = hasattr(comm, "allgather_slots_async") and os.environ.get("MAPA_KV_OVERLAP", "1") != "0"
         if not overlap:
@@ -524,15 +536,15 @@ class MapaEngine:
             segs = shard.kv_segments()
             own = segs[shard.rank]
             rest = [sg for r, sg in enumerate(segs) if r != shard.rank]
-            lse_l = self._empty(AAT_HEADS, L, dtype=torch.float32)
+            lse_l = self._empty(NH, L, dtype=torch.float32)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=own[1], kv_segments=[own], lse=lse_l,
                           kind="attention_global", **strides)
             handle.wait()
             ao_r = self._empty(L, C)
-            lse_r = self._empty(AAT_HEADS, L, dtype=torch.float32)
+            lse_r = self._empty(NH, L, dtype=torch.float32)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao_r, seq_kv=sum(sg[1] for sg in rest), kv_segments=rest,
                           lse=lse_r, kind="attention_global", **strides)
-            nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, AAT_HEADS, C)
+            nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, NH, C)
         nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
         self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)
         nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
@@ -540,6 +552,8 @@ class MapaEngine:
 
     # ----------------------------------------------------------------------------------------------- DPT
     def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None):
+        """fused_lp: the first DPT input — the fused encoder features (ENC_DIM) or, with three info-sharing taps
+        (model.py:1748-1768), the first tap (AAT_DIM); its width comes from the packed weight."""
         """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Returns the ReLU'd 128-ch hidden map at HxW."""
         owned = [self.dpt_feature(fused_lp, l11, l17, fin_lp, VB, hp, wp, taps)[0]]
         return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W)  # freed after its first conv
@@ -550,9 +564,9 @@ class MapaEngine:
         w = self.w
         n, T = VB, hp * wp
         lp = self.lp
-        # input_process 0: 1x1 1024->96, ConvT k4 s4, layer1_rn 3x3 96->256 (no bias)
+        # input_process 0: 1x1 1024 (or 768)->96, ConvT k4 s4, layer1_rn 3x3 96->256 (no bias)
         a = self._empty(n * T, 96)
-        nat.gemm(fused_lp, w.ip[0]["w"], n * T, 96, ENC_DIM, bias=w.ip[0]["b"], out_lp=a)
+        nat.gemm(fused_lp, w.ip[0]["w"], n * T, 96, w.ip[0]["w"].shape[1], bias=w.ip[0]["b"], out_lp=a)
         up0 = self._empty(n, 4 * hp, 4 * wp, 96)
         nat.gemm(a, w.ip[0]["ct"], n * T, 16 * 96, 96, bias=w.ip[0]["ct_b"], bias_mod=96, out_lp=up0,
                  pixshuf=(4, hp, wp, 96))
@@ -563,7 +577,7 @@ class MapaEngine:
         del a, up0
         # input_process 1: 1x1 768->192, ConvT k2 s2, layer2_rn
         a = self._empty(n * T, 192)
-        nat.gemm(l11, w.ip[1]["w"], n * T, 192, AAT_DIM, bias=w.ip[1]["b"], out_lp=a)
+        nat.gemm(l11, w.ip[1]["w"], n * T, 192, self.info.dim, bias=w.ip[1]["b"], out_lp=a)
         up1 = self._empty(n, 2 * hp, 2 * wp, 192)
         nat.gemm(a, w.ip[1]["ct"], n * T, 4 * 192, 192, bias=w.ip[1]["ct_b"], bias_mod=192, out_lp=up1,
                  pixshuf=(2, hp, wp, 192))
@@ -574,14 +588,14 @@ class MapaEngine:
         del a, up1
         # input_process 2: 1x1 768->384, layer3_rn
         a = self._empty(n * T, 384)
-        nat.gemm(l17, w.ip[2]["w"], n * T, 384, AAT_DIM, bias=w.ip[2]["b"], out_lp=a)
+        nat.gemm(l17, w.ip[2]["w"], n * T, 384, self.info.dim, bias=w.ip[2]["b"], out_lp=a)
         L2f = self._empty(n * T, 256, dtype=torch.float32)
         L2r = self._empty(n * T, 256)
         self._conv3(a, n, hp, wp, 384, w.layer_rn[2], 256, out_f32=L2f, out_lp_relu=L2r)
         del a
         # input_process 3: 1x1 768->768, 3x3 s2 768->768, layer4_rn
         a = self._empty(n * T, 768)
-        nat.gemm(fin_lp, w.ip[3]["w"], n * T, 768, AAT_DIM, bias=w.ip[3]["b"], out_lp=a)
+        nat.gemm(fin_lp, w.ip[3]["w"], n * T, 768, self.info.dim, bias=w.ip[3]["b"], out_lp=a)
         h3, w3 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1
         b3 = self._empty(n * h3 * w3, 768)
         self._conv3(a, n, hp, wp, 768, w.ip[3]["c3"], 768, stride=2, bias=w.ip[3]["c3_b"], out_lp=b3)
@@ -667,7 +681,7 @@ class MapaEngine:
         M = VB * T
         pf = self._empty(M, POSE_DIM, dtype=torch.float32)
         pl = self._empty(M, POSE_DIM)
-        nat.gemm(fin_lp, w.pose_proj, M, POSE_DIM, AAT_DIM, bias=w.pose_proj_b, out_f32=pf, out_lp=pl)
+        nat.gemm(fin_lp, w.pose_proj, M, POSE_DIM, self.info.dim, bias=w.pose_proj_b, out_f32=pf, out_lp=pl)
         t1, t2 = self._empty(M, POSE_DIM), self._empty(M, POSE_DIM)
         for blk in w.pose_res:
             (w1, b1), (w2, b2), (w3, b3) = blk
@@ -691,7 +705,7 @@ class MapaEngine:
         w = self.w.scale_mlp
         a = self._empty(1, 196, dtype=torch.float32)
         b = self._empty(1, 196, dtype=torch.float32)
-        nat.linear_small(tok, 1, AAT_DIM, w[0][0], w[0][1], 196, nat.ACT_NONE, a)
+        nat.linear_small(tok, 1, self.info.dim, w[0][0], w[0][1], 196, nat.ACT_NONE, a)
         nat.linear_small(a, 1, 196, w[1][0], w[1][1], 196, nat.ACT_RELU, b)
         nat.linear_small(b, 1, 196, w[2][0], w[2][1], 196, nat.ACT_RELU, a)
         raw = self._empty(1, dtype=torch.float32)
@@ -717,13 +731,16 @@ class MapaEngine:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
         with torch.cuda.device(self.device):
-            fused_lp, (hp, wp) = self.encode(imgs, taps, geo)
+            fused_lp, fused_f32, (hp, wp) = self.encode(imgs, taps, geo)
             T = hp * wp
             if shard is not None and (shard.counts[shard.rank] != VB or shard.tokens_per_view != T):
                 raise AssertionError("shard plan does not match the local views")
             if self.info.nonref_pe and pe_idx is None:
                 raise ValueError("this info-sharing variant encodes every view's index: pass pe_idx")
-            l11, l17, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx)
+            inter, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx,
+                                          fused_f32=fused_f32)
+            # DPT inputs (model.py:1724-1768): [encoder, tap0, tap1, final] or, with three taps, [tap0..2, final]
+            first, l11, l17 = (inter[0], inter[1], inter[2]) if len(inter) == 3 else (fused_lp, inter[0], inter[1])
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)
@@ -740,7 +757,7 @@ class MapaEngine:
             for v0 in range(0, VB, chunk):
                 n = min(chunk, VB - v0)
                 r0, r1 = v0 * T, (v0 + n) * T
-                hid = self.dpt(fused_lp[r0:r1], l11[r0:r1], l17[r0:r1], fin_lp[r0:r1], n, hp, wp, H, W,
+                hid = self.dpt(first[r0:r1], l11[r0:r1], l17[r0:r1], fin_lp[r0:r1], n, hp, wp, H, W,
                                taps if n == VB else None)
                 nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, pose_out[v0:v0 + n], scale, 1,
                                    out["pts3d"][v0:v0 + n], out["pts3d_cam"][v0:v0 + n],

@@ -48,9 +48,13 @@ def _check_config(encoder_config, info_sharing_config, pred_head_config):
     args = info_sharing_config.get("module_args", {})
     depth = int(args.get("depth", 12))
     idx = list(args.get("indices", []))
-    if len(idx) != 2 or not all(0 <= int(i) < depth for i in idx) or int(idx[0]) >= int(idx[1]):
-        # 3 indices (model.py:322-330: DPT on info-sharing taps only) is not part of this engine
-        problems.append(f"info-sharing intermediate indices {idx} (two increasing block indices < depth)")
+    if (len(idx) not in (2, 3) or not all(0 <= int(i) < depth for i in idx)
+            or any(int(a) >= int(b) for a, b in zip(idx, idx[1:]))):
+        problems.append(f"info-sharing intermediate indices {idx} (2 or 3 increasing block indices < depth)")
+    dim, heads = int(args.get("dim", 768)), int(args.get("num_heads", 12))
+    if heads <= 0 or dim != 64 * heads or float(args.get("mlp_ratio", 4.0)) != 4.0:
+        # the attention kernels are built for 64-wide heads (768/12 and the 48-layer 1024/16)
+        problems.append(f"info-sharing dim {dim} / {heads} heads / mlp_ratio {args.get('mlp_ratio', 4.0)}")
     if (info_sharing_config.get("custom_positional_encoding") is not None
             or args.get("custom_positional_encoding") is not None):
         # RoPE-2D: with MapAnything's scale token the reference adds a list of None positions to the position

@@ -25,7 +25,7 @@ from uniception.models.prediction_heads import (AdaptorOutput, DPTFeatureInput, 
                                                 RegressionWithConfidenceAndMaskAdaptorOutput, SummaryTaskOutput)
 
 from ... import _native as nat
-from .engine import AAT_DIM, ENC_DIM, PATCH
+from .engine import ENC_DIM, PATCH
 
 f32 = torch.float32
 
@@ -78,10 +78,13 @@ class DINOv2Encoder(_EngineModule):
 
 class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
     """uniception/models/info_sharing/alternating_attention_transformer.py:530-771 (released config: depth 24,
-    dim 768, IFR indices [11, 17], intermediates normed) — or, for a global_attention config, the GAT of
+    dim 768, IFR indices [11, 17], intermediates normed; any depth / width with 64-wide heads / 2 or 3 indices,
+    e.g. the 48-layer width-1024 configs) — or, for a global_attention config, the GAT of
     global_attention_transformer.py:458-640 (the engine follows model.info).  Exactly one additional input token
     (MapAnything's scale token)."""
-    dim = AAT_DIM
+    @property
+    def dim(self):
+        return self._model.info.dim
 
     @property
     def indices(self):
@@ -100,37 +103,38 @@ class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
             raise AssertionError("every view's features must be (B, 1024, h, w)")
         T = h * w
         eng = self._eng()
-        i0, i1 = self._model.info.indices
-        final, l11, l17 = ([None] * B for _ in range(3))
-        final_tok, tok11, tok17 = [None] * B, [None] * B, [None] * B
+        idx, D = self._model.info.indices, self._model.info.dim
+        final, final_tok = [None] * B, [None] * B
+        inter = [[None] * B for _ in idx]
+        inter_tok = [[None] * B for _ in idx]
         with torch.cuda.device(eng.device):
             for b in range(B):
-                fused = torch.empty(V * T + 1, ENC_DIM, dtype=eng.lp, device=eng.device)
-                fused[:V * T] = _rows(torch.stack([self._dev(f[b]) for f in feats], 0), eng.lp)
-                fused[V * T] = self._dev(tok[b, :, 0], eng.lp)
+                f32 = torch.empty(V * T + 1, ENC_DIM, dtype=torch.float32, device=eng.device)
+                f32[:V * T] = _rows(torch.stack([self._dev(f[b]) for f in feats], 0), torch.float32)
+                f32[V * T] = self._dev(tok[b, :, 0], torch.float32)
                 taps = {}
-                eng.aat(fused, V, T, taps, pe_idx=self._model._view_pe_rows(V))
-                final[b] = taps["aat_final"].reshape(V, h, w, AAT_DIM)
-                l11[b] = taps[f"aat_l{i0}"].reshape(V, h, w, AAT_DIM)
-                l17[b] = taps[f"aat_l{i1}"].reshape(V, h, w, AAT_DIM)
-                final_tok[b], tok11[b], tok17[b] = (taps["scale_token"], taps[f"aat_l{i0}_token"],
-                                                    taps[f"aat_l{i1}_token"])
+                eng.aat(f32.to(eng.lp), V, T, taps, pe_idx=self._model._view_pe_rows(V), fused_f32=f32)
+                final[b], final_tok[b] = taps["aat_final"].reshape(V, h, w, D), taps["scale_token"]
+                for j, d in enumerate(idx):
+                    inter[j][b] = taps[f"aat_l{d}"].reshape(V, h, w, D)
+                    inter_tok[j][b] = taps[f"aat_l{d}_token"]
 
         def pack(per_b, toks):
             views = [torch.stack([per_b[b][v] for b in range(B)], 0).permute(0, 3, 1, 2).contiguous()
                      for v in range(V)]
             return MultiViewTransformerOutput(features=views,
                                               additional_token_features=torch.stack(
-                                                  [t.reshape(AAT_DIM, 1) for t in toks], 0))
+                                                  [t.reshape(D, 1) for t in toks], 0))
 
-        return pack(final, final_tok), [pack(l11, tok11), pack(l17, tok17)]
+        return pack(final, final_tok), [pack(inter[j], inter_tok[j]) for j in range(len(idx))]
 
 
 MultiViewGlobalAttentionTransformerIFR = MultiViewAlternatingAttentionTransformerIFR  # same engine entry
 
 
 class DPTFeature(_EngineModule):
-    """uniception/models/prediction_heads/dpt.py:180-232: four features (1024, 768, 768, 768 channels) -> the
+    """uniception/models/prediction_heads/dpt.py:180-232: four features (1024, 768, 768, 768 channels; with three
+    info-sharing taps all four are the transformer's width, model.py:362-372) -> the
     256-channel map at 8x the token grid."""
 
     @torch.no_grad()
@@ -236,11 +240,12 @@ class MLPHead(_EngineModule):
     @torch.no_grad()
     def forward(self, head_input) -> SummaryTaskOutput:
         x = self._dev(head_input.last_feature)
-        if x.dim() != 3 or x.shape[1] != AAT_DIM or x.shape[2] != 1:
-            raise AssertionError(f"scale head expects (B, {AAT_DIM}, 1), got {tuple(x.shape)}")
+        D = self._model.info.dim
+        if x.dim() != 3 or x.shape[1] != D or x.shape[2] != 1:
+            raise AssertionError(f"scale head expects (B, {D}, 1), got {tuple(x.shape)}")
         eng = self._eng()
         with torch.cuda.device(eng.device):
-            out = torch.stack([eng.scale(x[b, :, 0].reshape(1, AAT_DIM).contiguous()) for b in range(x.shape[0])])
+            out = torch.stack([eng.scale(x[b, :, 0].reshape(1, D).contiguous()) for b in range(x.shape[0])])
         return SummaryTaskOutput(decoded_channels=out.reshape(-1, 1, 1))
 
 

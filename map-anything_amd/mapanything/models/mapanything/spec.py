@@ -46,7 +46,9 @@ class InfoSharingSpec:
     """
     kind: str = "alternating"
     depth: int = 24
-    indices: Tuple[int, int] = (11, 17)
+    dim: int = AAT_DIM      # 1024 / 16 heads in the 48-layer configs (proj_embed is then the identity)
+    heads: int = 12
+    indices: Tuple[int, ...] = (11, 17)  # 2 taps (DPT also reads the encoder features) or 3 (it does not)
     ref_pe: bool = True
     nonref_pe: bool = False
     rand_idx: bool = True
@@ -62,7 +64,8 @@ class InfoSharingSpec:
             return InfoSharingSpec()
         a = info_sharing_config.get("module_args", {})
         kind = "global" if info_sharing_config.get("model_type") == "global_attention" else "alternating"
-        common = dict(depth=int(a.get("depth", 12)), indices=tuple(int(i) for i in a.get("indices", (11, 17))),
+        common = dict(depth=int(a.get("depth", 12)), dim=int(a.get("dim", 768)), heads=int(a.get("num_heads", 12)),
+                      indices=tuple(int(i) for i in a.get("indices", (11, 17))),
                       scalable_softmax=bool(a.get("use_scalable_softmax", False)),
                       entropy_scaling=bool(a.get("use_entropy_scaling", False)),
                       entropy_base=int(a.get("base_token_count_for_entropy_scaling", 444)),
@@ -161,21 +164,24 @@ def canonical_spec(info: InfoSharingSpec = RELEASED_INFO) -> Spec:
     _global_rep_encoder(s, "cam_trans_scale_encoder", 1)
     _ln(s, "fusion_norm_layer", ENC_DIM)
     # AAT
+    D = info.dim
     if info.ref_pe:
-        s.append(("info_sharing.view_pos_table", (info.pe_rows, AAT_DIM)))
-    _linear(s, "info_sharing.proj_embed", AAT_DIM, ENC_DIM)
+        s.append(("info_sharing.view_pos_table", (info.pe_rows, D)))
+    if D != ENC_DIM:  # nn.Identity otherwise (alternating_attention_transformer.py:121-124)
+        _linear(s, "info_sharing.proj_embed", D, ENC_DIM)
     for b in range(info.depth):
         p = f"info_sharing.self_attention_blocks.{b}"
-        _ln(s, f"{p}.norm1", AAT_DIM)
-        _linear(s, f"{p}.attn.qkv", 3 * AAT_DIM, AAT_DIM)
-        _linear(s, f"{p}.attn.proj", AAT_DIM, AAT_DIM)
-        _ln(s, f"{p}.norm2", AAT_DIM)
-        _linear(s, f"{p}.mlp.fc1", AAT_MLP, AAT_DIM)
-        _linear(s, f"{p}.mlp.fc2", AAT_DIM, AAT_MLP)
-    _ln(s, "info_sharing.norm", AAT_DIM)
+        _ln(s, f"{p}.norm1", D)
+        _linear(s, f"{p}.attn.qkv", 3 * D, D)
+        _linear(s, f"{p}.attn.proj", D, D)
+        _ln(s, f"{p}.norm2", D)
+        _linear(s, f"{p}.mlp.fc1", 4 * D, D)
+        _linear(s, f"{p}.mlp.fc2", D, 4 * D)
+    _ln(s, "info_sharing.norm", D)
     # DPT feature head
     h = "dpt_feature_head"
-    in_dims = (ENC_DIM, AAT_DIM, AAT_DIM, AAT_DIM)
+    # three info-sharing taps feed the DPT without the encoder features (model.py:362-372)
+    in_dims = (D if len(info.indices) == 3 else ENC_DIM, D, D, D)
     for i, ld in enumerate(DPT_LAYER_DIMS):
         s.append((f"{h}.scratch.layer{i + 1}_rn.weight", (DPT_FEAT, ld, 3, 3)))
     for r in (1, 2, 3, 4):
@@ -197,7 +203,7 @@ def canonical_spec(info: InfoSharingSpec = RELEASED_INFO) -> Spec:
     _conv(s, "dpt_regressor_head.conv2.0", 128, 128, 3)
     _conv(s, "dpt_regressor_head.conv2.2", 6, 128, 1)
     # pose head
-    _conv(s, "pose_head.proj", POSE_DIM, AAT_DIM, 1)
+    _conv(s, "pose_head.proj", POSE_DIM, D, 1)
     for b in range(2):
         for c in (1, 2, 3):
             _conv(s, f"pose_head.res_conv.{b}.res_conv{c}", POSE_DIM, POSE_DIM, 1)
@@ -206,7 +212,7 @@ def canonical_spec(info: InfoSharingSpec = RELEASED_INFO) -> Spec:
     _linear(s, "pose_head.fc_t", 3, POSE_DIM)
     _linear(s, "pose_head.fc_rot", 4, POSE_DIM)
     # scale head
-    _linear(s, "scale_head.proj", 196, AAT_DIM)
+    _linear(s, "scale_head.proj", 196, D)
     _linear(s, "scale_head.mlp.0.0", 196, 196)
     _linear(s, "scale_head.mlp.1.0", 196, 196)
     _linear(s, "scale_head.output_proj", 1, 196)

@@ -91,9 +91,9 @@ class MapAnythingOracle:
         x = x + self.p(f"{name}.ls2.gamma") * self.mlp(self.ln(x, f"{name}.norm2"), f"{name}.mlp")
         return x
 
-    def aat_block(self, x, name, qmul=None):
+    def aat_block(self, x, name, qmul=None, heads=AAT_HEADS):
         """transformer_blocks.py:452-469 (init_values=None -> no LayerScale, eval -> no drop path)."""
-        x = x + self.attention(self.ln(x, f"{name}.norm1"), f"{name}.attn", AAT_HEADS, qmul)
+        x = x + self.attention(self.ln(x, f"{name}.norm1"), f"{name}.attn", heads, qmul)
         x = x + self.mlp(self.ln(x, f"{name}.norm2"), f"{name}.mlp")
         return x
 
@@ -235,7 +235,8 @@ class MapAnythingOracle:
         info = self.info
         kind = getattr(info, "kind", "alternating")
         depth = getattr(info, "depth", 24)
-        i0, i1 = getattr(info, "indices", (11, 17))
+        indices = tuple(getattr(info, "indices", (11, 17)))
+        D, heads = getattr(info, "dim", AAT_DIM), getattr(info, "heads", AAT_HEADS)
         ref_pe, nonref_pe = getattr(info, "ref_pe", True), getattr(info, "nonref_pe", False)
         qmul = None
         if info is not None and (info.scalable_softmax or info.entropy_scaling):
@@ -251,7 +252,8 @@ class MapAnythingOracle:
         T = h * w
         x = torch.stack(feats, 1).permute(0, 1, 3, 4, 2).reshape(B, V * T, C)
         x = torch.cat([x, scale_token.permute(0, 2, 1)], 1)
-        x = self.lin(x, "info_sharing.proj_embed")
+        if "info_sharing.proj_embed.weight" in self.sd:  # nn.Identity when dim == 1024 (:121-124)
+            x = self.lin(x, "info_sharing.proj_embed")
         if ref_pe:
             table = self.p("info_sharing.view_pos_table")
             rows = list(pe_rows) if pe_rows is not None else list(range(V))
@@ -259,37 +261,36 @@ class MapAnythingOracle:
             for v in range(V):
                 xv = x[:, v * T:(v + 1) * T]
                 if v == 0:
-                    xv = xv + table[0].reshape(1, 1, AAT_DIM)
+                    xv = xv + table[0].reshape(1, 1, D)
                 elif nonref_pe:
-                    xv = xv + table[rows[v]].reshape(1, 1, AAT_DIM)
+                    xv = xv + table[rows[v]].reshape(1, 1, D)
                 parts.append(xv)
             x = torch.cat(parts + [x[:, V * T:]], 1)
         inter = []
         for d in range(depth):
             name = f"info_sharing.self_attention_blocks.{d}"
             if kind == "global" or d % 2 == 0:
-                x = self.aat_block(x, name, qmul)
+                x = self.aat_block(x, name, qmul, heads)
             else:
                 extra = x[:, V * T:]
-                xv = x[:, :V * T].reshape(B * V, T, AAT_DIM)
-                xv = self.aat_block(xv, name, qmul).reshape(B, V * T, AAT_DIM)
+                xv = x[:, :V * T].reshape(B * V, T, D)
+                xv = self.aat_block(xv, name, qmul, heads).reshape(B, V * T, D)
                 x = torch.cat([xv, extra], 1)
-            if d in (i0, i1):
+            if d in indices:
                 inter.append(self.ln(x, "info_sharing.norm"))
         out = self.ln(x, "info_sharing.norm")
 
         def split(y):
-            f = y[:, :V * T].reshape(B, V, h, w, AAT_DIM).permute(0, 1, 4, 2, 3)
+            f = y[:, :V * T].reshape(B, V, h, w, D).permute(0, 1, 4, 2, 3)
             return [f[:, i] for i in range(V)], y[:, V * T:].permute(0, 2, 1)
 
         final_feats, tok = split(out)
-        l11, _ = split(inter[0])
-        l17, _ = split(inter[1])
+        taps = [split(t)[0] for t in inter]
         self.taps["aat_final"] = torch.stack(final_feats, 1)
-        self.taps["aat_l11"] = torch.stack(l11, 1)
-        self.taps["aat_l17"] = torch.stack(l17, 1)
+        for d, t in zip(indices, taps):
+            self.taps[f"aat_l{d}"] = torch.stack(t, 1)
         self.taps["scale_token"] = tok
-        return final_feats, l11, l17, tok
+        return final_feats, taps, tok
 
     # ------------------------------------------------------------------------------------------------- DPT
     def rcu(self, x, name):
@@ -364,8 +365,10 @@ class MapAnythingOracle:
         V = len(views)
         fused = self.encode_and_fuse(views)
         scale_tok = self.p("scale_token").view(1, -1, 1).repeat(B, 1, 1)
-        final, l11, l17, tok = self.aat(list(fused), scale_tok)
-        layers = [torch.cat(fused, 0), torch.cat(l11, 0), torch.cat(l17, 0), torch.cat(final, 0)]
+        final, taps, tok = self.aat(list(fused), scale_tok)
+        # DPT inputs (model.py:1724-1768): [encoder, tap0, tap1, final]; with three taps [tap0, tap1, tap2, final]
+        first = [torch.cat(fused, 0)] if len(taps) == 2 else []
+        layers = first + [torch.cat(t, 0) for t in taps] + [torch.cat(final, 0)]
         feat = self.dpt_feature(layers)
         self.taps["dpt_feature"] = feat
         dense = self.dpt_regressor(feat, (H, W))                              # (V*B, 6, H, W)

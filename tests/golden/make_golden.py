@@ -21,6 +21,9 @@ Info-sharing variants (the reference built with a modifi
                implementations' RNG use)
   aatpe_224    3 views 224x224, AAT with PE on the non-reference views too (sequential) and scalable softmax
   aatnoref_224 2 views 224x224, AAT without any view PE (distinguish_ref_and_non_ref_views False)
+  aat48_224    2 views 224x224, configs/model/info_sharing/aat_ifr_48_layers_escaling.yaml: 48 blocks of width 1024
+               / 16 heads (proj_embed = identity), three taps [11, 23, 35] feeding the DPT without the encoder
+               features (model.py:323-330, 1748-1768), entropy scaling
 """
 
 import importlib.util
@@ -81,6 +84,10 @@ VARIANTS = {
                   dict(views=3, h=224, w=224, seed=9)),
     "aatnoref_224": (_info_cfg("alternating_attention", distinguish_ref_and_non_ref_views=False),
                      dict(views=2, h=224, w=224, seed=10)),
+    "aat48_224": (_info_cfg("alternating_attention", name="aat_48_layers_ifr", indices=[11, 23, 35], size="48_layers",
+                            depth=48, dim=1024, num_heads=16, distinguish_ref_and_non_ref_views=True,
+                            use_entropy_scaling=True),
+                  dict(views=2, h=224, w=224, seed=11)),
 }
 
 
@@ -131,8 +138,8 @@ class Taps:
     def _aat(self, m, i, o):
         final, inter = o
         self.d["tap_aat_final"] = torch.stack(final.features, 1).float().numpy().copy()
-        self.d["tap_aat_l11"] = torch.stack(inter[0].features, 1).float().numpy().copy()
-        self.d["tap_aat_l17"] = torch.stack(inter[1].features, 1).float().numpy().copy()
+        for d, t in zip(m.indices, inter):  # the taps are named by their block index
+            self.d[f"tap_aat_l{d}"] = torch.stack(t.features, 1).float().numpy().copy()
         self.d["tap_scale_token"] = final.additional_token_features.float().numpy().copy()
 
     def _dpt(self, m, i, o):
@@ -198,7 +205,6 @@ KEEP_OUT = ("out_pts3d", "out_ray_directions", "out_depth_along_ray", "out_conf"
             "out_cam_trans", "out_cam_quats", "out_metric_scaling_factor", "out_intrinsics", "out_camera_poses")
 DENSE = ("out_pts3d", "out_ray_directions", "out_depth_along_ray", "out_conf", "out_non_ambiguous_mask_logits")
 SPATIAL_TAPS_NCHW = ("tap_encoder", "tap_dpt_feature")
-SPATIAL_TAPS_AAT = ("tap_aat_final", "tap_aat_l11", "tap_aat_l17")
 
 
 def shrink(d, out_step, tap_step, dpt_step):
@@ -210,8 +216,9 @@ def shrink(d, out_step, tap_step, dpt_step):
         out[k] = v[:, :, ::out_step, ::out_step] if k in DENSE else v
     out["tap_encoder"] = d["tap_encoder"][:, :, ::tap_step, ::tap_step]
     out["tap_fused_nhwc"] = d["tap_fused_nhwc"][:, ::tap_step, ::tap_step, :]
-    for k in SPATIAL_TAPS_AAT:
-        out[k] = d[k][:, :, :, ::tap_step, ::tap_step]
+    for k in d:
+        if k.startswith("tap_aat_"):
+            out[k] = d[k][:, :, :, ::tap_step, ::tap_step]
     out["tap_dpt_feature"] = d["tap_dpt_feature"][:, :, ::dpt_step, ::dpt_step]
     for k in ("tap_scale_token", "tap_pose_raw", "tap_scale_raw"):
         out[k] = d[k]
@@ -220,7 +227,7 @@ def shrink(d, out_step, tap_step, dpt_step):
 
 STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8),
          "ns_280x392": (4, 2, 8), "one_224": (2, 2, 8), "gat_224": (4, 2, 8), "aatpe_224": (4, 2, 8),
-         "aatnoref_224": (4, 2, 8)}
+         "aatnoref_224": (4, 2, 8), "aat48_224": (4, 2, 8)}
 
 
 def rel_l2(a, b):

@@ -224,13 +224,14 @@ def test_hip_graph_replay_matches_eager(model, precision):
 
 
 # ------------------------------------------------------------------------------ info-sharing variants (§8(f) row 4)
-@pytest.mark.parametrize("name", ["gat_224", "aatpe_224", "aatnoref_224"])
+@pytest.mark.parametrize("name", ["gat_224", "aatpe_224", "aatnoref_224", "aat48_224"])
 def test_info_sharing_variants_match_reference(golden, name):
     """GAT (24 global blocks, view PE on every view, entropy scaling), AAT with non-reference-view PE + scalable
     softmax, AAT without view PE: the reference rebuilt with each info_sharing_config (make_golden.py VARIANTS).
     fp32 mode at 1e-4; bf16 mode at 3x the reference's own bf16-vs-fp32 deviation on the same variant (scalable
     softmax multiplies the logits by ln N, so aatpe's is ~17x cfg1's), floor 5e-3 — for aatnoref, whose bf16 path
-    fails in the reference itself (make_golden.py), cfg1's with floor 1e-2; the transformer taps at 1e-4 in fp32."""
+    fails in the reference itself (make_golden.py), cfg1's with floor 1e-2; the transformer taps at 1e-4 in fp32.
+    aat48: the 48-layer escaling config (width 1024 / 16 heads, identity proj_embed, three taps into the DPT)."""
     from mapanything.models import MapAnything
     from tests_helpers import variant_config
 
@@ -254,7 +255,9 @@ def test_info_sharing_variants_match_reference(golden, name):
     tap_step = _meta(name)["steps_out_tap_dpt"][1]
     T = taps["aat_final"].shape[0] // case["views"]
     h = w = int(round(T ** 0.5))
-    for key in ("aat_final", "aat_l11", "aat_l17"):
+    keys = [k[4:] for k in g if k.startswith("tap_aat_")]  # final + the taps, named by block index
+    assert len(keys) == 1 + len(m.info.indices)
+    for key in keys:
         mine = taps[key].reshape(case["views"], h, w, -1).permute(0, 3, 1, 2)[None].cpu().numpy()
         ref = g[f"tap_{key}"]
         mine = mine[:, :, :, ::tap_step, ::tap_step]

@@ -108,7 +108,7 @@ def test_sharded_geometric_inputs_equal_single(precision, tol):
                 assert e < tol, (r, v, k, e)
 
 
-@pytest.mark.parametrize("variant", ["gat_224", "aatpe_224"])
+@pytest.mark.parametrize("variant", ["gat_224", "aatpe_224", "aat48_224"])
 def test_sharded_variants_equal_single(variant):
     """Info-sharing variants on the sharded path: GAT (every block global, view PE on every view: each rank adds
     the rows of its own views) and AAT with non-reference PE + scalable softmax (scale from the global token count

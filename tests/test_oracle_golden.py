@@ -59,7 +59,7 @@ def test_oracle_matches_reference(oracle, golden, name):
             mine = taps["encoder"].numpy()[:, :, ::tap_step, ::tap_step]
         elif key == "tap_fused_nhwc":
             mine = taps["fused_nhwc"].numpy()[:, ::tap_step, ::tap_step, :]
-        elif key in ("tap_aat_final", "tap_aat_l11", "tap_aat_l17"):
+        elif key.startswith("tap_aat_"):  # final + the taps, named by block index
             mine = taps[key[4:]].numpy()[:, :, :, ::tap_step, ::tap_step]
         elif key == "tap_dpt_feature":
             mine = taps["dpt_feature"].numpy()[:, :, ::dpt_step, ::dpt_step]

@@ -24,7 +24,7 @@ CASES = {
 
 
 # Info-sharing variants (make_golden.py VARIANTS): the reference rebuilt with these info_sharing_configs
-VARIANT_CASES = ("gat_224", "aatpe_224", "aatnoref_224")
+VARIANT_CASES = ("gat_224", "aatpe_224", "aatnoref_224", "aat48_224")
 
 
 def variant_config(name):
