@@ -215,6 +215,13 @@ int mapa_denorm_image(const float* img, int n, int H, int W, const float* mean, 
 int mapa_convert_rows(const float* src, int64_t lds, int rows, int cols, void* dst, int dst_dtype, int64_t ldd,
                       mapa_stream_t stream);
 
+/* Split-precision operand for the fp32 geometric encoders in bf16 mode: x fp32 [rows][cols] (row stride ldx) ->
+ * y bf16 [rows][3*cols_padded] = [hi | hi | lo] blocks (hi = bf16(x), lo = bf16(x - hi), zero past cols); paired
+ * with weights packed [hi | lo | hi] a bf16 GEMM over K = 3*cols_padded gives the fp32 product to ~2^-16.
+ * Replaces the fp32 conv/linear operands of DenseRepresentationEncoder (dense_rep_encoder.py:234-287). */
+int mapa_split_bf16x3(const float* x, int64_t ldx, int64_t rows, int cols, int cols_padded, void* y,
+                      mapa_stream_t stream);
+
 /* Deterministic synthetic weights on device: out[i] = (2*u_i - 1)*half + mid, u_i = splitmix64 stream of
  * `seed` (bit-identical to mapanything/utils/synthetic.py). */
 int mapa_fill_splitmix(float* out, int64_t n, uint64_t seed, float half, float mid, mapa_stream_t stream);

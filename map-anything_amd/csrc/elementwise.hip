@@ -323,6 +323,36 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, 
   }
 }
 
+// fp32 rows -> [hi | hi | lo] bf16 column blocks of width cp (zero-padded past cols), hi = bf16(x),
+// lo = bf16(x - hi): with weights packed [hi | lo | hi] one bf16 GEMM over K = 3*cp accumulates
+// x_hi*w_hi + x_hi*w_lo + x_lo*w_hi (the split-precision form of an fp32 product, ~2^-16 relative).
+__global__ void split_bf16x3_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int cols, int cp,
+                                    bf16_t* __restrict__ y) {
+  const int g4 = cp / 4;
+  const int64_t total = rows * g4;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = e / g4;
+    const int c = (int)(e - r * g4) * 4;
+    const float4 v = c < cols ? *reinterpret_cast<const float4*>(x + r * ldx + c) : float4{0.f, 0.f, 0.f, 0.f};
+    const float f[4] = {v.x, v.y, v.z, v.w};
+    bf16_t hi[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      hi[j] = f32_to_bf16(f[j]);
+      lo[j] = f32_to_bf16(f[j] - bf16_to_f32(hi[j]));
+    }
+    uint2 h, l;
+    h.x = (uint32_t)hi[0] | ((uint32_t)hi[1] << 16);
+    h.y = (uint32_t)hi[2] | ((uint32_t)hi[3] << 16);
+    l.x = (uint32_t)lo[0] | ((uint32_t)lo[1] << 16);
+    l.y = (uint32_t)lo[2] | ((uint32_t)lo[3] << 16);
+    bf16_t* o = y + r * 3 * cp + c;
+    *reinterpret_cast<uint2*>(o) = h;
+    *reinterpret_cast<uint2*>(o + cp) = h;
+    *reinterpret_cast<uint2*>(o + 2 * cp) = l;
+  }
+}
+
 __global__ void fill_splitmix_kernel(float* __restrict__ out, int64_t n, uint64_t seed, float half, float mid) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     uint64_t x = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
@@ -472,6 +502,17 @@ extern "C" int mapa_convert_rows(const float* src, int64_t lds, int rows, int co
   hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(TPB), 0, stream, src, lds, rows,
                      cols, dst, dst_dtype == MAPA_BF16 ? 1 : 0, ldd);
   MAPA_CHECK_LAUNCH("mapa_convert_rows");
+  return 0;
+}
+
+extern "C" int mapa_split_bf16x3(const float* x, int64_t ldx, int64_t rows, int cols, int cols_padded, void* y,
+                                 hipStream_t stream) {
+  MAPA_CHECK_ARG(x && y && rows > 0 && cols > 0 && cols % 4 == 0 && cols_padded % 8 == 0 && cols_padded >= cols &&
+                     ldx >= cols && ldx % 4 == 0,
+                 "mapa_split_bf16x3: bad args (cols %% 4, cols_padded %% 8, ldx %% 4)");
+  hipLaunchKernelGGL(split_bf16x3_kernel, dim3(grid_for(rows * (cols_padded / 4))), dim3(TPB), 0, stream, x, ldx,
+                     rows, cols, cols_padded, (bf16_t*)y);
+  MAPA_CHECK_LAUNCH("mapa_split_bf16x3");
   return 0;
 }
 

@@ -28,7 +28,7 @@ EXPORTED = (
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
-    "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
+    "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
     "mapa_normalize_image",
 )
 
@@ -108,6 +108,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_pose_inputs.argtypes = [vp, vp, vp, i, vp, vp, vp, vp]
     L.mapa_add_view_vectors.argtypes = [vp, i, i, i, vp, vp, i, vp]
     L.mapa_add_f32.argtypes = [vp, vp, i64, vp]
+    L.mapa_split_bf16x3.argtypes = [vp, i64, i64, i, i, vp, vp]
     L.mapa_view_rays.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
     L.mapa_apply_mask.argtypes = [vp, vp, vp, vp, i64, vp]
     L.mapa_confidence_mask.argtypes = [vp, vp, vp, i, i64, f, vp]
@@ -350,6 +351,14 @@ def dense_head_out(hidden, n, HW, w6, b6, pose_out, scale, batch, pts3d, pts3d_c
 def convert_rows(src, lds, rows, cols, dst, ldd):
     check(lib().mapa_convert_rows(ptr(src), lds, rows, cols, ptr(dst), dt_code(dst.dtype), ldd, stream()),
           "mapa_convert_rows")
+
+
+def split_bf16x3(x, rows, cols, cols_padded, y, ldx=None):
+    """x fp32 [rows][cols] -> y bf16 [rows][3*cols_padded] = [hi | hi | lo] (mapa.h mapa_split_bf16x3)."""
+    if x.dtype != torch.float32 or y.dtype != torch.bfloat16 or y.numel() < rows * 3 * cols_padded:
+        raise AssertionError("split_bf16x3: fp32 input, bf16 output of rows x 3*cols_padded")
+    check(lib().mapa_split_bf16x3(ptr(x), cols if ldx is None else ldx, rows, cols, cols_padded, ptr(y), stream()),
+          "mapa_split_bf16x3")
 
 
 def fill_splitmix(out, seed, half, mid):

@@ -177,22 +177,37 @@ class PackedWeights:
         return self.sd[name]
 
     def geometric(self, sd: Dict[str, object]) -> Dict[str, object]:
-        """fp32 kernel-layout weights of the dense (ray, depth) and global (depth-scale, camera) encoders, packed on
-        first use (the reference runs them with autocast disabled, model.py:1377)."""
+        """Kernel-layout weights of the dense (ray, depth) and global (depth-scale, camera) encoders, packed on
+        first use.  The reference runs them with autocast disabled (model.py:1377): fp32 mode keeps fp32 GEMMs; bf16
+        mode runs the dense encoders' convs / linears in split precision (split_bf16x3: weights [hi | lo | hi] per
+        tap against activations [hi | hi | lo], ~2^-16 relative, on the bf16 MFMA pipe)."""
         if getattr(self, "_geo", None) is not None:
             return self._geo
         dev = self.device
+        split = self.lp == torch.bfloat16
 
         def t(name):
             return torch.from_numpy(np.ascontiguousarray(_np(sd[name]))).to(dev)
 
+        def pack(w):  # [out][taps][cin] fp32 -> fp32 [out][taps*cin] or bf16 [out][taps*3*cinp] (hi | lo | hi)
+            o, taps, cin = w.shape
+            if not split:
+                return torch.from_numpy(np.ascontiguousarray(w.reshape(o, -1))).to(dev)
+            wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+            hi = wt.to(torch.bfloat16)
+            lo = (wt - hi.float()).to(torch.bfloat16)
+            cp = _ceil8(cin)
+            out = torch.zeros(o, taps, 3, cp, dtype=torch.bfloat16, device=dev)
+            out[:, :, 0, :cin], out[:, :, 1, :cin], out[:, :, 2, :cin] = hi, lo, hi
+            return out.reshape(o, -1)
+
         def c3(name):
             w = _np(sd[f"{name}.weight"])
-            return torch.from_numpy(np.ascontiguousarray(w.transpose(0, 2, 3, 1).reshape(w.shape[0], -1))).to(dev)
+            return pack(w.transpose(0, 2, 3, 1).reshape(w.shape[0], 9, w.shape[1]))
 
         def l1(name):
             w = _np(sd[f"{name}.weight"])
-            return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev)
+            return pack(w.reshape(w.shape[0], 1, -1))
 
         geo = {}
         for enc in ("ray_dirs_encoder", "depth_encoder"):
@@ -203,6 +218,7 @@ class PackedWeights:
                 n = f"{enc}.encoder.{i}"
                 d["blocks"].append(dict(c1=c3(f"{n}.conv1"), b1=t(f"{n}.conv1.bias"), c2=c3(f"{n}.conv2"),
                                         b2=t(f"{n}.conv2.bias"), sc=l1(f"{n}.shortcut"), sc_b=t(f"{n}.shortcut.bias")))
+            d["split"] = split
             geo[enc] = d
         for enc in ("depth_scale_encoder", "cam_rot_encoder", "cam_trans_encoder", "cam_trans_scale_encoder"):
             names = ("encoder.0.0.0.0", "encoder.0.0.1", "encoder.0.1", "encoder.1")
@@ -230,6 +246,10 @@ class PackedWeights:
                 out = torch.cat([pe[0, :1], patch], 0)
             self.pos_cache[key] = out.contiguous().to(self.device)
         return self.pos_cache[key]
+
+
+def _ceil8(c: int) -> int:
+    return (c + 7) // 8 * 8
 
 
 class MapaEngine:
@@ -404,28 +424,45 @@ class MapaEngine:
         hp, wp = H // PATCH, W // PATCH
         M = n * hp * wp
         cin = C * PATCH * PATCH
+
+        def operand(x, c):  # GEMM A operand and its per-tap width: fp32 as is, or [hi | hi | lo] bf16
+            if not g["split"]:
+                return x, c
+            cp = _ceil8(c)
+            y = self._empty(M, 3 * cp, dtype=torch.bfloat16)
+            nat.split_bf16x3(x, M, c, cp, y)
+            return y, 3 * cp
+
         u = self._empty(M, cin, dtype=f32)
         nat.pixel_unshuffle(data, n, H, W, C, PATCH, u, view_div=view_div)
         c0 = g["conv_in"].shape[0]
         x = self._empty(M, c0, dtype=f32)
-        nat.gemm(u, g["conv_in"], M, c0, 9 * cin, bias=g["conv_in_b"], out_f32=x, conv=(cin, hp, wp, hp, wp, 1))
+        a, k = operand(u, cin)
         del u
+        nat.gemm(a, g["conv_in"], M, c0, 9 * k, bias=g["conv_in_b"], out_f32=x, conv=(k, hp, wp, hp, wp, 1))
+        del a
         cin = c0
         for blk in g["blocks"]:
             co = blk["c1"].shape[0]
+            a, k = operand(x, cin)
             idt = self._empty(M, co, dtype=f32)
-            nat.gemm(x, blk["sc"], M, co, cin, bias=blk["sc_b"], out_f32=idt)
+            nat.gemm(a, blk["sc"], M, co, k, bias=blk["sc_b"], out_f32=idt)
             o = self._empty(M, co, dtype=f32)
-            nat.gemm(x, blk["c1"], M, co, 9 * cin, bias=blk["b1"], act=nat.ACT_GELU, out_f32=o,
-                     conv=(cin, hp, wp, hp, wp, 1))
+            nat.gemm(a, blk["c1"], M, co, 9 * k, bias=blk["b1"], act=nat.ACT_GELU, out_f32=o,
+                     conv=(k, hp, wp, hp, wp, 1))
+            del a
+            a, k = operand(o, co)
+            del o
             x = self._empty(M, co, dtype=f32)
-            nat.gemm(o, blk["c2"], M, co, 9 * co, bias=blk["b2"], resid1=idt, act=nat.ACT_GELU_POST, out_f32=x,
-                     conv=(co, hp, wp, hp, wp, 1))
-            del idt, o
+            nat.gemm(a, blk["c2"], M, co, 9 * k, bias=blk["b2"], resid1=idt, act=nat.ACT_GELU_POST, out_f32=x,
+                     conv=(k, hp, wp, hp, wp, 1))
+            del idt, a
             cin = co
         y = self._empty(M, ENC_DIM, dtype=f32)
-        nat.gemm(x, g["out"], M, ENC_DIM, cin, bias=g["out_b"], out_f32=y)
+        a, k = operand(x, cin)
         del x
+        nat.gemm(a, g["out"], M, ENC_DIM, k, bias=g["out_b"], out_f32=y)
+        del a
         f = self._empty(M, ENC_DIM, dtype=f32)
         nat.layernorm(y, M, ENC_DIM, g["nw"], g["nb"], eps=LN_EPS, y_f32=f)
         return f

@@ -430,3 +430,38 @@ def test_attention_partials_merge_to_full(nat, dtype, tol):
     nat.attention(q, kv, kv[:, C:], ob, seq_kv=233, kv_segments=segs_b, lse=lb, **st)
     nat.attn_merge(oa, la, ob, lb, oa, Sq, H, C)
     assert rel_l2(oa.float().cpu(), full.float().cpu()) < tol
+
+
+# ------------------------------------------------------------------------------------- split-precision operands
+@pytest.mark.parametrize("rows,cols,cp", [(37, 588, 592), (1369, 196, 200), (10, 1024, 1024)])
+def test_split_bf16x3_is_bit_exact(nat, rows, cols, cp):
+    """[hi | hi | lo] blocks: hi = bf16(x) (RNE), lo = bf16(x - hi), zero padding — bit-exact vs torch."""
+    x = _rand(rows, cols, scale=3.0, seed=11)
+    y = torch.full((rows, 3 * cp), 7.0, dtype=torch.bfloat16, device="cuda")
+    nat.split_bf16x3(x, rows, cols, cp, y)
+    hi = x.to(torch.bfloat16)
+    lo = (x - hi.float()).to(torch.bfloat16)
+    ref = torch.zeros(rows, 3, cp, dtype=torch.bfloat16, device="cuda")
+    ref[:, 0, :cols], ref[:, 1, :cols], ref[:, 2, :cols] = hi, hi, lo
+    assert torch.equal(y.view(torch.int16), ref.reshape(rows, -1).view(torch.int16))
+
+
+def test_split_precision_conv_matches_fp32(nat):
+    """A 3x3 conv run as one bf16 implicit-GEMM over [hi | hi | lo] activations and [hi | lo | hi] weights (the
+    geometric encoders' bf16-mode path) stays within ~1e-5 of the fp32 conv (plain bf16: ~3e-3)."""
+    n, h, w, C, Co = 2, 37, 37, 588, 768
+    x = _rand(n, C, h, w, seed=12)
+    wt = _rand(Co, C, 3, 3, scale=C ** -0.5 / 3, seed=13)
+    ref = F.conv2d(x.cpu().double(), wt.cpu().double(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    M, cp = n * h * w, 592
+    xr = x.permute(0, 2, 3, 1).reshape(M, C).contiguous()
+    a = torch.empty(M, 3 * cp, dtype=torch.bfloat16, device="cuda")
+    nat.split_bf16x3(xr, M, C, cp, a)
+    wk = wt.permute(0, 2, 3, 1).reshape(Co, 9, C)
+    whi = wk.to(torch.bfloat16)
+    wlo = (wk - whi.float()).to(torch.bfloat16)
+    wp = torch.zeros(Co, 9, 3, cp, dtype=torch.bfloat16, device="cuda")
+    wp[:, :, 0, :C], wp[:, :, 1, :C], wp[:, :, 2, :C] = whi, wlo, whi
+    out = torch.empty(M, Co, device="cuda")
+    nat.gemm(a, wp.reshape(Co, -1), M, Co, 9 * 3 * cp, out_f32=out, conv=(3 * cp, h, w, h, w, 1))
+    assert rel_l2(out.cpu(), ref) < 2e-5

@@ -130,6 +130,32 @@ def test_fp32_geometric_fused_tap(model, golden):
     assert rel_l2(fused[:, ::tap_step, ::tap_step], g["tap_fused_nhwc"]) < 1e-4
 
 
+def test_bf16_mode_geometric_encoders_are_split_precision(model):
+    """bf16 mode runs the (autocast-disabled, model.py:1377) ray / depth dense encoders as split-precision bf16
+    GEMMs: their features stay within 1e-4 of the exact-fp32 engine's (plain bf16 operands would be ~3e-3)."""
+    from mapanything.utils.inference import preprocess_input_views_for_inference, validate_input_views_for_inference
+
+    case = CASES["mixed_224"]
+    views = validate_input_views_for_inference(_views(case))
+    metric = model._metric_flags(views)
+    for v in views:
+        for k in list(v):
+            if isinstance(v[k], torch.Tensor):
+                v[k] = v[k].cuda()
+    views = preprocess_input_views_for_inference(views)
+    geo = model._geo_inputs(views, None, metric)
+    V, H, W = case["views"], case["h"], case["w"]
+    feats = {}
+    for prec in ("fp32", "bf16"):
+        eng = model.engine(prec)
+        g = eng.w.geometric(eng._sd)
+        assert g["ray_dirs_encoder"]["split"] == (prec == "bf16")
+        feats[prec] = (eng._dense_rep(geo.rays.contiguous(), V, H, W, 3, g["ray_dirs_encoder"]).cpu(),
+                       eng._dense_rep(geo.depth.contiguous(), V, H, W, 1, g["depth_encoder"]).cpu())
+    for a, b in zip(feats["bf16"], feats["fp32"]):
+        assert rel_l2(a, b) < 1e-4
+
+
 def test_ignore_all_geometric_inputs_is_image_only(model):
     case = CASES["mixed_224"]
     img_only = [{"img": v["img"], "data_norm_type": ["dinov2"]} for v in _views(case)]
