@@ -77,7 +77,7 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
 /* Tuning / test hook: force one kernel variant for every later mapa_gemm call (0 = automatic per-shape choice,
  * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
  * 2560..2574 = 256-row tiles, 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without
- * one the automatic choice runs). */
+ * one the automatic choice runs), 2590/2591 = four-wave 256x256 / 192x256 tiles. */
 int mapa_gemm_set_variant(int variant);
 
 /* ---------------------------------------------------------------------------------------------------------

@@ -363,6 +363,9 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
   if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
+  } else if (d->dtype == MAPA_BF16 && (variant == 2590 || variant == 2591) &&
+             launch_gemm_w4(a, conv, variant - 2590, stream)) {
+    // launched
   } else if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2574 &&
              launch_gemm_big(a, conv, variant - 2560, stream)) {
     // launched
@@ -379,7 +382,8 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582),
+                     (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582) ||
+                     variant == 2590 || variant == 2591,
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;

@@ -154,6 +154,9 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
 
+// Four-wave 256-column bf16 kernel (gemm_w4.hip): variant 0 = 256x256 tile, 1 = 192x256 tile; 1 workgroup/CU.
+bool launch_gemm_w4(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
+
 // Stream-K bf16 kernel (gemm_big.hip): variant 0 = 256x128 tiles, 2 workgroups per CU; 1 = 256x256, 1 per CU.
 // streamk_workspace_bytes: bytes the launch needs (ticket words + partial-sum slabs); launch returns false if
 // the workspace is missing or too small.
