@@ -3,6 +3,7 @@
   python bench.py                        # N=1: configs[1] = 8 views 518x518 bf16 image-only infer on 1 GPU
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
       bench.py --gpus N                  # 8 views per GPU (weak scaling), global-attention K/V all-gathered
+  ... bench.py --gpus N --total-views 100  # configs[2]: a fixed 100-view job split over the N ranks (strong)
 
 One step = one full `MapAnything.infer(views)` (validation, forward, post-processing with edge masks) over
 synthetic images with inputs already resident in HBM.  On one GPU the engine's launches are replayed from a captured
@@ -41,6 +42,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--views-per-gpu", type=int, default=8)
+    ap.add_argument("--total-views", type=int, default=0,
+                    help="strong scaling: this many views split over the ranks (configs[2]: 100), else views-per-gpu")
     ap.add_argument("--res", type=int, default=518)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -72,7 +75,7 @@ def main():
     from mapanything.utils import synthetic
     from tests_helpers import released_config
 
-    V_total = args.views_per_gpu * world
+    V_total = args.total_views or args.views_per_gpu * world
     H = W = args.res
     model = MapAnything(**released_config(), precision=args.precision).load_synthetic_weights().to(dev).eval()
     if world > 1:
@@ -172,15 +175,20 @@ def main():
         line = {
             "metric": "views/sec + ms/infer, N-view 518x518 bf16 at 1/2/4/8 MI355X",
             "value": value, "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if args.total_views else "weak",
+            "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
             "config": {"workload": f"{V_total}-view {H}x{W} " + (
                            "images+intrinsics+sparse depth (cfg4 inputs)" if args.geometric else
                            "image-only MapAnything.infer (configs[1] at N=1)"),
-                       "views": V_total, "views_per_gpu": args.views_per_gpu, "height": H, "width": W,
+                       "views": V_total, "views_per_gpu": V_total / world, "height": H, "width": W,
                        "batch_per_view": 1,
                        "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else "single"},
+            # algorithmic TFLOP/s of the whole job (global attention grows as (V*1369)^2: per-view work rises with
+            # the total view count, so weak-scaling views/s alone understates the per-GPU throughput at N > 1)
             "tflops_effective": (gf_view * value) if gf_view else None,
+            "tflops_effective_per_gpu": (gf_view * value / world) if gf_view else None,
+            "tflop_per_view": gf_view,
             "roofline": roofline,
             "cross_view_attention": xattn,
             "cpu_baseline": cpu,
