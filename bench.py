@@ -180,7 +180,8 @@ def main():
             "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
             "config": {"workload": f"{V_total}-view {H}x{W} " + (
                            "images+intrinsics+sparse depth (cfg4 inputs)" if args.geometric else
-                           "image-only MapAnything.infer (configs[1] at N=1)"),
+                           ("image-only MapAnything.infer (fixed job, strong scaling)" if args.total_views else
+                            "image-only MapAnything.infer (configs[1] at N=1)")),
                        "views": V_total, "views_per_gpu": V_total / world, "height": H, "width": W,
                        "batch_per_view": 1,
                        "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else "single"},

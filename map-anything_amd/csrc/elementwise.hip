@@ -118,12 +118,12 @@ template <typename TI, typename TO>
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                    int OW, TO* __restrict__ out) {
   const int c8 = C / 8;
-  const int total = n * OH * OW * c8;
+  const int64_t total = (int64_t)n * OH * OW * c8;  // > 2^31 past ~500 views at 518x518 x 128 channels
   const float sh = OHf > 1 ? (float)(IH - 1) / (float)(OHf - 1) : 0.f;
   const float sw = OWf > 1 ? (float)(IW - 1) / (float)(OWf - 1) : 0.f;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
-    const int c = (e % c8) * 8;
-    int r = e / c8;
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % c8) * 8;
+    int r = (int)(e / c8);
     const int ox = r % OW;
     r /= OW;
     const int oy = r % OH;
