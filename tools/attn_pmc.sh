@@ -1,12 +1,15 @@
 # PMC passes over the global-attention kernel (one counter set per rocprofv3 run)
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/apmc
+# ATTN_SHAPE="B H S reps" (default: the 8-view global layer), ATTN_OUT: output directory under gpurun_out/
+SHAPE=${ATTN_SHAPE:-"1 12 10953 5"}
+OUT=${ATTN_OUT:-gpurun_out/apmc}
+mkdir -p $OUT
 i=0
 for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY" \
            "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS" \
            "SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM SQ_CYCLES"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $set -d gpurun_out/apmc/p$i -o run --output-format csv -- python tools/attn_one.py 1 12 10953 5 > gpurun_out/apmc/p$i.log 2>&1 || { tail -5 gpurun_out/apmc/p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $set -d $OUT/p$i -o run --output-format csv -- python tools/attn_one.py $SHAPE > $OUT/p$i.log 2>&1 || { tail -5 $OUT/p$i.log; exit 1; }
 done
-find gpurun_out/apmc -name "*counter_collection*"
+find $OUT -name "*counter_collection*"
