@@ -56,7 +56,12 @@ def main():
                     help="per-kernel-group MFMA busy fraction + clock from a rocprofv3 SQ pass (tools/gpu_pmc.sh)")
     ap.add_argument("--attn-pmc-json", default=os.path.join(REPO, "profiles", "r1", "attn_global_pmc.json"),
                     help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh)")
+    ap.add_argument("--lib", default=None, help="A/B only: load this libmapa.so build (tools/ab_build.sh)")
     args = ap.parse_args()
+    if args.lib:
+        from mapanything import _native
+
+        _native.load_library(args.lib)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

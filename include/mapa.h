@@ -187,11 +187,17 @@ int mapa_dense_adaptor(const float* raw, int n, int64_t HW, float* value, float*
                        mapa_stream_t stream);
 
 /* infer() post-processing (inference.py:407-480): mask_out = mask_in & ~(depth_edge & normal_edge) per view
- * (geometry.py:1788-1853, 2102-2145, 2200-2258).  pts3d/pts3d_cam [n][H][W][3] f32 (depth_z = pts3d_cam z),
- * masks u8 [n][H][W].  work: n*H*W*17 bytes of scratch when use_edges. */
+ * (geometry.py:1788-1853 points_to_normals, 2102-2145 depth_edge, 2200-2258 normals_edge), bit-exact with the
+ * reference's numpy.  pts3d/pts3d_cam [n][H][W][3] f32 (depth_z = pts3d_cam z), masks u8 [n][H][W].
+ * normal_cos_thr: normals_edge's angle threshold as the float32 dot-product boundary (a window entry is an edge
+ * iff n_c . n_w < normal_cos_thr), from mapa_normal_cos_threshold(edge_normal_threshold) or a host arccos of the
+ * caller's choice.  work: n*H*W*17 bytes of scratch when use_edges. */
 int mapa_postprocess_mask(const float* pts3d, const float* pts3d_cam, const uint8_t* mask_in, uint8_t* mask_out,
-                          int n, int H, int W, float normal_tol_deg, float depth_rtol, int use_edges, void* work,
+                          int n, int H, int W, float normal_cos_thr, float depth_rtol, int use_edges, void* work,
                           mapa_stream_t stream);
+/* Host-only helper: the float32 boundary c with (float32 arccos(d) > deg2rad(tol_deg)) <=> d < c over d in
+ * [-1, 1] (arccos in double rounded to float32); -1 if no angle exceeds tol, 2 if every angle (also 0) does. */
+float mapa_normal_cos_threshold(double tol_deg);
 
 /* apply_confidence_mask (inference.py:455-470): per view thr = quantile(conf, q) (torch.quantile's linear
  * interpolation), mask_out = mask_in & (conf > thr).  conf [n][HW] f32, masks u8 [n][HW] (may alias). */

@@ -4,11 +4,15 @@
 // image de-normalisation (image.py:93-131).
 //
 // The mask is three 3x3-stencil passes over each view (NHWC, one thread per pixel):
-//   K1 normals + normal validity (points_to_normals with mask), K2 per-pixel max angle to the 3x3 window
-//   (NaN-propagating like numpy's .max, edge-replicated padding like np.pad mode="edge"), K3 3x3 nan-max
-//   pool of the angles (max_pool_2d uses np.nanmax with NaN padding) + depth-edge + final combine + zeroing
-//   of the dense geometry outputs.  Float operations follow numpy's order so equal inputs give equal bits.
+//   K1 normals + normal validity (points_to_normals with mask), K2 per-pixel window state of the normal angles
+//   (NaN-propagating like numpy's .max, edge-replicated padding like np.pad mode="edge", transposed mask
+//   window), K3 3x3 nan-max pool of the angles (max_pool_2d uses np.nanmax with NaN padding) + depth edge +
+//   final combine.  Float operations follow numpy's order (no fma contraction, -ffp-contract=off) so equal
+//   inputs give equal bits; the angle threshold is applied on the dot product (arccos is monotone).
 #include "mapa_common.h"
+
+#include <math.h>
+#include <string.h>
 
 namespace {
 
@@ -61,15 +65,16 @@ __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __r
     const bool mu = ldm(M, H, W, y - 1, x), ml = ldm(M, H, W, y, x - 1);
     const bool md = ldm(M, H, W, y + 1, x), mr = ldm(M, H, W, y, x + 1);
     const bool valid[4] = {mu && ml && mc, ml && md && mc, md && mr && mc, mr && mu && mc};
-    float s[3] = {0.f, 0.f, 0.f};
+    // (normal * valid).sum(axis=0): numpy starts from the first slice and adds the others in order
+    float s[3];
     bool any = false;
     for (int i = 0; i < 4; ++i) {
       const float inv = norm3(nn[i]) + 1e-12f;
-      if (valid[i]) {
-        for (int k = 0; k < 3; ++k) s[k] += nn[i][k] / inv;
-        any = true;
-      } else {
-        for (int k = 0; k < 3; ++k) s[k] += (nn[i][k] / inv) * 0.f;
+      const float vf = valid[i] ? 1.f : 0.f;
+      any |= valid[i];
+      for (int k = 0; k < 3; ++k) {
+        const float t = (nn[i][k] / inv) * vf;
+        s[k] = i == 0 ? t : s[k] + t;
       }
     }
     const float ns = norm3(s) + 1e-12f;
@@ -79,9 +84,16 @@ __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __r
   }
 }
 
-// K2: per-pixel window max of arccos(n_c . n_w) over the 3x3 window (edge padding), where(mask_w, angle, 0)
-__global__ void normal_angle_kernel(const float* __restrict__ nrm, const uint8_t* __restrict__ nmask, int n, int H,
-                                    int W, float* __restrict__ ang) {
+// K2: normals_edge before its max-pool.  Per pixel the reference takes A = max over the 3x3 window (edge
+// padding) of where(mask_window, arccos(n_c . n_w), 0) with NaN propagating, then compares the pooled max with
+// deg2rad(tol).  arccos is monotone, so "arccos(d) > tol" is "d < cos_thr" for the float32 boundary cos_thr the
+// host derives from the same arccos (mapa_normal_cos_threshold / the Python host); a masked-out entry is the
+// value 0 = arccos(1).  State per pixel: 2 = A is NaN (some masked-in |d| > 1 or NaN), 1 = A > tol, 0 = A <= tol.
+// The mask window is the TRANSPOSE of the normals window: sliding_window_2d(mask, axis=(-3, -2)) on the 2-D mask
+// wraps the axes to (1, 0) (geometry.py:1933, 2239-2247), so the normal at (y+dy, x+dx) is gated by the mask at
+// (y+dx, x+dy), both clamped to the image (np.pad mode="edge").
+__global__ void normal_state_kernel(const float* __restrict__ nrm, const uint8_t* __restrict__ nmask, int n, int H,
+                                    int W, float cos_thr, uint8_t* __restrict__ state) {
   const int64_t total = (int64_t)n * H * W;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int im = (int)(e / ((int64_t)H * W));
@@ -95,26 +107,29 @@ __global__ void normal_angle_kernel(const float* __restrict__ nrm, const uint8_t
       const float nc = norm3(q) + 1e-12f;
       for (int k = 0; k < 3; ++k) c[k] = q[k] / nc;
     }
-    float best = -INFINITY;
-    bool nan = false;
+    bool nan = false, edge = false;
     for (int dy = -1; dy <= 1; ++dy)
       for (int dx = -1; dx <= 1; ++dx) {
-        const int yy = min(max(y + dy, 0), H - 1), xx = min(max(x + dx, 0), W - 1);
-        const float* q = N + ((int64_t)yy * W + xx) * 3;
-        const float nq = norm3(q) + 1e-12f;
-        const float w0 = q[0] / nq, w1 = q[1] / nq, w2 = q[2] / nq;
-        float a = 0.f;
-        if (Mk[yy * W + xx]) a = acosf(c[0] * w0 + c[1] * w1 + c[2] * w2);
-        if (a != a) nan = true;
-        best = fmaxf(best, a);
+        const int ny = min(max(y + dy, 0), H - 1), nx = min(max(x + dx, 0), W - 1);
+        const int my = min(max(y + dx, 0), H - 1), mx = min(max(x + dy, 0), W - 1);
+        float d = 1.f;  // masked out: angle 0 = arccos(1)
+        if (Mk[my * W + mx]) {
+          const float* q = N + ((int64_t)ny * W + nx) * 3;
+          const float nq = norm3(q) + 1e-12f;
+          const float w0 = q[0] / nq, w1 = q[1] / nq, w2 = q[2] / nq;
+          d = c[0] * w0 + c[1] * w1 + c[2] * w2;
+          if (!(fabsf(d) <= 1.f)) nan = true;  // arccos -> NaN (also for NaN d)
+        }
+        edge |= d < cos_thr;
       }
-    ang[e] = nan ? __int_as_float(0x7fc00000) : best;
+    state[e] = nan ? 2 : (edge ? 1 : 0);
   }
 }
 
-// K3: nan-max pool of the angles, depth edge, final mask, zero masked geometry
-__global__ void mask_combine_kernel(const float* __restrict__ ang, const float* __restrict__ depth_z, int64_t dz_stride,
-                                    const uint8_t* __restrict__ m_in, int n, int H, int W, float tol_rad,
+// K3: nan-max pool of the angles (max_pool_2d pads with NaN and takes np.nanmax: the pooled max exceeds tol iff
+// some in-image, non-NaN neighbour does), depth edge, final mask
+__global__ void mask_combine_kernel(const uint8_t* __restrict__ state, const float* __restrict__ depth_z,
+                                    int64_t dz_stride, const uint8_t* __restrict__ m_in, int n, int H, int W,
                                     float rtol, int use_edges, uint8_t* __restrict__ m_out) {
   const int64_t total = (int64_t)n * H * W;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -124,24 +139,22 @@ __global__ void mask_combine_kernel(const float* __restrict__ ang, const float* 
       const int im = (int)(e / ((int64_t)H * W));
       const int rem = (int)(e - (int64_t)im * H * W);
       const int y = rem / W, x = rem - y * W;
-      const float* A = ang + (int64_t)im * H * W;
+      const uint8_t* S = state + (int64_t)im * H * W;
       const uint8_t* M = m_in + (int64_t)im * H * W;
       const float* D = depth_z + (int64_t)im * H * W * dz_stride;
-      float amax = -INFINITY, dmax = -INFINITY, ndmax = -INFINITY;
-      bool anyA = false;
+      float dmax = -INFINITY, ndmax = -INFINITY;
+      bool nedge = false;
       for (int dy = -1; dy <= 1; ++dy)
         for (int dx = -1; dx <= 1; ++dx) {
           const int yy = y + dy, xx = x + dx;
           if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;  // NaN padding: ignored by nanmax
-          const float a = A[yy * W + xx];
-          if (a == a) { amax = fmaxf(amax, a); anyA = true; }
           const int64_t k = (int64_t)yy * W + xx;
+          nedge |= S[k] == 1;
           const float d = M[k] ? D[k * dz_stride] : -INFINITY;
           const float nd = M[k] ? -D[k * dz_stride] : -INFINITY;
           if (d == d) dmax = fmaxf(dmax, d);
           if (nd == nd) ndmax = fmaxf(ndmax, nd);
         }
-      const bool nedge = anyA && (amax > tol_rad);
       const float diff = dmax + ndmax;
       const float dc = D[(int64_t)rem * dz_stride];
       const bool dedge = (diff / dc) > rtol;
@@ -304,26 +317,54 @@ extern "C" int mapa_apply_mask(float* pts3d, float* pts3d_cam, float* depth_alon
 }
 
 // mask_in: non-ambiguous (& confidence) mask u8 [n][H][W]; pts3d [n][H][W][3]; depth_z = pts3d_cam (z at +2,
-// stride 3); work = scratch of n*H*W*(3 floats + 1 float + 1 byte) bytes is carved from `work`.
+// stride 3); scratch carved from `work`: normals (12 B/pixel), normal mask and edge state (1 B/pixel each).
 extern "C" int mapa_postprocess_mask(const float* pts3d, const float* pts3d_cam, const uint8_t* mask_in,
-                                     uint8_t* mask_out, int n, int H, int W, float normal_tol_deg, float depth_rtol,
+                                     uint8_t* mask_out, int n, int H, int W, float normal_cos_thr, float depth_rtol,
                                      int use_edges, void* work, hipStream_t stream) {
   MAPA_CHECK_ARG(pts3d && pts3d_cam && mask_in && mask_out && n > 0 && H > 0 && W > 0,
                  "mapa_postprocess_mask: bad args");
   MAPA_CHECK_ARG(!use_edges || work, "mapa_postprocess_mask: edges need a work buffer");
   const int64_t P = (int64_t)n * H * W;
   float* nrm = reinterpret_cast<float*>(work);
-  float* ang = nrm + P * 3;
-  uint8_t* nmask = reinterpret_cast<uint8_t*>(ang + P);
+  uint8_t* nmask = reinterpret_cast<uint8_t*>(nrm + P * 3);
+  uint8_t* state = nmask + P;
   if (use_edges) {
     hipLaunchKernelGGL(normals_kernel, dim3(grid_for(P)), dim3(256), 0, stream, pts3d, mask_in, n, H, W, nrm, nmask);
-    hipLaunchKernelGGL(normal_angle_kernel, dim3(grid_for(P)), dim3(256), 0, stream, nrm, nmask, n, H, W, ang);
+    hipLaunchKernelGGL(normal_state_kernel, dim3(grid_for(P)), dim3(256), 0, stream, nrm, nmask, n, H, W,
+                       normal_cos_thr, state);
   }
-  const float tol = normal_tol_deg * 0.017453292519943295f;
-  hipLaunchKernelGGL(mask_combine_kernel, dim3(grid_for(P)), dim3(256), 0, stream, ang, pts3d_cam + 2, (int64_t)3,
-                     mask_in, n, H, W, tol, depth_rtol, use_edges, mask_out);
+  hipLaunchKernelGGL(mask_combine_kernel, dim3(grid_for(P)), dim3(256), 0, stream, state, pts3d_cam + 2, (int64_t)3,
+                     mask_in, n, H, W, depth_rtol, use_edges, mask_out);
   MAPA_CHECK_LAUNCH("mapa_postprocess_mask");
   return 0;
+}
+
+// Host: the float32 boundary of normals_edge's "arccos(d) > deg2rad(tol)" (numpy compares the float32 arccos with
+// the float64 threshold): the smallest float32 c with arccos(d) > tol <=> d < c for every float32 d in [-1, 1].
+// arccos is taken in double and rounded to float32 (numpy's float32 arccos is within an ulp of that; near any
+// threshold adjacent float32 inputs are ~90 ulps of angle apart).  Bisection over the ordered float32 bit patterns.
+static inline int32_t f32_order(float f) {
+  int32_t i;
+  memcpy(&i, &f, 4);
+  return i < 0 ? (int32_t)(0x80000000u - (uint32_t)i) : i;
+}
+static inline float f32_unorder(int32_t k) {
+  const int32_t i = k < 0 ? (int32_t)(0x80000000u - (uint32_t)k) : k;
+  float f;
+  memcpy(&f, &i, 4);
+  return f;
+}
+extern "C" float mapa_normal_cos_threshold(double tol_deg) {
+  const double tol = tol_deg * (3.141592653589793 / 180.0);
+  auto is_edge = [&](float d) { return (double)(float)acos((double)d) > tol; };
+  if (!is_edge(-1.f)) return -1.f;                      // nothing exceeds tol
+  if (is_edge(1.f)) return 2.f;                         // everything (also the masked-out 0) exceeds it
+  int32_t lo = f32_order(-1.f), hi = f32_order(1.f);    // is_edge(lo) true, is_edge(hi) false
+  while (hi - lo > 1) {
+    const int32_t mid = lo + (hi - lo) / 2;
+    if (is_edge(f32_unorder(mid))) lo = mid; else hi = mid;
+  }
+  return f32_unorder(hi);
 }
 
 extern "C" int mapa_recover_intrinsics(const float* rays, int n, int H, int W, float* K, hipStream_t stream) {

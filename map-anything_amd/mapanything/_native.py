@@ -29,7 +29,7 @@ EXPORTED = (
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
-    "mapa_normalize_image",
+    "mapa_normalize_image", "mapa_normal_cos_threshold",
 )
 
 
@@ -73,7 +73,7 @@ def load_library(path: Optional[str] = None):
     global _lib
     if _lib is not None:
         return _lib
-    p = path or os.environ.get("MAPA_LIB_PATH") or _LIB_PATH  # MAPA_LIB_PATH: A/B builds in tools/
+    p = path or _LIB_PATH
     if not os.path.exists(p):
         raise NativeError(f"libmapa.so not found at {p}: build it with `make -C map-anything_amd/csrc` "
                           f"(or __graft_entry__.build()); there is no CPU fallback")
@@ -101,6 +101,8 @@ def load_library(path: Optional[str] = None):
     L.mapa_convert_rows.argtypes = [vp, i64, i, i, vp, i, i64, vp]
     L.mapa_fill_splitmix.argtypes = [vp, i64, u64, f, f, vp]
     L.mapa_postprocess_mask.argtypes = [vp, vp, vp, vp, i, i, i, f, f, i, vp, vp]
+    L.mapa_normal_cos_threshold.argtypes = [ctypes.c_double]
+    L.mapa_normal_cos_threshold.restype = f
     L.mapa_recover_intrinsics.argtypes = [vp, i, i, i, vp, vp]
     L.mapa_denorm_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
     L.mapa_pixel_unshuffle.argtypes = [vp, i, i, i, i, i, vp, i, vp, i, i64, vp]
@@ -365,10 +367,15 @@ def fill_splitmix(out, seed, half, mid):
     check(lib().mapa_fill_splitmix(ptr(out), out.numel(), seed, half, mid, stream()), "mapa_fill_splitmix")
 
 
-def postprocess_mask(pts3d, pts3d_cam, mask_in, mask_out, n, H, W, normal_tol_deg, depth_rtol, use_edges, work):
+def postprocess_mask(pts3d, pts3d_cam, mask_in, mask_out, n, H, W, normal_cos_thr, depth_rtol, use_edges, work):
     check(lib().mapa_postprocess_mask(ptr(pts3d), ptr(pts3d_cam), ptr(mask_in), ptr(mask_out), n, H, W,
-                                      normal_tol_deg, depth_rtol, int(use_edges), ptr(work), stream()),
+                                      float(normal_cos_thr), depth_rtol, int(use_edges), ptr(work), stream()),
           "mapa_postprocess_mask")
+
+
+def normal_cos_threshold(tol_deg: float) -> float:
+    """The library's host-side boundary (double arccos rounded to float32), include/mapa.h."""
+    return float(load_library().mapa_normal_cos_threshold(float(tol_deg)))
 
 
 def recover_intrinsics(rays, n, H, W, K):

@@ -3,8 +3,10 @@ output post-processing (inference.py:314-506) with the per-pixel work in HIP ker
 
 from __future__ import annotations
 
+import functools
 from typing import Any, Dict, List
 
+import numpy as np
 import torch
 
 from .. import _native as nat
@@ -124,6 +126,46 @@ def rotation_matrix_to_quaternion(m: torch.Tensor) -> torch.Tensor:
     return torch.where(out[..., 3:4] < 0, -out, out)
 
 
+@functools.lru_cache(maxsize=64)
+def normal_cos_threshold(tol_deg: float) -> float:
+    """normals_edge compares numpy's float32 arccos of each window dot product with np.deg2rad(tol) in float64
+    (geometry.py:2248-2258).  arccos is monotone, so that test is `dot < c` for one float32 boundary c: found here
+    by bisection over the ordered float32 values in [-1, 1] with numpy's own float32 arccos (the function the
+    reference calls), checked against the library's double-precision boundary and verified on the 1024 floats
+    around it.  -1: no angle exceeds tol; 2: every angle does (also the 0 of masked-out entries)."""
+    tol = np.deg2rad(tol_deg)
+
+    def edge(d):
+        return bool(np.float64(np.arccos(np.float32(d))) > tol)
+
+    if not edge(-1.0):
+        return -1.0
+    if edge(1.0):
+        return 2.0
+    bits = lambda f: int(np.float32(f).view(np.int32))  # noqa: E731
+
+    def key(f):  # order-preserving int of a float32
+        b = bits(f)
+        return b if b >= 0 else -(b & 0x7FFFFFFF)
+
+    def unkey(k):
+        b = k if k >= 0 else (-k) | -0x80000000
+        return float(np.int32(b).view(np.float32))
+
+    lo, hi = key(-1.0), key(1.0)
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if edge(unkey(mid)):
+            lo = mid
+        else:
+            hi = mid
+    cs = np.array([unkey(k) for k in range(hi - 512, hi + 512)], np.float32)
+    cs = cs[(cs >= -1) & (cs <= 1)]
+    assert np.array_equal(np.arccos(cs).astype(np.float64) > tol, cs < np.float32(unkey(hi))), \
+        "numpy arccos is not monotone around the normal-edge threshold"
+    return unkey(hi)
+
+
 def postprocess_outputs(raw: Dict[str, torch.Tensor], imgs: torch.Tensor, mean: torch.Tensor, std: torch.Tensor, *,
                         apply_mask=True, mask_edges=True, edge_normal_threshold=5.0, edge_depth_threshold=0.03,
                         apply_confidence_mask=False, confidence_percentile=10) -> Dict[str, torch.Tensor]:
@@ -144,8 +186,9 @@ def postprocess_outputs(raw: Dict[str, torch.Tensor], imgs: torch.Tensor, mean: 
             m_in = m_conf
         m_out = torch.empty(V, H, W, device=imgs.device, dtype=torch.bool)  # kernels write 0/1 bytes
         work = torch.empty(V * H * W * 17, device=imgs.device, dtype=torch.uint8) if mask_edges else None
-        nat.postprocess_mask(raw["pts3d"], raw["pts3d_cam"], m_in, m_out, V, H, W, float(edge_normal_threshold),
-                             float(edge_depth_threshold), bool(mask_edges), work)
+        nat.postprocess_mask(raw["pts3d"], raw["pts3d_cam"], m_in, m_out, V, H, W,
+                             normal_cos_threshold(float(edge_normal_threshold)), float(edge_depth_threshold),
+                             bool(mask_edges), work)
         # zero the masked geometry in place (the raw tensors are this call's own outputs)
         nat.apply_mask(raw["pts3d"], raw["pts3d_cam"], raw["depth_along_ray"], m_out, V * H * W)
         out["mask"] = m_out

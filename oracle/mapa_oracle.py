@@ -16,7 +16,10 @@ arithmetic of `MapAnything.infer` (model.py:2206-2355) for the released config (
   pose / scale heads       pose_head.py:18-159, mlp_head.py:13-92
   adaptors                 adaptors.py:171-212, 237-280, 393-523, 586-732, 1012-1133, 1740-1796
   output assembly          model.py:1865-1923, 2116-2150, geometry.py:601-652, 855-907
-  postprocess (no mask)    inference.py:314-400, geometry.py:304-447, image.py:93-131
+  postprocess              inference.py:314-506, geometry.py:304-447, image.py:93-131; the apply_mask branch
+                           (edge / normal / depth / confidence masks) as numpy restatements of
+                           geometry.py:1788-1851 (points_to_normals), :2200-2259 (normals_edge), :2102-2143
+                           (depth_edge) and max_pool_2d's NaN-padded nanmax (:1976-2090)
 
 Parity pinning: this oracle is checked against fixtures produced by running the reference itself
 (tests/golden/make_golden.py -> tests/golden/golden_*.npz) on the same synthetic weights and inputs.
@@ -412,10 +415,9 @@ class MapAnythingOracle:
         return res
 
     @torch.no_grad()
-    def infer(self, views, apply_mask=False):
-        """model.py:2206-2355 (fp32, apply_mask=False path of postprocess, inference.py:314-400)."""
-        if apply_mask:
-            raise NotImplementedError("oracle covers the apply_mask=False postprocess")
+    def infer(self, views, apply_mask=False, mask_edges=True, edge_normal_threshold=5.0, edge_depth_threshold=0.03,
+              apply_confidence_mask=False, confidence_percentile=10):
+        """model.py:2206-2355 (fp32) with postprocess_model_outputs_for_inference (inference.py:314-506)."""
         pv = preprocess_views(views)
         raw = self.forward(pv)
         out = []
@@ -430,8 +432,127 @@ class MapAnythingOracle:
             P[:, :3, :3] = quat_to_rot(o["cam_quats"])
             P[:, :3, 3] = o["cam_trans"]
             o["camera_poses"] = P
+            if apply_mask:
+                m = postprocess_mask_np(o["pts3d"].numpy(), o["depth_z"][..., 0].numpy(),
+                                        o["non_ambiguous_mask"].numpy(), o["conf"],
+                                        mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
+                                        edge_depth_threshold=edge_depth_threshold,
+                                        apply_confidence_mask=apply_confidence_mask,
+                                        confidence_percentile=confidence_percentile)
+                mt = torch.from_numpy(m).unsqueeze(-1)
+                for k in ("pts3d", "pts3d_cam", "depth_along_ray", "depth_z"):
+                    o[k] = o[k] * mt
+                o["mask"] = mt
             out.append(o)
         return out
+
+
+# ------------------------------------------------------------------------------------- infer() masks (numpy)
+def _shift_zero(a, dy, dx):
+    """b[y, x] = a[y + dy, x + dx], zero (False) outside the image (the zero-padded maps of points_to_normals)."""
+    H, W = a.shape[:2]
+    b = np.zeros_like(a)
+    ys, yd = (slice(dy, H), slice(0, H - dy)) if dy >= 0 else (slice(0, H + dy), slice(-dy, H))
+    xs, xd = (slice(dx, W), slice(0, W - dx)) if dx >= 0 else (slice(0, W + dx), slice(-dx, W))
+    b[yd, xd] = a[ys, xs]
+    return b
+
+
+def _shift_edge(a, dy, dx):
+    """b[y, x] = a[clamp(y + dy), clamp(x + dx)] (np.pad mode="edge" then a window offset)."""
+    H, W = a.shape[:2]
+    yi = np.clip(np.arange(H) + dy, 0, H - 1)
+    xi = np.clip(np.arange(W) + dx, 0, W - 1)
+    return a[yi][:, xi]
+
+
+def _unit(v):
+    return v / (np.sqrt(v[..., 0] * v[..., 0] + v[..., 1] * v[..., 1] + v[..., 2] * v[..., 2])[..., None]
+                + np.float32(1e-12))
+
+
+def _cross(a, b):  # numpy's cross order: a1*b2 - a2*b1, a2*b0 - a0*b2, a0*b1 - a1*b0
+    return np.stack([a[..., 1] * b[..., 2] - a[..., 2] * b[..., 1], a[..., 2] * b[..., 0] - a[..., 0] * b[..., 2],
+                     a[..., 0] * b[..., 1] - a[..., 1] * b[..., 0]], -1)
+
+
+def points_to_normals_np(pts, mask):
+    """geometry.py:1788-1851 with a mask: (normals (H,W,3) f32, normal_mask (H,W) bool)."""
+    c = pts
+    nb = {d: _shift_zero(pts, *d) - c for d in ((-1, 0), (0, -1), (1, 0), (0, 1))}
+    mk = {d: _shift_zero(mask, *d) for d in ((-1, 0), (0, -1), (1, 0), (0, 1))}
+    up, left, down, right = nb[(-1, 0)], nb[(0, -1)], nb[(1, 0)], nb[(0, 1)]
+    mu, ml, md, mr = mk[(-1, 0)], mk[(0, -1)], mk[(1, 0)], mk[(0, 1)]
+    quads = [(_cross(up, left), mu & ml), (_cross(left, down), ml & md), (_cross(down, right), md & mr),
+             (_cross(right, up), mr & mu)]
+    acc, valid_any = None, np.zeros(mask.shape, bool)
+    for nrm, val in quads:
+        val = val & mask
+        term = _unit(nrm) * val[..., None].astype(np.float32)
+        acc = term if acc is None else acc + term
+        valid_any |= val
+    nrm = _unit(acc)
+    return np.where(valid_any[..., None], nrm, np.float32(0)).astype(np.float32), valid_any
+
+
+def _nanmax_pool3(a):
+    """max_pool_2d(a, 3, stride 1, padding 1): NaN padding, np.nanmax over rows then over columns."""
+    with np.errstate(invalid="ignore"):
+        import warnings
+
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            p = np.pad(a, 1, constant_values=np.nan)
+            r = np.nanmax(np.stack([p[0:-2], p[1:-1], p[2:]], -1), -1)
+            return np.nanmax(np.stack([r[:, 0:-2], r[:, 1:-1], r[:, 2:]], -1), -1)
+
+
+def normals_edge_np(normals, mask, tol_deg):
+    """geometry.py:2200-2259: window angles with edge padding; the mask window of a 2-D mask is the transpose
+    of the normals window (sliding_window_nd wraps axis=(-3, -2) to (1, 0) on a 2-D array, geometry.py:1933)."""
+    n = _unit(normals)
+    with np.errstate(invalid="ignore"):
+        angs = []
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                w = _shift_edge(n, dy, dx)
+                dot = n[..., 0] * w[..., 0] + n[..., 1] * w[..., 1] + n[..., 2] * w[..., 2]
+                angs.append(np.where(_shift_edge(mask, dx, dy), np.arccos(dot), np.float32(0)))
+        a = np.max(np.stack(angs, -1), -1)  # NaN propagates (np.max)
+        return _nanmax_pool3(a) > np.deg2rad(tol_deg)
+
+
+def depth_edge_np(depth, mask, rtol):
+    """geometry.py:2102-2143 with a mask (rtol only)."""
+    ninf = np.float32(-np.inf)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        diff = _nanmax_pool3(np.where(mask, depth, ninf)) + _nanmax_pool3(np.where(mask, -depth, ninf))
+        return diff / depth > rtol
+
+
+def postprocess_mask_np(pts3d, depth_z, non_ambiguous, conf, *, mask_edges=True, edge_normal_threshold=5.0,
+                        edge_depth_threshold=0.03, apply_confidence_mask=False, confidence_percentile=10):
+    """inference.py:407-480 per batch of one view: pts3d (B,H,W,3), depth_z (B,H,W) f32, non_ambiguous (B,H,W)
+    bool, conf (B,H,W) torch -> final mask (B,H,W) bool."""
+    final = np.asarray(non_ambiguous).astype(bool)
+    if apply_confidence_mask:
+        c = torch.as_tensor(conf).cpu()
+        B = c.shape[0]
+        thr = torch.quantile(c.reshape(B, -1), confidence_percentile / 100.0, dim=1).view(B, 1, 1)
+        final = final & (c > thr).numpy()
+    if mask_edges:
+        edges = []
+        for b in range(final.shape[0]):
+            m = final[b]
+            if not m.any():
+                edges.append(np.zeros_like(m))
+                continue
+            nrm, nm = points_to_normals_np(pts3d[b], m)
+            ne = normals_edge_np(nrm, nm, edge_normal_threshold)
+            de = depth_edge_np(depth_z[b], m, edge_depth_threshold)
+            edges.append(~(de & ne))
+        final = final & np.stack(edges, 0)
+    return final
 
 
 # ------------------------------------------------------------------------------------------------ geometry

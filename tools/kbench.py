@@ -9,6 +9,9 @@ import torch  # noqa: E402
 
 from mapanything import _native as nat  # noqa: E402
 
+if os.environ.get("MAPA_AB_LIB"):  # A/B builds (tools/ab_build.sh): load before any other call
+    nat.load_library(os.environ["MAPA_AB_LIB"])
+
 nat.lib()
 V, T = 8, 1369
 R, L = V * (T + 1), V * T + 1
