@@ -22,7 +22,9 @@ extern "C" {
 
 typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
 
-enum { MAPA_F32 = 0, MAPA_BF16 = 1 };
+/* MAPA_BF16X3: split-precision bf16 operand rows [hi | hi | lo] (3x the logical width; see mapa_split_bf16x3),
+ * accepted as an OUTPUT dtype by mapa_layernorm (y_lp) and mapa_bilinear_ac */
+enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2 };
 enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
 enum { MAPA_OUT_ROWMAJOR = 0, MAPA_OUT_PIXSHUF = 1 };
 enum { MAPA_ACT_NONE = 0, MAPA_ACT_GELU = 1, MAPA_ACT_RELU = 2, MAPA_ACT_GELU_POST = 3 };
@@ -37,7 +39,7 @@ int mapa_device_check(int device);
  *   v = acc + bias[n % bias_mod]; v = act(v); v *= gamma[n]; v += resid1[o] + resid2[o];
  *   (act MAPA_ACT_GELU_POST: v = gelu(acc + bias + resid1 + resid2), gamma must be NULL — ResidualBlock,
  *   dense_rep_encoder.py:44-52)
- *   out_f32[o] = v; out_lp[o] = lowp(v); out_lp_relu[o] = lowp(max(v,0))
+ *   out_f32[o] = v; out_lp[o] = lowp(v); out_lp_relu[o] = lowp(max(v,0)); out_s3 / out_s3_relu: split operand
  * Replaces nn.Linear (transformer_blocks.py:65-212, dinov2 layers/block.py:93-118, mlp_head.py, pose_head.py),
  * nn.Conv2d 1x1/3x3 (dpt.py:94-311, dpt_block.py:114-177, pose_head.py:18-48, dense_rep_encoder.py:31-287),
  * nn.ConvTranspose2d k=s (dpt.py:101-131; out_mode PIXSHUF) and the 14x14/14 patch-embed conv.
@@ -69,6 +71,13 @@ typedef struct {
    * again when each call completes.  NULL / too small -> the data-parallel schedule (same results to rounding). */
   void* workspace;
   int64_t workspace_bytes;
+  /* Split-precision operand outputs (dtype BF16 only; NULL = off): row r of out_s3 is 3*ld bf16 wide (ld = ldo, or
+   * ps_cout in PIXSHUF mode) and holds [hi | hi | lo] of the output row, hi = bf16(v), lo = bf16(v - hi) — the
+   * mapa_split_bf16x3 layout, so the next GEMM/conv (conv_C = 3*C, weights [hi | lo | hi] per tap) computes the
+   * fp32 product to ~2^-16.  out_s3_relu: the same of max(v, 0).  Used for the downstream heads, which the reference
+   * runs with autocast disabled (model.py:1774). */
+  void* out_s3;
+  void* out_s3_relu;
 } mapa_gemm_desc;
 
 int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
@@ -124,7 +133,8 @@ int mapa_attn_merge(const void* o_a, const float* lse_a, const void* o_b, const 
                     float* lse_out, int dtype, int rows, int heads, int64_t ld, mapa_stream_t stream);
 
 /* LayerNorm over the last dim (nn.LayerNorm eps=1e-6): y = (x-mean)/sqrt(var+eps)*w + b.
- * x: f32 rows (row stride ldx); outputs optional: y_f32 (ldy), y_lp (bf16 or f32 per lp_dtype, ldy).
+ * x: f32 rows (row stride ldx); outputs optional: y_f32 (ldy), y_lp (bf16 or f32 per lp_dtype, ldy; MAPA_BF16X3:
+ * split rows of 3*ldy bf16).
  * Output row r reads input row (in_group > 0 ? (r / in_group) * in_group_stride + r % in_group : r) + in_row_off
  * (e.g. drop the DINOv2 cls row of every view: group T, stride T+1, offset 1). */
 int mapa_layernorm(const float* x, int64_t ldx, int rows, int dim, const float* w, const float* b, float eps,
@@ -146,7 +156,8 @@ int mapa_assemble_tokens(const float* patch, const float* cls, const float* pos,
 int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, const float* vec, mapa_stream_t stream);
 
 /* Bilinear resize, align_corners=True, NHWC.  Output grid is the full (OHf, OWf) grid of F.interpolate; only
- * rows < OH and cols < OW are written (fused crop, dpt.py:213).  in: f32 or bf16 (in_dtype), out: out_dtype. */
+ * rows < OH and cols < OW are written (fused crop, dpt.py:213).  in: f32 or bf16 (in_dtype), out: out_dtype
+ * (MAPA_BF16X3: split rows [hi | hi | lo] of 3*C bf16 per pixel). */
 int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH, int OW,
                      void* out, int out_dtype, mapa_stream_t stream);
 

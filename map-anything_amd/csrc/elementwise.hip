@@ -114,7 +114,7 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 // One thread = 8 channels of one output pixel (16-B bf16 accesses); consecutive threads walk the channels of a
 // pixel, so a wave reads each of the 4 source taps and writes the output as contiguous row segments.  32-bit
 // indexing (the caller checks the element count).
-template <typename TI, typename TO>
+template <typename TI, typename TO, bool S3 = false>  // S3: split operand rows [hi | hi | lo] (3C wide)
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                    int OW, TO* __restrict__ out) {
   const int c8 = C / 8;
@@ -135,14 +135,20 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
     const TI* base = in + (size_t)im * IH * IW * C + c;
     const size_t o00 = ((size_t)y0 * IW + x0) * C, o01 = ((size_t)y0 * IW + x1) * C;
     const size_t o10 = ((size_t)y1 * IW + x0) * C, o11 = ((size_t)y1 * IW + x1) * C;
-    TO* op = out + (((size_t)im * OH + oy) * OW + ox) * C + c;
+    TO* op = out + (((size_t)im * OH + oy) * OW + ox) * (S3 ? 3 * C : C) + c;
     f32x4 a0, a1, b0, b1, c0, c1, d0, d1;
     load8(base + o00, a0, a1);
     load8(base + o01, b0, b1);
     load8(base + o10, c0, c1);
     load8(base + o11, d0, d1);
-    store8(op, ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0),
-           ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1));
+    const f32x4 r0 = ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0);
+    const f32x4 r1 = ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1);
+    if constexpr (S3) {
+      store_split3(op, C, r0);
+      store_split3(op + 4, C, r1);
+    } else {
+      store8(op, r0, r1);
+    }
   }
 }
 
@@ -408,7 +414,16 @@ extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int
   const int64_t total = (int64_t)n * OH * OW * (C / 8);
   MAPA_CHECK_ARG(total < (1LL << 31), "mapa_bilinear_ac: too many outputs for one launch");
   const dim3 g(grid_for(total)), b(TPB);
-  if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
+  MAPA_CHECK_ARG((in_dtype == MAPA_F32 || in_dtype == MAPA_BF16) &&
+                     (out_dtype == MAPA_F32 || out_dtype == MAPA_BF16 || out_dtype == MAPA_BF16X3),
+                 "mapa_bilinear_ac: bad dtypes");
+  if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32)
+    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, true>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
+                       OHf, OWf, OH, OW, (bf16_t*)out);
+  else if (out_dtype == MAPA_BF16X3)
+    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, true>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C,
+                       OHf, OWf, OH, OW, (bf16_t*)out);
+  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
     hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
                        OWf, OH, OW, (bf16_t*)out);
   else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16)

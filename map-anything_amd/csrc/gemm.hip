@@ -318,7 +318,8 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int E = d->dtype == MAPA_BF16 ? 8 : 4;
   MAPA_CHECK_ARG(d->K % E == 0, "mapa_gemm: K=%d must be a multiple of %d", d->K, E);
   MAPA_CHECK_ARG(d->A && d->W, "mapa_gemm: null operand");
-  MAPA_CHECK_ARG(d->out_f32 || d->out_lp || d->out_lp_relu, "mapa_gemm: no output");
+  MAPA_CHECK_ARG(d->out_f32 || d->out_lp || d->out_lp_relu || d->out_s3 || d->out_s3_relu, "mapa_gemm: no output");
+  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || (!d->out_s3 && !d->out_s3_relu), "mapa_gemm: split outputs need dtype bf16");
   MAPA_CHECK_ARG(d->act >= MAPA_ACT_NONE && d->act <= MAPA_ACT_GELU_POST, "mapa_gemm: bad act %d", d->act);
   MAPA_CHECK_ARG(d->act != MAPA_ACT_GELU_POST || !d->gamma, "mapa_gemm: GELU_POST takes no gamma");
   if (d->a_mode == MAPA_A_CONV3X3) {
@@ -351,6 +352,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   a.gamma = d->gamma; a.act = d->act;
   a.resid1 = d->resid1; a.resid2 = d->resid2;
   a.out_f32 = d->out_f32; a.out_lp = d->out_lp; a.out_lp_relu = d->out_lp_relu; a.ldo = d->ldo;
+  a.out_s3 = d->out_s3; a.out_s3_relu = d->out_s3_relu;
   a.out_mode = d->out_mode; a.ps_s = d->ps_s; a.ps_h = d->ps_h; a.ps_w = d->ps_w; a.ps_cout = d->ps_cout;
   a.vec_ok = (d->N % 4 == 0) && (d->out_mode == MAPA_OUT_PIXSHUF || d->ldo % 4 == 0);
   MAPA_CHECK_ARG(a.vec_ok || d->out_mode == MAPA_OUT_ROWMAJOR, "mapa_gemm: pixel shuffle needs N %% 4 == 0");

@@ -21,6 +21,8 @@ struct GemmArgs {
   float* out_f32;
   void* out_lp;
   void* out_lp_relu;
+  void* out_s3;       // split-precision operand outputs (bf16 kernels): [hi | hi | lo] of v, row stride 3*ld
+  void* out_s3_relu;
   int64_t ldo;
   int out_mode;  // 0 row-major, 1 pixel shuffle
   int ps_s, ps_h, ps_w, ps_cout;
@@ -57,7 +59,7 @@ __device__ __forceinline__ float epi_act(float v, int act) {
 struct EpiCol {
   int n0;
   float bv[4], gv[4];
-  int64_t col_off;
+  int64_t col_off;  // column inside an output row (the pixel's channel in PIXSHUF mode)
   int ps_ky, ps_kx;
   bool vec;
 };
@@ -87,16 +89,20 @@ __device__ __forceinline__ EpiCol epi_col_setup(const GemmArgs& p, int n0) {
 // for row m, columns c.n0..c.n0+3 (caller guarantees m < M and n0 < N).
 template <typename T>
 __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c, int m, f32x4 a) {
-  int64_t off;
+  int64_t orow, ld;  // output row (pixel in PIXSHUF mode) and its stride
   if (p.out_mode == 0) {
-    off = (int64_t)m * p.ldo + c.col_off;
+    orow = m;
+    ld = p.ldo;
   } else {
     const int hw = p.ps_h * p.ps_w;
     const int img = m / hw, rem = m - img * hw;
     const int y = rem / p.ps_w, x = rem - y * p.ps_w;
     const int64_t W2 = (int64_t)p.ps_w * p.ps_s, H2 = (int64_t)p.ps_h * p.ps_s;
-    off = (((int64_t)img * H2 + y * p.ps_s + c.ps_ky) * W2 + x * p.ps_s + c.ps_kx) * p.ps_cout + c.col_off;
+    orow = ((int64_t)img * H2 + y * p.ps_s + c.ps_ky) * W2 + x * p.ps_s + c.ps_kx;
+    ld = p.ps_cout;
   }
+  const int64_t off = orow * ld + c.col_off;
+  const int64_t off3 = orow * 3 * ld + c.col_off;  // split-operand rows are [hi | hi | lo], 3*ld wide
   f32x4 v;
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + c.bv[e], p.act) * c.gv[e];
@@ -121,6 +127,11 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
         u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
       }
+      if (p.out_s3) store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v);
+      if (p.out_s3_relu) {
+        const f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
+        store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, rr);
+      }
     } else {
       if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
       if (p.out_lp_relu) {
@@ -142,6 +153,8 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
       if constexpr (sizeof(T) == 2) {
         if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
         if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
+        if (p.out_s3) store_split1(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + e, ld, x);
+        if (p.out_s3_relu) store_split1(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + e, ld, fmaxf(x, 0.f));
       } else {
         if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
         if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);

@@ -46,7 +46,9 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     for (int j = 0; j < 4; ++j) y[j] = (v[i][j] - mean) * rstd * wv[j] + bv[j];
     if (yf) *reinterpret_cast<f32x4*>(yf + (int64_t)row * ldy + c) = y;
     if (ylp) {
-      if (lp_bf16) {
+      if (lp_bf16 == 2) {  // split operand row: [hi | hi | lo], 3*ldy wide
+        store_split3(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 3 * ldy + c, ldy, y);
+      } else if (lp_bf16) {
         uint2 pk;
         pk.x = pack_bf16x2(y[0], y[1]);
         pk.y = pack_bf16x2(y[2], y[3]);
@@ -68,7 +70,8 @@ extern "C" int mapa_layernorm(const float* x, int64_t ldx, int rows, int dim, co
   MAPA_CHECK_ARG(dim == 768 || dim == 1024 || dim == 512 || dim == 256, "mapa_layernorm: dim %d unsupported", dim);
   MAPA_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "mapa_layernorm: strides must be multiples of 4");
   const dim3 grid((rows + 3) / 4), blk(256);
-  const int bf = lp_dtype == MAPA_BF16;
+  MAPA_CHECK_ARG(lp_dtype == MAPA_F32 || lp_dtype == MAPA_BF16 || lp_dtype == MAPA_BF16X3, "mapa_layernorm: bad lp_dtype");
+  const int bf = lp_dtype == MAPA_BF16X3 ? 2 : lp_dtype == MAPA_BF16 ? 1 : 0;
   switch (dim / 256) {
     case 1: hipLaunchKernelGGL(layernorm_kernel<1>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off); break;
     case 2: hipLaunchKernelGGL(layernorm_kernel<2>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off); break;

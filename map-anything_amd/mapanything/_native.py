@@ -15,7 +15,7 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmapa.so")
 _lib = None
 
-F32, BF16 = 0, 1
+F32, BF16, BF16X3 = 0, 1, 2
 A_DENSE, A_CONV3X3 = 0, 1
 OUT_ROWMAJOR, OUT_PIXSHUF = 0, 1
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_POST = 0, 1, 2, 3
@@ -44,6 +44,7 @@ class GemmDesc(ctypes.Structure):
         ("out_lp", ctypes.c_void_p), ("out_lp_relu", ctypes.c_void_p), ("ldo", ctypes.c_int64),
         ("out_mode", ctypes.c_int), ("ps_s", ctypes.c_int), ("ps_h", ctypes.c_int), ("ps_w", ctypes.c_int),
         ("ps_cout", ctypes.c_int), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
+        ("out_s3", ctypes.c_void_p), ("out_s3_relu", ctypes.c_void_p),
     ]
 
 
@@ -234,8 +235,10 @@ def gemm_set_variant(variant: int = 0):
 
 
 def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_NONE, resid1=None, resid2=None,
-         out_f32=None, out_lp=None, out_lp_relu=None, ldo=None, conv=None, pixshuf=None):
-    """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout)."""
+         out_f32=None, out_lp=None, out_lp_relu=None, out_s3=None, out_s3_relu=None, ldo=None, conv=None,
+         pixshuf=None):
+    """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout).
+    out_s3 / out_s3_relu: split-precision operand outputs (bf16 [rows][3*ldo], [hi | hi | lo])."""
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype
@@ -257,6 +260,11 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     d.out_f32 = None if out_f32 is None else out_f32.data_ptr()
     d.out_lp = None if out_lp is None else out_lp.data_ptr()
     d.out_lp_relu = None if out_lp_relu is None else out_lp_relu.data_ptr()
+    for t in (out_s3, out_s3_relu):
+        if t is not None and t.dtype != torch.bfloat16:
+            raise NativeError("split outputs are bf16 [rows][3*ld]")
+    d.out_s3 = None if out_s3 is None else out_s3.data_ptr()
+    d.out_s3_relu = None if out_s3_relu is None else out_s3_relu.data_ptr()
     d.ldo = ldo if ldo is not None else N
     if pixshuf is not None:
         d.out_mode = OUT_PIXSHUF
@@ -270,7 +278,9 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     tok = _tic()
     check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
-    _toc(tok, "conv3x3" if conv is not None else "gemm", 2.0 * M * N * K)
+    # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops
+    split = "_split" if (W.dtype == torch.bfloat16 and getattr(W, "_mapa_split", False)) else ""
+    _toc(tok, ("conv3x3" if conv is not None else "gemm") + split, 2.0 * M * N * K)
 
 
 def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, k_bstride, k_rstride,
@@ -301,9 +311,15 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
     _toc(tok, kind, 4.0 * batch * heads * seq_q * seq_kv * 64)
 
 
-def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, ldy=None, group=0,
+def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, y_s3=None, ldy=None, group=0,
               group_stride=0, row_off=0):
-    lp_dtype = BF16 if (y_lp is not None and y_lp.dtype == torch.bfloat16) else F32
+    """y_s3: split-precision operand rows (bf16 [rows][3*ldy]) instead of y_lp."""
+    if y_s3 is not None:
+        if y_lp is not None or y_s3.dtype != torch.bfloat16:
+            raise NativeError("layernorm: y_s3 (bf16) replaces y_lp")
+        y_lp, lp_dtype = y_s3, BF16X3
+    else:
+        lp_dtype = BF16 if (y_lp is not None and y_lp.dtype == torch.bfloat16) else F32
     tok = _tic()
     check(lib().mapa_layernorm(ptr(x), ldx if ldx is not None else dim, rows, dim, ptr(w), ptr(b), eps, ptr(y_f32),
                                ptr(y_lp), lp_dtype, ldy if ldy is not None else dim, group, group_stride, row_off,
@@ -324,9 +340,12 @@ def add_rowvec(x, ldx, r0, r1, dim, vec):
     check(lib().mapa_add_rowvec(ptr(x), ldx, r0, r1, dim, ptr(vec), stream()), "mapa_add_rowvec")
 
 
-def bilinear_ac(inp, n, IH, IW, C, OHf, OWf, OH, OW, out):
+def bilinear_ac(inp, n, IH, IW, C, OHf, OWf, OH, OW, out, split_out=False):
+    """split_out: out is a split-precision operand (bf16 [pixels][3*C], [hi | hi | lo])."""
+    if split_out and out.dtype != torch.bfloat16:
+        raise NativeError("bilinear_ac: split output is bf16")
     check(lib().mapa_bilinear_ac(ptr(inp), dt_code(inp.dtype), n, IH, IW, C, OHf, OWf, OH, OW, ptr(out),
-                                 dt_code(out.dtype), stream()), "mapa_bilinear_ac")
+                                 BF16X3 if split_out else dt_code(out.dtype), stream()), "mapa_bilinear_ac")
 
 
 def mean_tokens(x, n, T, C, y):

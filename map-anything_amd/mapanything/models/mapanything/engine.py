@@ -11,9 +11,13 @@ torch allocations on the current device; torch does nothing else.  Layout in HBM
                     pixel-shuffled map directly from the GEMM epilogue
   outputs           NHWC fp32 [view][H][W][c] (the reference's (B,H,W,c) per view, view-major)
 
-Precision modes: "bf16" (bf16 MFMA operands, fp32 accumulate / LayerNorm / softmax / residuals — the reference's
-own autocast recipe, model.py:2287-2302) and "fp32" (exact-fp32 MFMA everywhere, for parity against the fp32
-reference to ~1e-5).
+Precision modes: "bf16" (the reference's own autocast recipe, model.py:2287-2302: the encoder and the transformer run
+on bf16 MFMA operands with fp32 accumulate / LayerNorm / softmax / residuals; the geometric-input encoders
+(autocast disabled, model.py:1377) and the downstream heads (autocast disabled, model.py:1774-1799) stay fp32-exact,
+computed as split-precision bf16 GEMMs: activations [hi | hi | lo], weights [hi | lo | hi], ~2^-16 relative) and
+"fp32" (exact-fp32 MFMA everywhere, for parity against the fp32 reference to ~1e-5).  heads="bf16" is an opt-in
+fast mode that runs the heads on plain bf16 operands — NOT the reference's recipe (bench.py reports it as a
+separate, labelled line).
 """
 
 from __future__ import annotations
@@ -65,12 +69,30 @@ class GeoInputs:
         return not self.ray_views and not self.depth_views and not any(self.cam_mask)
 
 
-class PackedWeights:
-    """Canonical state dict -> device buffers in kernel layout (done once at load)."""
+def _split_pack(w: np.ndarray, dev) -> torch.Tensor:
+    """[out][taps][cin] fp32 -> bf16 [out][taps * 3 * ceil8(cin)] = [hi | lo | hi] per tap: the weight side of a
+    split-precision GEMM against activations [hi | hi | lo] (mapa_split_bf16x3 / the GEMM's out_s3 epilogue)."""
+    o, taps, cin = w.shape
+    wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+    hi = wt.to(torch.bfloat16)
+    lo = (wt - hi.float()).to(torch.bfloat16)
+    cp = _ceil8(cin)
+    out = torch.zeros(o, taps, 3, cp, dtype=torch.bfloat16, device=dev)
+    out[:, :, 0, :cin], out[:, :, 1, :cin], out[:, :, 2, :cin] = hi, lo, hi
+    out = out.reshape(o, -1)
+    out._mapa_split = True  # timed as its own class (nat.gemm: "gemm_split" / "conv3x3_split")
+    return out
 
-    def __init__(self, sd: Dict[str, object], device, lp_dtype: torch.dtype, info: InfoSharingSpec = RELEASED_INFO):
+
+class PackedWeights:
+    """Canonical state dict -> device buffers in kernel layout (done once at load).  head_split: the downstream
+    heads' GEMM weights are packed for split-precision operands (the reference's fp32 heads in bf16 mode)."""
+
+    def __init__(self, sd: Dict[str, object], device, lp_dtype: torch.dtype, info: InfoSharingSpec = RELEASED_INFO,
+                 head_split: bool = False):
         self.device = device
         self.lp = lp_dtype
+        self.head_split = head_split
         self.sd = sd
         g = self._get
         dev = device
@@ -92,6 +114,24 @@ class PackedWeights:
             ci, co, k, _ = w.shape
             return torch.from_numpy(np.ascontiguousarray(w.transpose(2, 3, 1, 0).reshape(k * k * co, ci))).to(
                 dev, self.lp)
+
+        def hpack(w):  # head weights [out][taps][cin]: lp (or fp32) [out][taps*cin], or split-packed
+            if head_split:
+                return _split_pack(w, dev)
+            return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev, self.lp)
+
+        def hlin(name):
+            w = _np(g(f"{name}.weight"))
+            return hpack(w.reshape(w.shape[0], 1, -1))
+
+        def hconv3(name):
+            w = _np(g(f"{name}.weight"))
+            return hpack(w.transpose(0, 2, 3, 1).reshape(w.shape[0], 9, w.shape[1]))
+
+        def hconvT(name):
+            w = _np(g(f"{name}.weight"))
+            ci, co, k, _ = w.shape
+            return hpack(w.transpose(2, 3, 1, 0).reshape(k * k * co, 1, ci))
 
         self.f32, self.lin, self.conv3 = f32, lin, conv3
         # DINOv2
@@ -138,31 +178,31 @@ class PackedWeights:
         h = "dpt_feature_head"
         ip = f"{h}.input_process"
         self.ip = [
-            dict(w=lin(f"{ip}.0.0.0"), b=f32(f"{ip}.0.0.0.bias"), ct=convT(f"{ip}.0.0.1"), ct_b=f32(f"{ip}.0.0.1.bias")),
-            dict(w=lin(f"{ip}.1.0.0"), b=f32(f"{ip}.1.0.0.bias"), ct=convT(f"{ip}.1.0.1"), ct_b=f32(f"{ip}.1.0.1.bias")),
-            dict(w=lin(f"{ip}.2.0.0"), b=f32(f"{ip}.2.0.0.bias")),
-            dict(w=lin(f"{ip}.3.0.0"), b=f32(f"{ip}.3.0.0.bias"), c3=conv3(f"{ip}.3.0.1"), c3_b=f32(f"{ip}.3.0.1.bias")),
+            dict(w=hlin(f"{ip}.0.0.0"), b=f32(f"{ip}.0.0.0.bias"), ct=hconvT(f"{ip}.0.0.1"), ct_b=f32(f"{ip}.0.0.1.bias")),
+            dict(w=hlin(f"{ip}.1.0.0"), b=f32(f"{ip}.1.0.0.bias"), ct=hconvT(f"{ip}.1.0.1"), ct_b=f32(f"{ip}.1.0.1.bias")),
+            dict(w=hlin(f"{ip}.2.0.0"), b=f32(f"{ip}.2.0.0.bias")),
+            dict(w=hlin(f"{ip}.3.0.0"), b=f32(f"{ip}.3.0.0.bias"), c3=hconv3(f"{ip}.3.0.1"), c3_b=f32(f"{ip}.3.0.1.bias")),
         ]
-        self.layer_rn = [conv3(f"{h}.scratch.layer{i + 1}_rn") for i in range(4)]
+        self.layer_rn = [hconv3(f"{h}.scratch.layer{i + 1}_rn") for i in range(4)]
         self.refine = {}
         for r in (1, 2, 3, 4):
             n = f"{h}.scratch.refinenet{r}"
-            d = dict(out=lin(f"{n}.out_conv"), out_b=f32(f"{n}.out_conv.bias"))
+            d = dict(out=hlin(f"{n}.out_conv"), out_b=f32(f"{n}.out_conv.bias"))
             units = ("resConfUnit2",) if r == 4 else ("resConfUnit1", "resConfUnit2")
             for u in units:
-                d[u] = dict(c1=conv3(f"{n}.{u}.conv1"), b1=f32(f"{n}.{u}.conv1.bias"),
-                            c2=conv3(f"{n}.{u}.conv2"), b2=f32(f"{n}.{u}.conv2.bias"))
+                d[u] = dict(c1=hconv3(f"{n}.{u}.conv1"), b1=f32(f"{n}.{u}.conv1.bias"),
+                            c2=hconv3(f"{n}.{u}.conv2"), b2=f32(f"{n}.{u}.conv2.bias"))
             self.refine[r] = d
-        self.reg_c1, self.reg_b1 = conv3("dpt_regressor_head.conv1"), f32("dpt_regressor_head.conv1.bias")
-        self.reg_c2, self.reg_b2 = conv3("dpt_regressor_head.conv2.0"), f32("dpt_regressor_head.conv2.0.bias")
+        self.reg_c1, self.reg_b1 = hconv3("dpt_regressor_head.conv1"), f32("dpt_regressor_head.conv1.bias")
+        self.reg_c2, self.reg_b2 = hconv3("dpt_regressor_head.conv2.0"), f32("dpt_regressor_head.conv2.0.bias")
         self.reg_w6 = f32("dpt_regressor_head.conv2.2.weight").reshape(6, 128).contiguous()
         self.reg_b6 = f32("dpt_regressor_head.conv2.2.bias")
         # pose head (1x1 convs as GEMMs, MLP tail fp32)
-        self.pose_proj, self.pose_proj_b = lin("pose_head.proj"), f32("pose_head.proj.bias")
+        self.pose_proj, self.pose_proj_b = hlin("pose_head.proj"), f32("pose_head.proj.bias")
         self.pose_res = []
         for b in range(2):
             n = f"pose_head.res_conv.{b}"
-            self.pose_res.append([(lin(f"{n}.res_conv{c}"), f32(f"{n}.res_conv{c}.bias")) for c in (1, 2, 3)])
+            self.pose_res.append([(hlin(f"{n}.res_conv{c}"), f32(f"{n}.res_conv{c}.bias")) for c in (1, 2, 3)])
         self.pose_mlp = [(f32(f"pose_head.more_mlps.{i}.weight"), f32(f"pose_head.more_mlps.{i}.bias")) for i in (0, 2)]
         # fc_t (3) and fc_rot (4) share their input: one 7-row linear gives cat([t, rot]) (pose_head.py:155-158)
         self.pose_tr = (torch.cat([f32("pose_head.fc_t.weight"), f32("pose_head.fc_rot.weight")], 0).contiguous(),
@@ -190,16 +230,9 @@ class PackedWeights:
             return torch.from_numpy(np.ascontiguousarray(_np(sd[name]))).to(dev)
 
         def pack(w):  # [out][taps][cin] fp32 -> fp32 [out][taps*cin] or bf16 [out][taps*3*cinp] (hi | lo | hi)
-            o, taps, cin = w.shape
             if not split:
-                return torch.from_numpy(np.ascontiguousarray(w.reshape(o, -1))).to(dev)
-            wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
-            hi = wt.to(torch.bfloat16)
-            lo = (wt - hi.float()).to(torch.bfloat16)
-            cp = _ceil8(cin)
-            out = torch.zeros(o, taps, 3, cp, dtype=torch.bfloat16, device=dev)
-            out[:, :, 0, :cin], out[:, :, 1, :cin], out[:, :, 2, :cin] = hi, lo, hi
-            return out.reshape(o, -1)
+                return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev)
+            return _split_pack(w, dev)
 
         def c3(name):
             w = _np(sd[f"{name}.weight"])
@@ -254,17 +287,52 @@ def _ceil8(c: int) -> int:
 
 class MapaEngine:
     def __init__(self, sd: Dict[str, object], device=None, precision: str = "bf16",
-                 info: InfoSharingSpec = RELEASED_INFO):
+                 info: InfoSharingSpec = RELEASED_INFO, heads: str = "fp32"):
         if precision not in ("bf16", "fp32"):
             raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision}")
+        if heads not in ("fp32", "bf16"):
+            raise ValueError(f"heads must be 'fp32' (the reference's recipe) or 'bf16' (fast mode), got {heads}")
         nat.lib()  # fail loudly without the HIP library / a gfx950 device
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.precision = precision
         self.lp = torch.bfloat16 if precision == "bf16" else torch.float32
+        # heads at the reference's fp32 in bf16 mode: split-precision operands (hsplit); fp32 mode is exact already
+        self.heads = "fp32" if precision == "fp32" else heads
+        self.hsplit = precision == "bf16" and heads == "fp32"
         self._sd = sd  # host state dict: the geometric encoders are packed on first use
         self.info = info
         with torch.cuda.device(self.device):
-            self.w = PackedWeights(sd, self.device, self.lp, info)
+            self.w = PackedWeights(sd, self.device, self.lp, info, head_split=self.hsplit)
+
+    # ------------------------------------------------------------------------- head operands (model.py:1774)
+    def _hop(self, rows, C):
+        """Operand buffer of a head GEMM/conv input with C logical channels: split rows [hi | hi | lo] (bf16,
+        3C wide) when the heads run at the reference's fp32 in bf16 mode, else lp rows."""
+        if self.hsplit:
+            return torch.empty(rows, 3 * C, dtype=torch.bfloat16, device=self.device)
+        return self._empty(rows, C)
+
+    def _hw(self, C):
+        """Per-pixel operand width of a head input with C logical channels."""
+        return 3 * C if self.hsplit else C
+
+    def _hout(self, buf=None, relu=None):
+        """GEMM output keywords writing head operands: out_s3 / out_s3_relu in split mode, else out_lp / _relu."""
+        d = {}
+        if buf is not None:
+            d["out_s3" if self.hsplit else "out_lp"] = buf
+        if relu is not None:
+            d["out_s3_relu" if self.hsplit else "out_lp_relu"] = relu
+        return d
+
+    def head_rows(self, x_f32):
+        """fp32 rows [R][C] -> a head operand (module-level API inputs, model.py:1774 fp32 heads)."""
+        R, C = x_f32.shape
+        if self.hsplit:
+            y = self._hop(R, C)
+            nat.split_bf16x3(x_f32.contiguous(), R, C, C, y)
+            return y
+        return x_f32.to(self.lp).contiguous()
 
     # ---------------------------------------------------------------------------------------- profiling
     def enable_kernel_timing(self):
@@ -277,9 +345,16 @@ class MapaEngine:
     def _empty(self, *shape, dtype=None):
         return torch.empty(shape, dtype=dtype or self.lp, device=self.device)
 
-    def _ln(self, x, rows, dim, w, b, *, y_f32=None, y_lp=None, group=0, gstride=0, off=0, ldx=None):
-        nat.layernorm(x, rows, dim, w, b, eps=LN_EPS, ldx=ldx, y_f32=y_f32, y_lp=y_lp, group=group,
+    def _ln(self, x, rows, dim, w, b, *, y_f32=None, y_lp=None, y_s3=None, group=0, gstride=0, off=0, ldx=None):
+        nat.layernorm(x, rows, dim, w, b, eps=LN_EPS, ldx=ldx, y_f32=y_f32, y_lp=y_lp, y_s3=y_s3, group=group,
                       group_stride=gstride, row_off=off)
+
+    def _ln_head(self, x, rows, dim, w, b, out, **kw):
+        """LayerNorm whose output feeds a head: split operand rows in split mode, else lp rows."""
+        if self.hsplit:
+            self._ln(x, rows, dim, w, b, y_s3=out, **kw)
+        else:
+            self._ln(x, rows, dim, w, b, y_lp=out, **kw)
 
     def _conv3(self, x, n, IH, IW, C, wmat, Cout, stride=1, **epi):
         OH, OW = (IH + 2 - 3) // stride + 1, (IW + 2 - 3) // stride + 1
@@ -320,7 +395,8 @@ class MapaEngine:
             self.geometric(enc, geo, VB, H, W)
         fused_lp = self._empty(VB * T + 1, ENC_DIM)
         identity = w.pe_proj is None  # the transformer reads the fp32 fused rows directly
-        fused_f32 = self._empty(VB * T + 1, ENC_DIM, dtype=torch.float32) if taps is not None or identity else None
+        need_f32 = taps is not None or identity or self.hsplit  # split heads read the fp32 fused rows (DPT input 0)
+        fused_f32 = self._empty(VB * T + 1, ENC_DIM, dtype=torch.float32) if need_f32 else None
         self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
         nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
         if fused_f32 is not None:
@@ -486,8 +562,8 @@ class MapaEngine:
     def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None, pe_idx=None, fused_f32=None):
         """The multi-view transformer with intermediate-feature return: AAT (alternating_attention_transformer.py:
         530-771; released config: 24 blocks, taps after 11 and 17) or GAT (global_attention_transformer.py:458-640:
-        every block global), per self.info.  Returns the list of normed taps (2 or 3, lp, VB*T rows), the final
-        features (lp) and the final scale-token feature (f32, dim).  fused_f32: the fp32 fused rows (with the scale token), needed
+        every block global), per self.info.  Returns the list of normed taps (2 or 3, VB*T rows) and the final
+        features as head operands (_hop: split rows or lp), and the final scale-token feature (f32, dim).  fused_f32: the fp32 fused rows (with the scale token), needed
         when proj_embed is the identity.  pe_idx: (V_total,) int64 device tensor of view-PE table rows (row 0 for the
         reference view) when the variant encodes non-reference views too.  With `shard` (parallel.ShardPlan) this
         rank holds only its views (+ the scale-token replica) and the global layers all-gather K/V through `comm`."""
@@ -526,10 +602,10 @@ class MapaEngine:
             else:                   # frame attention inside each view; the scale token bypasses the block
                 self._block(y, yn, qkv, ao, hbuf, VB * T, D, NH, p, attn_batch=VB, attn_seq=T,
                             gamma=False, attn_scale=f_scale)
-            if d in info.indices:
-                t_lp = self._empty(VB * T, D)
+            if d in info.indices:  # IFR taps feed only the DPT (a head: fp32 in the reference, model.py:1774)
+                t_lp = self._hop(VB * T, D)
                 t_f = self._empty(VB * T, D, dtype=torch.float32) if taps is not None else None
-                self._ln(y, VB * T, D, w.aat_nw, w.aat_nb, y_lp=t_lp, y_f32=t_f)
+                self._ln_head(y, VB * T, D, w.aat_nw, w.aat_nb, t_lp, y_f32=t_f)
                 inter[d] = t_lp
                 if taps is not None:
                     taps[f"aat_l{d}"] = t_f
@@ -537,9 +613,9 @@ class MapaEngine:
                     self._ln(y[VB * T:], 1, D, w.aat_nw, w.aat_nb, y_f32=tk)
                     taps[f"aat_l{d}_token"] = tk
         del yn, qkv, ao, hbuf
-        fin_lp = self._empty(L, D)
+        fin_lp = self._hop(L, D)  # the final features feed the DPT and the pose head only
         fin_f32 = self._empty(L, D, dtype=torch.float32)
-        self._ln(y, L, D, w.aat_nw, w.aat_nb, y_lp=fin_lp, y_f32=fin_f32)
+        self._ln_head(y, L, D, w.aat_nw, w.aat_nb, fin_lp, y_f32=fin_f32)
         if taps is not None:
             taps["aat_final"] = fin_f32[:VB * T]
             taps["scale_token"] = fin_f32[VB * T]
@@ -589,56 +665,65 @@ class MapaEngine:
 
     # ----------------------------------------------------------------------------------------------- DPT
     def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None):
-        """fused_lp: the first DPT input — the fused encoder features (ENC_DIM) or, with three info-sharing taps
-        (model.py:1748-1768), the first tap (AAT_DIM); its width comes from the packed weight."""
-        """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Returns the ReLU'd 128-ch hidden map at HxW."""
+        """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Inputs are head operands (_hop rows); fused_lp
+        is the first DPT input — the fused encoder features (ENC_DIM) or, with three info-sharing taps
+        (model.py:1748-1768), the first tap; its width comes from the packed weight.  Returns the ReLU'd 128-ch
+        hidden map at HxW (fp32 in split mode, else lp)."""
         owned = [self.dpt_feature(fused_lp, l11, l17, fin_lp, VB, hp, wp, taps)[0]]
         return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W)  # freed after its first conv
 
+    def _hconv3(self, x, n, IH, IW, C, wmat, Cout, stride=1, **epi):
+        """3x3 conv of a head operand with C logical channels."""
+        return self._conv3(x, n, IH, IW, self._hw(C), wmat, Cout, stride=stride, **epi)
+
+    def _hmap(self, rows, C):
+        """A head feature map that is re-read by a bilinear resize: fp32 in split mode, else lp."""
+        return self._empty(rows, C, dtype=torch.float32 if self.hsplit else self.lp)
+
     def dpt_feature(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, taps=None, want_f32=False):
-        """DPTFeature (dpt.py:180-232): the four IFR features [VB*T][C] (lp) -> the 256-ch map at 8x
-        [VB][8hp][8wp][256] (lp; f32 copy too if taps is given or want_f32)."""
+        """DPTFeature (dpt.py:180-232): the four IFR features [VB*T][C] (head operands) -> the 256-ch map at 8x
+        [VB][8hp][8wp][256] (head operand; f32 copy too if taps is given or want_f32)."""
         w = self.w
         n, T = VB, hp * wp
-        lp = self.lp
+        D = self.info.dim
         # input_process 0: 1x1 1024 (or 768)->96, ConvT k4 s4, layer1_rn 3x3 96->256 (no bias)
-        a = self._empty(n * T, 96)
-        nat.gemm(fused_lp, w.ip[0]["w"], n * T, 96, w.ip[0]["w"].shape[1], bias=w.ip[0]["b"], out_lp=a)
-        up0 = self._empty(n, 4 * hp, 4 * wp, 96)
-        nat.gemm(a, w.ip[0]["ct"], n * T, 16 * 96, 96, bias=w.ip[0]["ct_b"], bias_mod=96, out_lp=up0,
-                 pixshuf=(4, hp, wp, 96))
+        a = self._hop(n * T, 96)
+        nat.gemm(fused_lp, w.ip[0]["w"], n * T, 96, w.ip[0]["w"].shape[1], bias=w.ip[0]["b"], **self._hout(a))
+        up0 = self._hop(n * 16 * T, 96)
+        nat.gemm(a, w.ip[0]["ct"], n * T, 16 * 96, self._hw(96), bias=w.ip[0]["ct_b"], bias_mod=96,
+                 pixshuf=(4, hp, wp, 96), **self._hout(up0))
         h0, w0 = 4 * hp, 4 * wp
         L0f = self._empty(n * h0 * w0, 256, dtype=torch.float32)
-        L0r = self._empty(n * h0 * w0, 256)
-        self._conv3(up0, n, h0, w0, 96, w.layer_rn[0], 256, out_f32=L0f, out_lp_relu=L0r)
+        L0r = self._hop(n * h0 * w0, 256)
+        self._hconv3(up0, n, h0, w0, 96, w.layer_rn[0], 256, out_f32=L0f, **self._hout(relu=L0r))
         del a, up0
         # input_process 1: 1x1 768->192, ConvT k2 s2, layer2_rn
-        a = self._empty(n * T, 192)
-        nat.gemm(l11, w.ip[1]["w"], n * T, 192, self.info.dim, bias=w.ip[1]["b"], out_lp=a)
-        up1 = self._empty(n, 2 * hp, 2 * wp, 192)
-        nat.gemm(a, w.ip[1]["ct"], n * T, 4 * 192, 192, bias=w.ip[1]["ct_b"], bias_mod=192, out_lp=up1,
-                 pixshuf=(2, hp, wp, 192))
+        a = self._hop(n * T, 192)
+        nat.gemm(l11, w.ip[1]["w"], n * T, 192, self._hw(D), bias=w.ip[1]["b"], **self._hout(a))
+        up1 = self._hop(n * 4 * T, 192)
+        nat.gemm(a, w.ip[1]["ct"], n * T, 4 * 192, self._hw(192), bias=w.ip[1]["ct_b"], bias_mod=192,
+                 pixshuf=(2, hp, wp, 192), **self._hout(up1))
         h1, w1 = 2 * hp, 2 * wp
         L1f = self._empty(n * h1 * w1, 256, dtype=torch.float32)
-        L1r = self._empty(n * h1 * w1, 256)
-        self._conv3(up1, n, h1, w1, 192, w.layer_rn[1], 256, out_f32=L1f, out_lp_relu=L1r)
+        L1r = self._hop(n * h1 * w1, 256)
+        self._hconv3(up1, n, h1, w1, 192, w.layer_rn[1], 256, out_f32=L1f, **self._hout(relu=L1r))
         del a, up1
         # input_process 2: 1x1 768->384, layer3_rn
-        a = self._empty(n * T, 384)
-        nat.gemm(l17, w.ip[2]["w"], n * T, 384, self.info.dim, bias=w.ip[2]["b"], out_lp=a)
+        a = self._hop(n * T, 384)
+        nat.gemm(l17, w.ip[2]["w"], n * T, 384, self._hw(D), bias=w.ip[2]["b"], **self._hout(a))
         L2f = self._empty(n * T, 256, dtype=torch.float32)
-        L2r = self._empty(n * T, 256)
-        self._conv3(a, n, hp, wp, 384, w.layer_rn[2], 256, out_f32=L2f, out_lp_relu=L2r)
+        L2r = self._hop(n * T, 256)
+        self._hconv3(a, n, hp, wp, 384, w.layer_rn[2], 256, out_f32=L2f, **self._hout(relu=L2r))
         del a
         # input_process 3: 1x1 768->768, 3x3 s2 768->768, layer4_rn
-        a = self._empty(n * T, 768)
-        nat.gemm(fin_lp, w.ip[3]["w"], n * T, 768, self.info.dim, bias=w.ip[3]["b"], out_lp=a)
+        a = self._hop(n * T, 768)
+        nat.gemm(fin_lp, w.ip[3]["w"], n * T, 768, self._hw(D), bias=w.ip[3]["b"], **self._hout(a))
         h3, w3 = (hp - 1) // 2 + 1, (wp - 1) // 2 + 1
-        b3 = self._empty(n * h3 * w3, 768)
-        self._conv3(a, n, hp, wp, 768, w.ip[3]["c3"], 768, stride=2, bias=w.ip[3]["c3_b"], out_lp=b3)
+        b3 = self._hop(n * h3 * w3, 768)
+        self._hconv3(a, n, hp, wp, 768, w.ip[3]["c3"], 768, stride=2, bias=w.ip[3]["c3_b"], **self._hout(b3))
         L3f = self._empty(n * h3 * w3, 256, dtype=torch.float32)
-        L3r = self._empty(n * h3 * w3, 256)
-        self._conv3(b3, n, h3, w3, 768, w.layer_rn[3], 256, out_f32=L3f, out_lp_relu=L3r)
+        L3r = self._hop(n * h3 * w3, 256)
+        self._hconv3(b3, n, h3, w3, 768, w.layer_rn[3], 256, out_f32=L3f, **self._hout(relu=L3r))
         del a, b3
         # refinenet4 (RCU2 only) -> x2 -> crop to (hp, wp) -> out_conv
         o = self._fusion_single(n, h3, w3, 4, L3f, L3r)
@@ -655,42 +740,47 @@ class MapaEngine:
 
     def dpt_regress(self, feat_lp, n, hf, wf, H, W):
         """DPTRegressionProcessor up to the last ReLU (dpt.py:285-311): conv3x3 256->128 at 8x, bilinear
-        (align_corners) to HxW, conv3x3 128->128 + ReLU -> hidden [n*H*W][128] (lp).  feat_lp may be a
-        one-element list, handed over so that the 8x map is freed as soon as it has been read."""
+        (align_corners) to HxW, conv3x3 128->128 + ReLU -> hidden [n*H*W][128] (fp32 in split mode, else lp).
+        feat_lp (a head operand) may be a one-element list, handed over so that the 8x map is freed as soon as it
+        has been read."""
         w = self.w
         if isinstance(feat_lp, list):
             feat_lp = feat_lp.pop()
-        r1 = self._empty(n * hf * wf, 128)
-        self._conv3(feat_lp, n, hf, wf, 256, w.reg_c1, 128, bias=w.reg_b1, out_lp=r1)
+        r1 = self._hmap(n * hf * wf, 128)
+        self._hconv3(feat_lp, n, hf, wf, 256, w.reg_c1, 128, bias=w.reg_b1,
+                     **({"out_f32": r1} if self.hsplit else {"out_lp": r1}))
         del feat_lp
-        r1u = self._empty(n * H * W, 128)
-        nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u)
+        r1u = self._hop(n * H * W, 128)
+        nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u, split_out=self.hsplit)
         del r1
-        hid = self._empty(n * H * W, 128)
-        self._conv3(r1u, n, H, W, 128, w.reg_c2, 128, bias=w.reg_b2, act=nat.ACT_RELU, out_lp=hid)
+        hid = self._hmap(n * H * W, 128)
+        self._hconv3(r1u, n, H, W, 128, w.reg_c2, 128, bias=w.reg_b2, act=nat.ACT_RELU,
+                     **({"out_f32": hid} if self.hsplit else {"out_lp": hid}))
         return hid
 
     def _fusion_single(self, n, h, w_, r, x_f, x_r):
         u = self.w.refine[r]["resConfUnit2"]
-        c1 = self._empty(n * h * w_, 256)
-        self._conv3(x_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, out_lp=c1)
-        o = self._empty(n * h * w_, 256)
-        self._conv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=x_f, out_lp=o)
+        c1 = self._hop(n * h * w_, 256)
+        self._hconv3(x_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, **self._hout(c1))
+        o = self._hmap(n * h * w_, 256)
+        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=x_f,
+                     **({"out_f32": o} if self.hsplit else {"out_lp": o}))
         return o
 
     def _fusion_two(self, n, h, w_, r, path_f, skip_f, skip_r):
         d = self.w.refine[r]
         u = d["resConfUnit1"]
-        c1 = self._empty(n * h * w_, 256)
-        self._conv3(skip_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, out_lp=c1)
+        c1 = self._hop(n * h * w_, 256)
+        self._hconv3(skip_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, **self._hout(c1))
         s_f = self._empty(n * h * w_, 256, dtype=torch.float32)
-        s_r = self._empty(n * h * w_, 256)
-        self._conv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=skip_f, resid2=path_f, out_f32=s_f,
-                    out_lp_relu=s_r)
+        s_r = self._hop(n * h * w_, 256)
+        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=skip_f, resid2=path_f, out_f32=s_f,
+                     **self._hout(relu=s_r))
         u = d["resConfUnit2"]
-        self._conv3(s_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, out_lp=c1)
-        o = self._empty(n * h * w_, 256)
-        self._conv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=s_f, out_lp=o)
+        self._hconv3(s_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, **self._hout(c1))
+        o = self._hmap(n * h * w_, 256)
+        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=s_f,
+                     **({"out_f32": o} if self.hsplit else {"out_lp": o}))
         return o
 
     def _upsample_outconv(self, o, n, h, w_, r, crop=None, lowp=False, taps=None):
@@ -698,33 +788,36 @@ class MapaEngine:
         d = self.w.refine[r]
         Hf, Wf = 2 * h, 2 * w_
         oh, ow = crop if crop is not None else (Hf, Wf)
-        up = self._empty(n * oh * ow, 256)
-        nat.bilinear_ac(o, n, h, w_, 256, Hf, Wf, oh, ow, up)
+        up = self._hop(n * oh * ow, 256)
+        nat.bilinear_ac(o, n, h, w_, 256, Hf, Wf, oh, ow, up, split_out=self.hsplit)
+        K = self._hw(256)
         if lowp:
-            out = self._empty(n * oh * ow, 256)
+            out = self._hop(n * oh * ow, 256)
             f = self._empty(n * oh * ow, 256, dtype=torch.float32) if taps is not None else None
-            nat.gemm(up, d["out"], n * oh * ow, 256, 256, bias=d["out_b"], out_lp=out, out_f32=f)
+            nat.gemm(up, d["out"], n * oh * ow, 256, K, bias=d["out_b"], out_f32=f, **self._hout(out))
             if taps is not None:
                 taps["dpt_feature"] = f.view(n, oh, ow, 256)
             return out
         out = self._empty(n * oh * ow, 256, dtype=torch.float32)
-        nat.gemm(up, d["out"], n * oh * ow, 256, 256, bias=d["out_b"], out_f32=out)
+        nat.gemm(up, d["out"], n * oh * ow, 256, K, bias=d["out_b"], out_f32=out)
         return out
 
     # ------------------------------------------------------------------------------------- pose / scale
     def pose(self, fin_lp, VB, T, taps=None):
-        """PoseHead (pose_head.py:50-159) -> raw (VB, 7)."""
+        """PoseHead (pose_head.py:50-159) on the final features (a head operand) -> raw (VB, 7)."""
         w = self.w
         M = VB * T
         pf = self._empty(M, POSE_DIM, dtype=torch.float32)
-        pl = self._empty(M, POSE_DIM)
-        nat.gemm(fin_lp, w.pose_proj, M, POSE_DIM, self.info.dim, bias=w.pose_proj_b, out_f32=pf, out_lp=pl)
-        t1, t2 = self._empty(M, POSE_DIM), self._empty(M, POSE_DIM)
+        pl = self._hop(M, POSE_DIM)
+        nat.gemm(fin_lp, w.pose_proj, M, POSE_DIM, self._hw(self.info.dim), bias=w.pose_proj_b, out_f32=pf,
+                 **self._hout(pl))
+        t1, t2 = self._hop(M, POSE_DIM), self._hop(M, POSE_DIM)
+        K = self._hw(POSE_DIM)
         for blk in w.pose_res:
             (w1, b1), (w2, b2), (w3, b3) = blk
-            nat.gemm(pl, w1, M, POSE_DIM, POSE_DIM, bias=b1, act=nat.ACT_RELU, out_lp=t1)
-            nat.gemm(t1, w2, M, POSE_DIM, POSE_DIM, bias=b2, act=nat.ACT_RELU, out_lp=t2)
-            nat.gemm(t2, w3, M, POSE_DIM, POSE_DIM, bias=b3, act=nat.ACT_RELU, resid1=pf, out_f32=pf, out_lp=pl)
+            nat.gemm(pl, w1, M, POSE_DIM, K, bias=b1, act=nat.ACT_RELU, **self._hout(t1))
+            nat.gemm(t1, w2, M, POSE_DIM, K, bias=b2, act=nat.ACT_RELU, **self._hout(t2))
+            nat.gemm(t2, w3, M, POSE_DIM, K, bias=b3, act=nat.ACT_RELU, resid1=pf, out_f32=pf, **self._hout(pl))
         pooled = self._empty(VB, POSE_DIM, dtype=torch.float32)
         nat.mean_tokens(pf, VB, T, POSE_DIM, pooled)
         h1 = self._empty(VB, POSE_DIM, dtype=torch.float32)
@@ -777,7 +870,11 @@ class MapaEngine:
             inter, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx,
                                           fused_f32=fused_f32)
             # DPT inputs (model.py:1724-1768): [encoder, tap0, tap1, final] or, with three taps, [tap0..2, final]
-            first, l11, l17 = (inter[0], inter[1], inter[2]) if len(inter) == 3 else (fused_lp, inter[0], inter[1])
+            if len(inter) == 3:
+                first, l11, l17 = inter
+            else:  # the fused encoder features, as a head operand (fp32 in the reference's heads)
+                first = self.head_rows(fused_f32[:VB * T]) if self.hsplit else fused_lp
+                l11, l17 = inter
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)

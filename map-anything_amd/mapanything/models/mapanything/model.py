@@ -8,8 +8,10 @@ the gfx950 HIP library (`MapaEngine`); this class is host glue: validation, devi
 Differences that are by design:
   * weights come from a LOCAL directory (config.json + model.safetensors) or the synthetic named-PRNG
     checkpoint; there is no hub download (no network on this box),
-  * `precision="bf16"` (default) mirrors `infer(use_amp=True, amp_dtype="bf16")`; `use_amp=False` (or
-    precision="fp32") runs the exact-fp32 MFMA path,
+  * `precision="bf16"` (default) mirrors `infer(use_amp=True, amp_dtype="bf16")` — bf16 encoder/transformer, the
+    geometric encoders and the downstream heads fp32-exact as the reference runs them with autocast disabled
+    (model.py:1377, 1774; split-precision bf16 GEMMs on MI355X); `use_amp=False` (or precision="fp32") runs the
+    exact-fp32 MFMA path; `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
   * multi-view batches are processed B = 1 per view (the reference's configs all use B = 1).
 """
 
@@ -77,7 +79,8 @@ class MapAnything:
     def __init__(self, name: str, encoder_config: Dict, info_sharing_config: Dict, pred_head_config: Dict,
                  geometric_input_config: Dict, fusion_norm_layer=None, pretrained_checkpoint_path: str = None,
                  load_specific_pretrained_submodules: bool = False, specific_pretrained_submodules: list = None,
-                 torch_hub_force_reload: bool = False, precision: str = "bf16", hip_graphs: bool = True):
+                 torch_hub_force_reload: bool = False, precision: str = "bf16", hip_graphs: bool = True,
+                 head_precision: str = "fp32"):
         _check_config(encoder_config, info_sharing_config, pred_head_config)
         self.info = InfoSharingSpec.from_config(info_sharing_config)
         self.name = name
@@ -92,6 +95,9 @@ class MapAnything:
                                     specific_pretrained_submodules=specific_pretrained_submodules,
                                     torch_hub_force_reload=torch_hub_force_reload)
         self.precision = precision
+        if head_precision not in ("fp32", "bf16"):
+            raise ValueError(f"head_precision must be 'fp32' or 'bf16', got {head_precision}")
+        self.head_precision = head_precision
         self._sd: Optional[Dict[str, np.ndarray]] = None
         self._engines: Dict[tuple, Any] = {}
         self._device = torch.device("cpu")
@@ -116,7 +122,7 @@ class MapAnything:
                 "(no hub access); download the checkpoint elsewhere and pass its directory")
         with open(os.path.join(path, "config.json")) as f:
             cfg = json.loads(_strip_comments(f.read()))
-        cfg.update({k: v for k, v in kwargs.items() if k in ("precision",)})
+        cfg.update({k: v for k, v in kwargs.items() if k in ("precision", "head_precision", "hip_graphs")})
         model = cls(**cfg)
         st = os.path.join(path, "model.safetensors")
         if os.path.exists(st):
@@ -237,10 +243,10 @@ class MapAnything:
                                "load_synthetic_weights()")
         if self._device.type != "cuda":
             raise nat.NativeError("MapAnything (MI355X engine) runs on a gfx950 device only: call .to('cuda')")
-        key = (str(self._device), prec)
+        key = (str(self._device), prec, self.head_precision)
         if key not in self._engines:
             from .engine import MapaEngine
-            self._engines[key] = MapaEngine(self._sd, self._device, prec, self.info)
+            self._engines[key] = MapaEngine(self._sd, self._device, prec, self.info, heads=self.head_precision)
         return self._engines[key]
 
     def enable_view_sharding(self, group=None, comm=None):
@@ -346,7 +352,7 @@ class MapAnything:
         if (not self.hip_graphs or plan is not None or geo is not None or dpt_chunk is not None
                 or nat._timing is not None or imgs.device.type != "cuda"):
             return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx)
-        key = (eng.precision, tuple(imgs.shape), imgs.device.index)
+        key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index)
         with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
             entry = self._graphs.get(key)
             if entry is None:
@@ -420,12 +426,14 @@ class MapAnything:
 
     def _dpt_chunk(self, memory_efficient: bool):
         """Views per dense-head pass.  memory_efficient_inference mirrors _compute_adaptive_minibatch_size
-        (model.py:1440-1477): 95 % of free HBM over a per-view bound (≈320 MB for this engine's dense head at
-        518², against the reference's 680 MB); otherwise every view in one pass."""
+        (model.py:1440-1477): 95 % of free HBM over a per-view bound (the dense head's peak at 518²: ≈420 MB with
+        fp32-exact split-precision heads — the 518² split operand of the last conv plus its fp32 output — ≈320 MB
+        with bf16 heads; the reference's is 680 MB); otherwise every view in one pass."""
         if not memory_efficient:
             return None
         free = torch.cuda.mem_get_info(self._device)[0]
-        return max(1, int(0.95 * free / (320 * 1024 * 1024)))
+        per_view = 420 if self.head_precision == "fp32" else 320
+        return max(1, int(0.95 * free / (per_view * 1024 * 1024)))
 
     def _local_views(self, views):
         if self._comm is None:

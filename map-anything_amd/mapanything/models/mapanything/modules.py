@@ -143,7 +143,7 @@ class DPTFeature(_EngineModule):
         B, _, h, w = f0.shape
         eng = self._eng()
         with torch.cuda.device(eng.device):
-            rows = [_rows(self._dev(f), eng.lp) for f in (f0, f1, f2, f3)]
+            rows = [eng.head_rows(_rows(self._dev(f), f32)) for f in (f0, f1, f2, f3)]
             _, feat = eng.dpt_feature(rows[0], rows[1], rows[2], rows[3], B, h, w, want_f32=True)
         return DPTFeatureInput(features_upsampled_8x=feat.permute(0, 3, 1, 2).contiguous(),
                                target_output_shape=tuple(head_input.target_output_shape))
@@ -164,10 +164,10 @@ class DPTRegressionProcessor(_EngineModule):
         B, _, hf, wf = x.shape
         eng = self._eng()
         with torch.cuda.device(eng.device):
-            hid = eng.dpt_regress(_rows(self._dev(x), eng.lp), B, hf, wf, H, W)
-            w6 = self._w6.get(eng.precision)
+            hid = eng.dpt_regress(eng.head_rows(_rows(self._dev(x), f32)), B, hf, wf, H, W)
+            w6 = self._w6.get(hid.dtype)
             if w6 is None:
-                w6 = self._w6[eng.precision] = torch.empty(6, 128, dtype=eng.lp, device=eng.device)
+                w6 = self._w6[hid.dtype] = torch.empty(6, 128, dtype=hid.dtype, device=eng.device)
                 nat.convert_rows(eng.w.reg_w6, 128, 6, 128, w6, 128)
             raw = torch.empty(B * H * W, 6, dtype=f32, device=eng.device)
             nat.gemm(hid, w6, B * H * W, 6, 128, bias=eng.w.reg_b6, out_f32=raw)
@@ -215,7 +215,7 @@ class PoseHead(_EngineModule):
         B, _, h, w = x.shape
         eng = self._eng()
         with torch.cuda.device(eng.device):
-            raw = eng.pose(_rows(self._dev(x), eng.lp), B, h * w)
+            raw = eng.pose(eng.head_rows(_rows(self._dev(x), f32)), B, h * w)
         return SummaryTaskOutput(decoded_channels=raw)
 
 

@@ -3,8 +3,13 @@ weights, same seeded inputs) and against the CPU oracle.
 
 Tolerances (rel-L2 per output):
   * precision "fp32" (exact-fp32 MFMA): 1e-4 — the structural proof that every op matches the reference;
-  * precision "bf16" (the reference's own autocast recipe): 3x the reference's own bf16-vs-fp32 deviation
-    measured on the same case (tests/golden/golden_bf16_yardsticks.json), floor 2e-3.
+  * precision "bf16" (the reference's own autocast recipe: bf16 encoder / transformer, fp32 geometric encoders and
+    heads): BF16_FACTOR x the reference's own bf16-vs-fp32 deviation measured on the same case
+    (tests/golden/golden_bf16_yardsticks.json) for the dense per-pixel outputs, floor BF16_FLOOR; the per-view
+    vectors and the scalar scale (SMALL_KEYS: <= 16 numbers per view, so one rel-L2 is one noisy sample of the
+    bf16 rounding walk — measured ratios 0.9-1.6 against the reference's single sample) get SMALL_FACTOR; the
+    achieved rel-L2 and its ratio to the yardstick are printed (pytest -s);
+  * head_precision "bf16" (opt-in fast mode, NOT the reference's recipe): 3x the yardstick, floor 2e-3.
 """
 
 import json
@@ -19,6 +24,14 @@ from conftest import GOLDEN, rel_l2
 pytestmark = pytest.mark.gpu
 
 from tests_helpers import CASES, make_views
+BF16_FACTOR, BF16_FLOOR, SMALL_FACTOR = 1.5, 1e-3, 2.5
+SMALL_KEYS = ("cam_trans", "cam_quats", "metric_scaling_factor", "camera_poses")
+
+
+def _bf16_tol(yard):
+    return lambda k: max(BF16_FLOOR, (SMALL_FACTOR if k in SMALL_KEYS else BF16_FACTOR) * yard[f"out_{k}"])
+
+
 OUT_KEYS = ("pts3d", "ray_directions", "depth_along_ray", "conf", "non_ambiguous_mask_logits", "cam_trans",
             "cam_quats", "metric_scaling_factor", "intrinsics", "camera_poses")
 
@@ -44,7 +57,7 @@ def _yard(name="cfg1_224"):
     return json.load(open(os.path.join(GOLDEN, "golden_bf16_yardsticks.json")))[name]
 
 
-def _compare(preds, g, step, tol_fn):
+def _compare(preds, g, step, tol_fn, yard=None, label=""):
     errs = {}
     for k in OUT_KEYS:
         ref = g[f"out_{k}"]
@@ -53,6 +66,11 @@ def _compare(preds, g, step, tol_fn):
             mine = mine[:, :, ::step, ::step]
         assert mine.shape == ref.shape, (k, mine.shape, ref.shape)
         errs[k] = rel_l2(mine, ref)
+    if yard is not None:
+        print(f"\n[{label}] rel-L2 vs fp32 reference (ratio to the reference's own bf16 deviation):")
+        for k, e in errs.items():
+            y = yard.get(f"out_{k}")
+            print(f"  {k:28s} {e:.3e}" + (f"  yard {y:.3e}  ratio {e / y:.2f}" if y else ""))
     bad = {k: (e, tol_fn(k)) for k, e in errs.items() if not e < tol_fn(k)}
     assert not bad, f"rel-L2 over tolerance: {bad} (all: {errs})"
     return errs
@@ -72,7 +90,22 @@ def test_bf16_mode_within_reference_bf16_yardstick(model, golden, name):
     step = _meta(name)["steps_out_tap_dpt"][0]
     yard = _yard(name)
     preds = model.infer(_views(CASES[name]), apply_mask=False)
-    _compare(preds, g, step, lambda k: max(2e-3, 3.0 * yard[f"out_{k}"]))
+    _compare(preds, g, step, _bf16_tol(yard), yard, f"bf16 {name}")
+
+
+@pytest.mark.parametrize("name", ["cfg1_224", "v2_518"])
+def test_bf16_heads_fast_mode_within_3x_yardstick(golden, name):
+    """head_precision="bf16": the heads on plain bf16 operands (opt-in fast mode, labelled in bench.py)."""
+    from mapanything.models import MapAnything
+    from tests_helpers import released_config
+
+    m = MapAnything(**released_config(), head_precision="bf16").load_synthetic_weights().to("cuda").eval()
+    assert m.engine().heads == "bf16" and not m.engine().hsplit
+    g = golden(name)
+    step = _meta(name)["steps_out_tap_dpt"][0]
+    yard = _yard(name)
+    preds = m.infer(_views(CASES[name]), apply_mask=False)
+    _compare(preds, g, step, lambda k: max(2e-3, 3.0 * yard[f"out_{k}"]), yard, f"bf16-heads {name}")
 
 
 def test_fp32_taps_match_reference(model, golden):
@@ -242,7 +275,7 @@ def test_hip_graph_replay_matches_eager(model, precision):
     assert model.hip_graphs
     g_a = model._run_engine(eng, imgs_a, None, None, None)
     g_b = model._run_engine(eng, imgs_b, None, None, None)  # replay of the graph captured by the first call
-    assert (precision, tuple(imgs_a.shape), imgs_a.device.index) in model._graphs
+    assert (precision, eng.heads, tuple(imgs_a.shape), imgs_a.device.index) in model._graphs
     for k in eager_a:
         assert torch.equal(g_a[k], eager_a[k]), k
         assert torch.equal(g_b[k], eager_b[k]), k
@@ -271,7 +304,7 @@ def test_info_sharing_variants_match_reference(golden, name):
     if "out_pts3d" not in yard:  # no reference bf16 run to measure against: cfg1's yardstick, floor 1e-2
         yard, floor = _yard("cfg1_224"), 1e-2
     preds = m.infer(_views(case), apply_mask=False)
-    _compare(preds, g, step, lambda k: max(floor, 3.0 * yard[f"out_{k}"]))
+    _compare(preds, g, step, lambda k: max(floor, 3.0 * yard[f"out_{k}"]), yard, f"bf16 {name}")
     # intermediate taps of the variant's transformer, fp32 engine
     eng = m.engine("fp32")
     imgs = torch.cat([v["img"] for v in _views(case)], 0).cuda()
