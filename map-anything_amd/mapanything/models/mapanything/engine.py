@@ -616,6 +616,10 @@ class MapaEngine:
         fin_lp = self._hop(L, D)  # the final features feed the DPT and the pose head only
         fin_f32 = self._empty(L, D, dtype=torch.float32)
         self._ln_head(y, L, D, w.aat_nw, w.aat_nb, fin_lp, y_f32=fin_f32)
+        if shard is not None and shard.world > 1:
+            # the scale-token replicas round differently per rank (query blocking, merge order): rank 0's final
+            # scale-token feature is the one every rank's scale head reads (one D-float broadcast)
+            comm.broadcast_(fin_f32[VB * T:], 0)
         if taps is not None:
             taps["aat_final"] = fin_f32[:VB * T]
             taps["scale_token"] = fin_f32[VB * T]
@@ -640,7 +644,10 @@ class MapaEngine:
         strides = dict(batch=1, heads=NH, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
                        v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C, scale=scale)
         overlap = hasattr(comm, "allgather_slots_async") and os.environ.get("MAPA_KV_OVERLAP", "1") != "0"
-        if not overlap:
+        if shard.world == 1:  # a one-rank group: every key is local, nothing to exchange
+            nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
+                          kv_segments=shard.kv_segments(), kind="attention_global", **strides)
+        elif not overlap:
             comm.allgather_slots(kv_full, shard.max_rows)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
                           kv_segments=shard.kv_segments(), kind="attention_global", **strides)

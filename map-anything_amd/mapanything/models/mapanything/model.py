@@ -102,6 +102,7 @@ class MapAnything:
         self._engines: Dict[tuple, Any] = {}
         self._device = torch.device("cpu")
         self._comm = None
+        self._gather = None
         self.training = False
         # Replay the engine's ~2.7k launches per forward from a captured HIP graph (image-only, single device,
         # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
@@ -249,13 +250,18 @@ class MapAnything:
             self._engines[key] = MapaEngine(self._sd, self._device, prec, self.info, heads=self.head_precision)
         return self._engines[key]
 
-    def enable_view_sharding(self, group=None, comm=None):
+    def enable_view_sharding(self, group=None, comm=None, gather_outputs: Optional[str] = None):
         """Shard the views over the ranks of `group` (one process per GPU, torch.distributed over RCCL) or of an
-        explicit communicator (parallel.ThreadComm in tests).  infer()/forward() then run only this rank's
-        views; the returned list holds this rank's views' outputs and None for the others."""
+        explicit communicator (parallel.ThreadComm in tests).  infer()/forward() then run only this rank's views.
+        gather_outputs: None -> the returned list holds this rank's views' outputs and None for the others;
+        "rank0" -> rank 0 returns every view's outputs, as the reference's infer does (model.py:2266-2282), the
+        other ranks their own views'; "all" -> every rank returns every view's outputs."""
         from ...parallel import DistComm
 
+        if gather_outputs not in (None, "rank0", "all"):
+            raise ValueError(f"gather_outputs must be None, 'rank0' or 'all', got {gather_outputs!r}")
         self._comm = comm if comm is not None else DistComm(group)
+        self._gather = gather_outputs
         return self
 
     # ------------------------------------------------------------------------------------------ forward
@@ -324,7 +330,7 @@ class MapAnything:
         geo = self._geo_inputs(views, plan, self._metric_flags(views))
         imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
         raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference))
-        return self._assemble(split_views(raw, len(local), with_post=False), plan, len(views))
+        return self._finish(raw, plan, len(views), with_post=False)
 
     _MAX_GRAPHS = 4
 
@@ -422,7 +428,7 @@ class MapAnything:
                                    edge_depth_threshold=edge_depth_threshold,
                                    apply_confidence_mask=apply_confidence_mask,
                                    confidence_percentile=confidence_percentile)
-        return self._assemble(split_views(post, len(local), with_post=True), plan, len(views))
+        return self._finish(post, plan, len(views), with_post=True)
 
     def _dpt_chunk(self, memory_efficient: bool):
         """Views per dense-head pass.  memory_efficient_inference mirrors _compute_adaptive_minibatch_size
@@ -444,10 +450,20 @@ class MapAnything:
         plan = ShardPlan(len(views), self._comm.world, self._comm.rank, (H // 14) * (W // 14))
         return [views[i] for i in plan.local_views], plan
 
-    @staticmethod
-    def _assemble(local_out, plan, V):
+    def _finish(self, batched, plan, V, with_post):
+        """Batched view-major outputs of this rank -> the reference's per-view list (gathered across ranks when
+        enable_view_sharding(gather_outputs=...) asks for it)."""
         if plan is None:
-            return local_out
+            return split_views(batched, V, with_post)
+        if self._gather is not None and plan.world > 1:
+            dst = 0 if self._gather == "rank0" else None
+            full = {}
+            for k, t in batched.items():
+                # metric_scaling_factor is already the same on every rank (rank 0's scale token, engine.aat)
+                full[k] = t if k == "metric_scaling_factor" else self._comm.gather_views(t, plan.counts, dst)
+            if dst is None or plan.rank == dst:
+                return split_views(full, V, with_post)
+        local_out = split_views(batched, len(plan.local_views), with_post)
         out = [None] * V
         for i, v in enumerate(plan.local_views):
             out[v] = local_out[i]

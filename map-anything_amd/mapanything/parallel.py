@@ -5,8 +5,11 @@ most one: 100 views on 8 ranks -> 13,13,13,13,12,12,12,12).  Every stage of the 
 12 global layers of the alternating-attention transformer (alternating_attention_transformer.py:658-661): there
 each rank computes Q for its own tokens and attends to the K/V of ALL tokens, so K/V are all-gathered once per
 global layer (RCCL over xGMI; backend "nccl" of torch.distributed IS RCCL on ROCm).  The scale token is carried
-by every rank as a bit-identical replica (identical inputs in identical order), and its K/V are contributed once,
-by rank 0.  Nothing else crosses GPUs; outputs stay on the rank that owns the view.
+by every rank as a replica whose K/V are contributed once, by rank 0; the replicas are NOT bit-identical (each
+rank's query block count, attention chunking and partial-merge order differ, so they round differently), so the
+final scale-token feature of rank 0 is broadcast before the scale head: every rank derives the same
+metric_scaling_factor.  Outputs stay on the rank that owns the view, or are gathered (to rank 0 or to every
+rank) when the model asks for it (MapAnything.enable_view_sharding(gather_outputs=...)).
 
 Gathered K/V layout: [world][max_rows][2*C] with rank r's block in slot r (its valid rows first, padding after);
 the attention kernel reads the valid rows through its K/V segment table, so no compaction copy is needed.
@@ -84,10 +87,35 @@ class DistComm:
         mine = full.narrow(0, self.rank * rows_per_slot, rows_per_slot)
         return self.dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
 
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        """In place: every rank's t = rank src's t."""
+        self.dist.broadcast(t, src, group=self.group)
+
+    def gather_views(self, local: torch.Tensor, counts: List[int], dst: Optional[int]) -> Optional[torch.Tensor]:
+        """View-major local rows [counts[rank], ...] -> [sum(counts), ...] in rank order on rank dst (None: on
+        every rank); other ranks get None.  Slots are padded to max(counts) so one collective moves them."""
+        if local.dtype == torch.bool:  # moved as bytes
+            out = self.gather_views(local.view(torch.uint8), counts, dst)
+            return None if out is None else out.view(torch.bool)
+        mx = max(counts)
+        slot = torch.zeros((mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+        slot[:local.shape[0]].copy_(local)
+        if dst is None:
+            full = torch.empty((self.world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+            self.dist.all_gather_into_tensor(full, slot, group=self.group)
+        else:
+            lst = [torch.empty_like(slot) for _ in range(self.world)] if self.rank == dst else None
+            self.dist.gather(slot, lst, dst=dst, group=self.group)
+            if self.rank != dst:
+                return None
+            full = torch.cat(lst, 0)
+        return torch.cat([full[r * mx:r * mx + c] for r, c in enumerate(counts)], 0)
+
 
 class ThreadComm:
     """In-process communicator for tests: P threads (one engine each, same device) exchange slots through a
-    barrier; the exchanged bytes are identical to what all_gather_into_tensor delivers."""
+    barrier; the exchanged bytes are identical to what all_gather_into_tensor delivers.  Each rank thread must
+    launch on its own HIP stream (as separate processes do): the library's scratch buffers are per stream."""
 
     def __init__(self, world: int):
         self.world = world
@@ -115,6 +143,30 @@ class ThreadComm:
         if full.is_cuda:
             torch.cuda.current_stream().synchronize()
         self._barrier.wait()
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        if t.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        self._bufs[self.rank] = t
+        self._barrier.wait()
+        if self.rank != src:
+            t.copy_(self._bufs[src])
+            if t.is_cuda:
+                torch.cuda.current_stream().synchronize()
+        self._barrier.wait()
+
+    def gather_views(self, local: torch.Tensor, counts: List[int], dst: Optional[int]) -> Optional[torch.Tensor]:
+        if local.is_cuda:
+            torch.cuda.current_stream().synchronize()
+        self._bufs[self.rank] = local
+        self._barrier.wait()
+        out = None
+        if dst is None or self.rank == dst:
+            out = torch.cat([self._bufs[r].to(local.device) for r in range(self.world)], 0)
+            if local.is_cuda:
+                torch.cuda.current_stream().synchronize()
+        self._barrier.wait()
+        return out
 
     def allgather_slots_async(self, full: torch.Tensor, rows_per_slot: int):
         """Deferred exchange: this rank's slot is final now (synchronised), the other slots are filled at wait();

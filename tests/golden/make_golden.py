@@ -12,6 +12,9 @@ Cases:
   cfg1_224   2 views 224x224 image-only, fp32 (full outputs + taps)
   v2_518     2 views 518x518 image-only, fp32 (outputs subsampled [::7, ::7] + taps subsampled)
   mm_224     2 views 224x224 + intrinsics + 90 %-sparse depth_z + is_metric_scale (full outputs + taps)
+  cfg2_518   configs[1] itself: 8 views 518x518 image-only, the bench's input seed (outputs [::7, ::7], taps strided)
+  cfg4_518   configs[3] itself: 32 views 518x518 + intrinsics + 90 %-sparse depth_z + is_metric_scale (fp32 only:
+             the CPU bf16 emulation at this size is too slow; the GPU test uses cfg2's bf16 yardstick)
   cfg1_224 under the reference's own bf16 autocast recipe, emulated on CPU (device "cuda" -> "cpu"):
              rel-L2 of bf16 vs fp32 per output key = the bf16 yardstick (golden_bf16_yardstick.json)
 Info-sharing variants (the reference built with a modified info_sharing_config):
@@ -225,7 +228,7 @@ def shrink(d, out_step, tap_step, dpt_step):
     return {k: np.ascontiguousarray(v) for k, v in out.items()}
 
 
-STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8),
+STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "cfg2_518": (7, 6, 24), "cfg4_518": (14, 12, 48), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8),
          "ns_280x392": (4, 2, 8), "one_224": (2, 2, 8), "gat_224": (4, 2, 8), "aatpe_224": (4, 2, 8),
          "aatnoref_224": (4, 2, 8), "aat48_224": (4, 2, 8)}
 
@@ -255,7 +258,10 @@ def main():
         "mixed_224": dict(views=3, h=224, w=224, seed=5, mixed=True),
         "ns_280x392": dict(views=2, h=280, w=392, seed=6),
         "one_224": dict(views=1, h=224, w=224, seed=7, rays_only=True),
+        "cfg2_518": dict(views=8, h=518, w=518, seed=2),
+        "cfg4_518": dict(views=32, h=518, w=518, seed=4, multimodal=True),
     }
+    no_bf16 = ("cfg4_518",)
     only = os.environ.get("GOLDEN_ONLY")
     variants = dict(VARIANTS)
     if only:
@@ -285,6 +291,8 @@ def main():
     ypath = os.path.join(HERE, "golden_bf16_yardsticks.json")
     yards = json.load(open(ypath)) if os.path.exists(ypath) else {}
     for name in cases:
+        if name in no_bf16:
+            continue
         try:
             out16, dt16 = run_case(models[name], cases[name], bf16=True)
         except RuntimeError as e:

@@ -76,7 +76,10 @@ def _compare(preds, g, step, tol_fn, yard=None, label=""):
     return errs
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224"])
+ALL_CASES = ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224", "cfg2_518"]
+
+
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_fp32_mode_matches_reference(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]
@@ -84,7 +87,7 @@ def test_fp32_mode_matches_reference(model, golden, name):
     _compare(preds, g, step, lambda k: 1e-4)
 
 
-@pytest.mark.parametrize("name", ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224"])
+@pytest.mark.parametrize("name", ALL_CASES)
 def test_bf16_mode_within_reference_bf16_yardstick(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]

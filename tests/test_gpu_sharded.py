@@ -12,6 +12,41 @@ from conftest import rel_l2
 pytestmark = pytest.mark.gpu
 
 
+def _run_ranks(comm, world, fn):
+    """fn(rank) on `world` threads (one per rank, all on the test box's one GPU) -> list of results.  Each rank
+    thread launches on its own HIP stream, as separate processes would: the library's per-stream scratch
+    (attention split partials, _native.attention_workspace) must not be shared by concurrently enqueuing ranks."""
+    outs, errs = [None] * world, []
+    streams = [torch.cuda.Stream() for _ in range(world)]
+    torch.cuda.synchronize()
+
+    def run(rank):
+        try:
+            comm.bind(rank)
+            with torch.cuda.stream(streams[rank]):
+                outs[rank] = fn(rank)
+                torch.cuda.current_stream().synchronize()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            raise
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+    assert not errs, errs
+    torch.cuda.synchronize()
+    return outs
+
+
+def _scale_equal_across_ranks(outs):
+    """Every rank's views carry the same metric_scaling_factor tensor value (rank 0's scale token)."""
+    scales = [next(o for o in outs[r] if o is not None)["metric_scaling_factor"].cpu() for r in range(len(outs))]
+    for s_ in scales[1:]:
+        assert torch.equal(s_, scales[0]), scales
+
+
 def _views(n, h, w, seed):
     from mapanything.utils import synthetic
 
@@ -19,7 +54,7 @@ def _views(n, h, w, seed):
 
 
 @pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 2.4e-2)])  # bf16: 3x reference bf16 yardstick
-@pytest.mark.parametrize("world,V", [(2, 3), (3, 3)])
+@pytest.mark.parametrize("world,V", [(1, 2), (2, 3), (3, 3)])
 def test_sharded_equals_single(precision, tol, world, V):
     from mapanything.models import MapAnything
     from mapanything.parallel import ThreadComm
@@ -33,24 +68,7 @@ def test_sharded_equals_single(precision, tol, world, V):
     model._sd = ref_model._sd
     model.enable_view_sharding(comm=comm)
     model.engine()  # build weights once, before the threads start
-    outs = [None] * world
-    errs = []
-
-    def run(rank):
-        try:
-            comm.bind(rank)
-            outs[rank] = model.forward(views)
-        except Exception as e:  # noqa: BLE001
-            errs.append(e)
-            raise
-
-    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=300)
-    assert not errs, errs
-    torch.cuda.synchronize()
+    outs = _run_ranks(comm, world, lambda rank: model.forward(views))
     for r in range(world):
         for v, o in enumerate(outs[r]):
             if o is None:
@@ -58,9 +76,112 @@ def test_sharded_equals_single(precision, tol, world, V):
             for k in ("pts3d", "conf", "cam_quats", "cam_trans", "metric_scaling_factor"):
                 e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
                 assert e < tol, (r, v, k, e)
-    # every view produced exactly once
+    # every view produced exactly once; one metric scale for the whole job
     owners = [sum(outs[r][v] is not None for r in range(world)) for v in range(V)]
     assert owners == [1] * V
+    _scale_equal_across_ranks(outs)
+
+
+def test_sharded_gather_outputs_to_rank0():
+    """enable_view_sharding(gather_outputs="rank0"): rank 0 returns every view (the reference's infer contract,
+    model.py:2266-2282), equal to what the owning ranks computed; other ranks keep their own views."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ThreadComm
+    from tests_helpers import released_config
+
+    world, V = 2, 3
+    views = _views(V, 224, 224, seed=13)
+    base = MapAnything(**released_config()).load_synthetic_weights().to("cuda")
+    outs = {}
+    for mode in (None, "rank0"):
+        comm = ThreadComm(world)
+        model = MapAnything(**released_config()).to("cuda")
+        model._sd = base._sd
+        model.enable_view_sharding(comm=comm, gather_outputs=mode)
+        model.engine()
+        outs[mode] = _run_ranks(comm, world, lambda rank: model.infer(views))
+    own = outs[None]
+    full = outs["rank0"][0]
+    assert all(o is not None for o in full)
+    for v in range(V):
+        owner = next(r for r in range(world) if own[r][v] is not None)
+        for k in ("pts3d", "mask", "conf", "intrinsics", "camera_poses", "img_no_norm", "depth_z"):
+            assert torch.equal(full[v][k], own[owner][v][k]), (v, k)
+    assert outs["rank0"][1][0] is None and outs["rank0"][1][2] is not None
+
+
+def test_cfg3_layout_100_views_on_8_ranks():
+    """configs[2]'s shard layout: 100 views at 518x518 over 8 ranks (13,13,13,13,12,12,12,12; per global layer
+    each rank's 13*1369+1-row K/V slot all-gathered, 136 901 keys) equals the single-GPU run of the same job, and
+    every rank derives the same metric scale.  bf16 (the bench recipe); the ranks are 8 threads on one GPU."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ShardPlan, ThreadComm
+    from tests_helpers import released_config
+
+    world, V = 8, 100
+    assert ShardPlan(V, world, 0, 1369).counts == [13, 13, 13, 13, 12, 12, 12, 12]
+    views = _views(V, 518, 518, seed=21)
+    ref_model = MapAnything(**released_config()).load_synthetic_weights().to("cuda")
+    ref = ref_model.forward(views)
+    ref = [{k: ref[v][k].float().cpu() for k in ("pts3d", "conf", "cam_quats", "cam_trans",
+                                                 "metric_scaling_factor")} for v in range(V)]
+    torch.cuda.empty_cache()
+    comm = ThreadComm(world)
+    model = MapAnything(**released_config()).to("cuda")
+    model._sd = ref_model._sd
+    del ref_model
+    model.enable_view_sharding(comm=comm)
+    model.engine()
+    outs = _run_ranks(comm, world, lambda rank: model.forward(views))
+    worst = {}
+    for r in range(world):
+        for v, o in enumerate(outs[r]):
+            if o is None:
+                continue
+            for k in ref[v]:
+                worst[k] = max(worst.get(k, 0.0), rel_l2(o[k].float().cpu(), ref[v][k]))
+    print("\n[cfg3 layout] worst per-view rel-L2 sharded vs single:", worst)
+    assert all(e < 2.4e-2 for e in worst.values()), worst
+    _scale_equal_across_ranks(outs)
+
+
+def test_memory_efficient_sharded_equals_single():
+    """configs[4]'s path at test size: memory_efficient_inference=True (dense head over view chunks, model.py:
+    1479-1516) combined with view sharding (2 ranks), against the unsharded, unchunked run (fp32, 2e-5)."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ThreadComm
+    from tests_helpers import released_config
+
+    world, V = 2, 5
+    views = _views(V, 224, 224, seed=14)
+    ref_model = MapAnything(**released_config(), precision="fp32").load_synthetic_weights().to("cuda")
+    ref = ref_model.infer(views, use_amp=False, apply_mask=False)
+    comm = ThreadComm(world)
+    model = MapAnything(**released_config(), precision="fp32").to("cuda")
+    model._sd = ref_model._sd
+    model.enable_view_sharding(comm=comm)
+    model.engine()
+    chunks = []
+    real = model._dpt_chunk
+
+    def small_chunks(me):  # free HBM would allow every view in one pass: force 2-view chunks
+        c = real(me)
+        chunks.append(c)
+        return 2 if me else c
+
+    model._dpt_chunk = small_chunks
+    outs = _run_ranks(comm, world, lambda rank: model.infer(views, use_amp=False, apply_mask=False,
+                                                            memory_efficient_inference=True))
+    assert chunks and all(c is not None and c >= 1 for c in chunks)
+    for r in range(world):
+        for v, o in enumerate(outs[r]):
+            if o is None:
+                continue
+            for k in ("pts3d", "conf", "cam_quats", "metric_scaling_factor", "intrinsics"):
+                e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
+                assert e < 2e-5, (r, v, k, e)
+            flips = (o["non_ambiguous_mask"].cpu() != ref[v]["non_ambiguous_mask"].cpu()).float().mean()
+            assert flips < 1e-4, (r, v, flips)
 
 
 @pytest.mark.parametrize("precision,tol", [("fp32", 2e-5)])
@@ -80,25 +201,8 @@ def test_sharded_geometric_inputs_equal_single(precision, tol):
     model._sd = ref_model._sd
     model.enable_view_sharding(comm=comm)
     model.engine("fp32")
-    outs = [None] * world
-    errs = []
     per_rank_views = [make_views(case) for _ in range(world)]
-
-    def run(rank):
-        try:
-            comm.bind(rank)
-            outs[rank] = model.infer(per_rank_views[rank], use_amp=False, apply_mask=False)
-        except Exception as e:  # noqa: BLE001
-            errs.append(e)
-            raise
-
-    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=300)
-    assert not errs, errs
-    torch.cuda.synchronize()
+    outs = _run_ranks(comm, world, lambda rank: model.infer(per_rank_views[rank], use_amp=False, apply_mask=False))
     for r in range(world):
         for v, o in enumerate(outs[r]):
             if o is None:
@@ -127,23 +231,7 @@ def test_sharded_variants_equal_single(variant):
     model._sd = ref_model._sd
     model.enable_view_sharding(comm=comm)
     model.engine()
-    outs, errs = [None] * world, []
-
-    def run(rank):
-        try:
-            comm.bind(rank)
-            outs[rank] = model.forward(views)
-        except Exception as e:  # noqa: BLE001
-            errs.append(e)
-            raise
-
-    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(timeout=300)
-    assert not errs, errs
-    torch.cuda.synchronize()
+    outs = _run_ranks(comm, world, lambda rank: model.forward(views))
     for r in range(world):
         for v, o in enumerate(outs[r]):
             if o is None:

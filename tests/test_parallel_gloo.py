@@ -116,3 +116,60 @@ def test_sharded_global_attention_gloo(world, V, overlap):
     for rank, err, same_set in res:
         assert same_set, f"rank {rank}: gathered K/V set differs from the global token set"
         assert err < 1e-5, f"rank {rank}: sharded attention differs by {err}"
+
+
+def _gather_worker(rank, world, port, q):
+    """DistComm.broadcast_ (the scale-token feature) and gather_views (outputs to rank 0 / to every rank) over a
+    real gloo group, and MapAnything._finish assembling the reference's per-view list from them."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mapanything.models.mapanything.model import MapAnything
+
+        V = 7
+        plan = ShardPlan(V, world, rank, 4)
+        comm = DistComm()
+        tok = torch.full((1, 8), float(rank + 1))
+        comm.broadcast_(tok, 0)
+        ok_bcast = bool((tok == 1.0).all())
+        lv = list(plan.local_views)
+        local = {"pts3d": torch.stack([torch.full((1, 2, 2, 3), float(v)) for v in lv], 0).view(len(lv), 2, 2, 3),
+                 "non_ambiguous_mask": torch.tensor([[[v % 2 == 0]] for v in lv]).view(len(lv), 1, 1),
+                 "metric_scaling_factor": torch.ones(1, 1)}
+        m = MapAnything.__new__(MapAnything)  # host glue only: no weights, no device
+        m._comm = comm
+        res = {}
+        for mode in ("rank0", "all", None):
+            m._gather = mode
+            out = m._finish(dict(local), plan, V, with_post=False)
+            got = [None if o is None else float(o["pts3d"].flatten()[0]) for o in out]
+            masks = [None if o is None else bool(o["non_ambiguous_mask"].flatten()[0]) for o in out]
+            res[mode] = (got, masks)
+        q.put((rank, ok_bcast, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_scale_token_broadcast_and_output_gather_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    V = 7
+    every = [float(v) for v in range(V)]
+    every_mask = [v % 2 == 0 for v in range(V)]
+    for rank, ok_bcast, r in res:
+        assert ok_bcast, rank
+        plan = ShardPlan(V, world, rank, 4)
+        own = [float(v) if v in plan.local_views else None for v in range(V)]
+        assert r["all"] == (every, every_mask)
+        assert r["rank0"][0] == (every if rank == 0 else own)
+        assert r[None][0] == own

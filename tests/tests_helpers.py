@@ -20,6 +20,7 @@ CASES = {
     "mixed_224": dict(views=3, h=224, w=224, seed=5, mixed=True),
     "ns_280x392": dict(views=2, h=280, w=392, seed=6),
     "one_224": dict(views=1, h=224, w=224, seed=7, rays_only=True),
+    "cfg2_518": dict(views=8, h=518, w=518, seed=2),   # configs[1] at its real size (the bench's input seed)
 }
 
 
