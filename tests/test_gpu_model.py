@@ -76,7 +76,10 @@ def _compare(preds, g, step, tol_fn, yard=None, label=""):
     return errs
 
 
-ALL_CASES = ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224", "cfg2_518"]
+ALL_CASES = ["cfg1_224", "v2_518", "mm_224", "mixed_224", "ns_280x392", "one_224", "cfg2_518", "cfg4_518"]
+# cases whose reference bf16 run was not generated (the CPU bf16 emulation at 32 x 518^2 takes too long): the
+# nearest yardstick (cfg2: 8 views 518^2) with factor 3 (the bf16 deviation grows with the global key count)
+YARD_FALLBACK = {"cfg4_518": ("cfg2_518", 3.0)}
 
 
 @pytest.mark.parametrize("name", ALL_CASES)
@@ -91,9 +94,15 @@ def test_fp32_mode_matches_reference(model, golden, name):
 def test_bf16_mode_within_reference_bf16_yardstick(model, golden, name):
     g = golden(name)
     step = _meta(name)["steps_out_tap_dpt"][0]
-    yard = _yard(name)
+    if name in YARD_FALLBACK:
+        src, factor = YARD_FALLBACK[name]
+        yard = _yard(src)
+        tol = lambda k: max(BF16_FLOOR, factor * yard[f"out_{k}"])  # noqa: E731
+    else:
+        yard = _yard(name)
+        tol = _bf16_tol(yard)
     preds = model.infer(_views(CASES[name]), apply_mask=False)
-    _compare(preds, g, step, _bf16_tol(yard), yard, f"bf16 {name}")
+    _compare(preds, g, step, tol, yard, f"bf16 {name}")
 
 
 @pytest.mark.parametrize("name", ["cfg1_224", "v2_518"])

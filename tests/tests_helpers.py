@@ -21,6 +21,8 @@ CASES = {
     "ns_280x392": dict(views=2, h=280, w=392, seed=6),
     "one_224": dict(views=1, h=224, w=224, seed=7, rays_only=True),
     "cfg2_518": dict(views=8, h=518, w=518, seed=2),   # configs[1] at its real size (the bench's input seed)
+    # configs[3] at its real size: 32 views + intrinsics + 90 %-sparse depth + metric flag
+    "cfg4_518": dict(views=32, h=518, w=518, seed=4, multimodal=True),
 }
 
 
