@@ -274,6 +274,14 @@ int mapa_add_view_vectors(float* x, int T, int C, int nviews, const float* vecs,
 int mapa_view_rays(const float* K, const float* rays_in, const float* depth_z, int n, int H, int W, float* rays,
                    float* depth_along_ray, mapa_stream_t stream);
 
+/* RoPE-2D in place (uniception croco RoPE2D / cuRoPE2D forward: pos_embed.py:101-155, curope/kernels.cu:17-82):
+ * tokens (B, H, N, D) bf16 or f32 with element strides sb, sh, sn (head dim contiguous, D % 16 == 0), positions
+ * int64 (B, N, 2) = (y, x).  Head dim [u_y | v_y | u_x | v_x] (quarters Q = D/4); pair j of each half rotates by
+ * pos * f0 / base^(j/Q): u' = u cos - v sin, v' = v cos + u sin (fp32 math).  Also usable on the packed qkv buffer
+ * (sn = 3*C, sh = 64) before the attention. */
+int mapa_rope2d(void* tokens, int dtype, int B, int H, int N, int D, int64_t sb, int64_t sh, int64_t sn,
+                const int64_t* positions, float base, float f0, mapa_stream_t stream);
+
 /* dst[i] += src[i] (n % 4 == 0) */
 int mapa_add_f32(float* dst, const float* src, int64_t n, mapa_stream_t stream);
 

@@ -29,7 +29,7 @@ EXPORTED = (
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
-    "mapa_normalize_image", "mapa_normal_cos_threshold",
+    "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d",
 )
 
 
@@ -118,6 +118,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_attn_merge.argtypes = [vp, vp, vp, vp, vp, vp, i, i, i, i64, vp]
     L.mapa_dense_adaptor.argtypes = [vp, i, i64, vp, vp, vp, vp, vp]
     L.mapa_normalize_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
+    L.mapa_rope2d.argtypes = [vp, i, i, i, i, i, i64, i64, i64, vp, f, f, vp]
     _lib = L
     return L
 
@@ -201,6 +202,7 @@ def _toc(tok, kind, flops=0.0):
 _WS_NEED = {}
 _WS = {}
 _AWS = {}
+_WS_RETIRED = []  # grown-out GEMM workspaces, kept alive for graphs captured against them
 
 
 def gemm_workspace(nbytes: int) -> torch.Tensor:
@@ -211,6 +213,9 @@ def gemm_workspace(nbytes: int) -> torch.Tensor:
     key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
+        if ws is not None:
+            # a captured HIP graph may hold the old buffer's address: never free a workspace once used
+            _WS_RETIRED.append(ws)
         ws = _WS[key] = torch.zeros(max(nbytes, 0 if ws is None else ws.numel()), dtype=torch.uint8,
                                     device="cuda")
     return ws
@@ -464,3 +469,11 @@ def normalize_image(hwc_u8, n, H, W, mean, std, out):
     s = (ctypes.c_float * 3)(*[float(x) for x in std])
     check(lib().mapa_normalize_image(ptr(hwc_u8), n, H, W, ctypes.cast(m, ctypes.c_void_p),
                                      ctypes.cast(s, ctypes.c_void_p), ptr(out), stream()), "mapa_normalize_image")
+
+
+def rope2d(tokens, positions, B, H, N, D, sb, sh, sn, base, f0):
+    """In-place RoPE-2D on tokens (B, H, N, D) with element strides (sb, sh, sn); positions int64 (B, N, 2)."""
+    if positions.dtype != torch.int64 or not positions.is_contiguous():
+        raise NativeError("rope2d: positions must be contiguous int64 (B, N, 2)")
+    check(lib().mapa_rope2d(ptr(tokens), dt_code(tokens.dtype), B, H, N, D, sb, sh, sn, ptr(positions), float(base),
+                            float(f0), stream()), "mapa_rope2d")

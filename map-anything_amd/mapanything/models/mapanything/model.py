@@ -29,7 +29,7 @@ import torch
 from ... import _native as nat
 from ...utils.inference import (postprocess_outputs, preprocess_input_views_for_inference,
                                 validate_input_views_for_inference)
-from .spec import InfoSharingSpec, aliases, canonical_spec
+from .spec import InfoSharingSpec, aliases, canonical_spec, full_spec
 
 SUPPORTED = dict(
     encoder="dinov2", size="large", info_sharing=("alternating_attention", "global_attention"),
@@ -167,6 +167,41 @@ class MapAnything:
         self._graphs.clear()
         self._modules.clear()
         return self
+
+    def state_dict(self) -> "OrderedDict[str, torch.Tensor]":
+        """nn.Module.state_dict() of the reference model (model.py:96): every key the reference's state dict has —
+        the canonical tensors and the alias keys of the shared DPT modules (`dense_head.0/1.*`,
+        `scratch.layer_rn.N`, `input_process.N.1`), which share storage as in the reference — as fp32 CPU tensors."""
+        if self._sd is None:
+            raise RuntimeError("no weights loaded")
+        canon = {k: torch.from_numpy(v) for k, v in self._sd.items()}
+        al = aliases(self.info)
+        return OrderedDict((name, canon[al.get(name, name)]) for name, _ in full_spec(self.info))
+
+    def named_parameters(self):
+        """(name, tensor) once per distinct tensor (nn.Module de-duplicates shared parameters the same way)."""
+        if self._sd is None:
+            raise RuntimeError("no weights loaded")
+        for name, _ in canonical_spec(self.info):
+            yield name, torch.from_numpy(self._sd[name])
+
+    def parameters(self):
+        for _, t in self.named_parameters():
+            yield t
+
+    def save_pretrained(self, save_directory: str):
+        """PyTorchModelHubMixin.save_pretrained layout: config.json (the constructor config) + model.safetensors
+        (one entry per distinct tensor, as safetensors' save_model de-duplicates shared storage)."""
+        from safetensors.numpy import save_file
+
+        if self._sd is None:
+            raise RuntimeError("no weights loaded")
+        os.makedirs(save_directory, exist_ok=True)
+        cfg = {k: v for k, v in self.class_init_args.items() if v is not None}
+        with open(os.path.join(save_directory, "config.json"), "w") as f:
+            json.dump(cfg, f, indent=1)
+        save_file({k: np.ascontiguousarray(v) for k, v in self._sd.items()},
+                  os.path.join(save_directory, "model.safetensors"))
 
     def load_synthetic_weights(self):
         """Named-PRNG synthetic checkpoint (mapanything/utils/synthetic.py) — bench/tests only."""
@@ -374,13 +409,15 @@ class MapAnything:
                 # are the ones the graph uses (no allocation or zero-fill inside the capture)
                 with torch.cuda.graph(graph, stream=side):
                     static_out = eng.run(static_in, pe_idx=static_pe)
-                entry = (graph, static_in, static_out, static_pe)
+                # the side stream is kept with the graph: its handle keys the per-stream workspaces the graph
+                # captured (_native._WS/_AWS), so it must not be destroyed and its handle reused while the graph lives
+                entry = (graph, static_in, static_out, static_pe, side)
                 self._graphs[key] = entry
                 while len(self._graphs) > self._MAX_GRAPHS:
                     self._graphs.popitem(last=False)
             else:
                 self._graphs.move_to_end(key)
-            graph, static_in, static_out, static_pe = entry
+            graph, static_in, static_out, static_pe, _side = entry
             static_in.copy_(imgs)
             if static_pe is not None:
                 static_pe.copy_(pe_idx)

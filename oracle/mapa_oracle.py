@@ -677,3 +677,30 @@ def preprocess_views(views):
             pv["ray_directions_cam"] = pv.pop("ray_directions")
         out.append(pv)
     return out
+
+
+def rope2d(tokens, positions, base=100.0):
+    """RoPE2D forward, restating uniception/models/libs/croco/pos_embed.py:101-155 (the reference's pure-torch
+    fallback; curope/kernels.cu:17-82 computes the same rotation): tokens (B, H, N, D) fp32, positions (B, N, 2)
+    int64 (y, x) -> rotated copy.  Each half of the head dim (y half, x half) is rotated with rotate_half by
+    angles pos * inv_freq, inv_freq[j] = 1 / base^(2j / (D/2)) for j < D/4, the cos/sin tables duplicated."""
+    tokens = torch.as_tensor(tokens, dtype=torch.float32)
+    positions = torch.as_tensor(positions, dtype=torch.int64)
+    D = tokens.shape[3] // 2
+    seq = int(positions.max()) + 1
+    inv_freq = 1.0 / (base ** (torch.arange(0, D, 2).float() / D))
+    freqs = torch.einsum("i,j->ij", torch.arange(seq, dtype=inv_freq.dtype), inv_freq)
+    freqs = torch.cat((freqs, freqs), dim=-1)
+    cos, sin = freqs.cos(), freqs.sin()
+
+    def rot_half(x):
+        x1, x2 = x[..., : x.shape[-1] // 2], x[..., x.shape[-1] // 2:]
+        return torch.cat((-x2, x1), dim=-1)
+
+    def rope1d(t, p1):
+        c = torch.nn.functional.embedding(p1, cos)[:, None, :, :]
+        s = torch.nn.functional.embedding(p1, sin)[:, None, :, :]
+        return t * c + rot_half(t) * s
+
+    y, x = tokens.chunk(2, dim=-1)
+    return torch.cat((rope1d(y, positions[:, :, 0]), rope1d(x, positions[:, :, 1])), dim=-1)

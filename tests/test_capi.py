@@ -55,3 +55,33 @@ def test_product_path_fails_loudly_without_gpu():
 
     with pytest.raises(_native.NativeError):
         _native.lib()
+
+
+def test_descriptor_layouts_match_header(tmp_path):
+    """ctypes GemmDesc / AttnDesc field offsets equal the C compiler's offsetof for include/mapa.h (the split
+    operand outputs were appended to mapa_gemm_desc; a mismatch would shift every field after it)."""
+    import shutil
+    import subprocess
+
+    from mapanything import _native
+
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    fields = {"mapa_gemm_desc": _native.GemmDesc, "mapa_attn_desc": _native.AttnDesc}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "mapa.h"', "int main(void) {"]
+    for cname, cls in fields.items():
+        lines.append(f'printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            lines.append(f'printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    lines.append("return 0; }")
+    src = tmp_path / "off.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "off"
+    subprocess.run([cc, "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {(a, b): int(c) for a, b, c in (ln.split() for ln in out if ln)}
+    for cname, cls in fields.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
+        for fname, _ in cls._fields_:
+            assert got[(cname, fname)] == getattr(cls, fname).offset, (cname, fname)

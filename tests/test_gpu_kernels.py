@@ -542,3 +542,44 @@ def test_bilinear_split_output(nat):
     nat.bilinear_ac(x, n, IH, IW, C, OH, OW, OH, OW, yf)
     nat.bilinear_ac(x, n, IH, IW, C, OH, OW, OH, OW, ys, split_out=True)
     assert torch.equal(ys, _split_expect(yf))
+
+
+# ------------------------------------------------------------------------------------------- RoPE-2D
+def test_rope2d_matches_reference_fixture():
+    """uniception croco RoPE2D (pos_embed.py:101-155 / curope kernels.cu:17-82) through the RoPE2D op: fp32 to
+    within the sincos rounding of the reference's own outputs (fixture from the reference, make_rope_golden.py)."""
+    import os
+
+    from conftest import GOLDEN
+    from uniception.models.libs.croco.pos_embed import RoPE2D
+
+    g = np.load(os.path.join(GOLDEN, "golden_rope2d.npz"))
+    t = torch.from_numpy(g["grid_tokens"]).cuda()
+    out = RoPE2D(freq=100.0)(t, torch.from_numpy(g["grid_pos"]).cuda())
+    assert out.data_ptr() == t.data_ptr()  # in place, as cuRoPE2D
+    assert (out.cpu() - torch.from_numpy(g["grid_out"])).abs().max() < 2e-5
+    for base in (100, 10000):
+        t = torch.from_numpy(g["rand_tokens"]).cuda()
+        RoPE2D(freq=float(base))(t, torch.from_numpy(g["rand_pos"]).cuda())
+        assert (t.cpu() - torch.from_numpy(g[f"rand_out_base{base}"])).abs().max() < 2e-5, base
+
+
+def test_rope2d_bf16_on_packed_qkv_rows(nat):
+    """The same rotation in place on the Q and K column blocks of a packed [rows][3C] bf16 qkv buffer (what an
+    attention with RoPE positions reads), V untouched; against the oracle on the fp32 values."""
+    from oracle.mapa_oracle import rope2d
+
+    N, H = 300, 12
+    C = 64 * H
+    qkv = _rand(N, 3 * C, seed=51).to(torch.bfloat16)
+    pos = torch.randint(0, 40, (1, N, 2), generator=torch.Generator().manual_seed(3)).cuda()
+    ref = qkv.float().cpu()
+    work = qkv.clone()
+    for blk in (0, 1):  # Q then K: (B=1, H, N, 64) views with strides (., 64, 3C)
+        nat.rope2d(work[:, blk * C:], pos, 1, H, N, 64, 0, 64, 3 * C, 100.0, 1.0)
+    for blk in (0, 1):
+        x = ref[:, blk * C:(blk + 1) * C].view(N, H, 64).permute(1, 0, 2)[None]
+        want = rope2d(x, pos.cpu())[0].permute(1, 0, 2).reshape(N, C)
+        got = work[:, blk * C:(blk + 1) * C].float().cpu()
+        assert rel_l2(got, want) < 4e-3
+    assert torch.equal(work[:, 2 * C:], qkv[:, 2 * C:])

@@ -349,3 +349,18 @@ def test_random_view_pe_indices_follow_the_reference_draw():
     torch.manual_seed(123)
     expect = torch.cat([torch.zeros(1, dtype=torch.int64), torch.randint(low=1, high=1000, size=(4,))])
     assert torch.equal(rows, expect)
+
+
+def test_from_pretrained_checkpoint_runs_identically(model, tmp_path):
+    """save_pretrained -> from_pretrained (config.json + model.safetensors under the reference's names) gives the
+    same engine outputs as the in-memory synthetic checkpoint, bit for bit."""
+    from mapanything.models import MapAnything
+
+    model.save_pretrained(str(tmp_path))
+    m = MapAnything.from_pretrained(str(tmp_path)).to("cuda").eval()
+    views = _views(CASES["cfg1_224"])
+    a = model.infer(views, apply_mask=False)
+    b = m.infer(views, apply_mask=False)
+    for x, y in zip(a, b):
+        for k in ("pts3d", "conf", "cam_quats", "metric_scaling_factor"):
+            assert torch.equal(x[k], y[k]), k

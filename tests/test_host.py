@@ -106,3 +106,56 @@ def test_module_surface_is_exposed():
                  "pose_head", "pose_adaptor", "scale_head", "scale_adaptor", "fusion_norm_layer"):
         assert callable(getattr(m, name)), name
     assert m.encoder is m.encoder and m.info_sharing.indices == (11, 17)
+
+
+def _released_model(**kw):
+    from mapanything.models import MapAnything
+    from tests_helpers import released_config
+
+    return MapAnything(**released_config(), **kw)
+
+
+@pytest.mark.parametrize("layout", ["all_880_keys", "deduplicated"])
+def test_from_pretrained_local_safetensors(tmp_path, layout):
+    """MapAnything.from_pretrained(local_dir) reads config.json + model.safetensors written under the reference's
+    state-dict names (model.py:17, 96): either every one of the 880 keys (aliases included, as nn.Module's
+    state_dict lists them) or one name per shared tensor (safetensors' save_model de-duplication).  The loaded
+    weights equal the synthetic checkpoint exactly."""
+    from safetensors.numpy import save_file
+
+    from mapanything.models import MapAnything
+    from mapanything.models.mapanything.spec import aliases
+    from tests_helpers import released_config
+
+    src = _released_model().load_synthetic_weights()
+    sd = src.state_dict()
+    ref_names = [k for k, _ in json.load(open(os.path.join(GOLDEN, "ref_state_dict_spec.json")))]
+    assert list(sd.keys()) == ref_names or sorted(sd.keys()) == sorted(ref_names)
+    if layout == "deduplicated":
+        al = aliases()
+        sd = {k: v for k, v in sd.items() if k not in al}
+    save_file({k: v.numpy().copy() for k, v in sd.items()}, str(tmp_path / "model.safetensors"))
+    with open(tmp_path / "config.json", "w") as f:
+        json.dump(released_config(), f)
+    m = MapAnything.from_pretrained(str(tmp_path), head_precision="bf16")
+    assert m.head_precision == "bf16"
+    assert set(m._sd) == set(src._sd)
+    for k in src._sd:
+        assert np.array_equal(m._sd[k], src._sd[k]), k
+    # state_dict aliases share storage with their canonical tensor, as in the reference
+    full = m.state_dict()
+    assert full["dense_head.0.scratch.layer1_rn.weight"].data_ptr() == \
+        full["dpt_feature_head.scratch.layer1_rn.weight"].data_ptr()
+    assert len(list(m.parameters())) == len(src._sd)
+
+
+def test_save_pretrained_round_trip(tmp_path):
+    from mapanything.models import MapAnything
+
+    src = _released_model().load_synthetic_weights()
+    src.save_pretrained(str(tmp_path))
+    m = MapAnything.from_pretrained(str(tmp_path))
+    for k in src._sd:
+        assert np.array_equal(m._sd[k], src._sd[k]), k
+    with pytest.raises(FileNotFoundError):
+        MapAnything.from_pretrained(str(tmp_path / "missing"))

@@ -70,3 +70,17 @@ def test_oracle_matches_reference(oracle, golden, name):
         assert err < TOL, f"{name}:{key} rel-L2 {err:.3e}"
         checked += 1
     assert checked >= 15
+
+
+def test_oracle_rope2d_matches_reference_fixture():
+    """oracle.rope2d restates the reference's RoPE2D (pos_embed.py:101-155); fixture from the reference itself
+    (tests/golden/make_rope_golden.py)."""
+    import numpy as np
+
+    from oracle.mapa_oracle import rope2d
+
+    g = np.load(os.path.join(GOLDEN, "golden_rope2d.npz"))
+    assert np.array_equal(rope2d(g["grid_tokens"], g["grid_pos"]).numpy(), g["grid_out"])
+    for base in (100, 10000):
+        got = rope2d(g["rand_tokens"], g["rand_pos"], base=float(base)).numpy()
+        assert np.array_equal(got, g[f"rand_out_base{base}"]), base
