@@ -301,11 +301,17 @@ static int forced_variant() {
 // automatically: on the path shapes the data-parallel kernels measured faster (2580/2581), or equal within noise at
 // the bench level (2582, tail-only stream-K: every full wave of 256x128 tiles data-parallel, only the last partial
 // wave split; enc.qkv 108 -> 97 us and aat.fc1 77 -> 75 us in isolation, 266 vs 266 views/s in the bench).
+// Automatic stream-K: problems with fewer 256x128 tiles than CUs and a long K (the fp32-exact split-precision DPT
+// convs at 19x19 and 37x37: K = 27*C = 6912..20736, M = views*361 or views*1369) leave most of the chip idle in
+// the data-parallel schedule; splitting K over the persistent grid measured 1.5-3.2x faster (kbench, 8 views:
+// layer4_rn 392 -> 122 us, input_process.3 conv 394 -> 177, layer3_rn 194 -> 102, refinenet3/4 convs 142 -> 100).
 int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   const int f = forced_variant();
   if (f) return f >= 2580 && f <= 2582 ? f : 0;
-  (void)dtype; (void)conv; (void)M; (void)N; (void)K;
-  return 0;
+  if (dtype != MAPA_BF16) return 0;
+  const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
+  (void)conv;
+  return (big_tiles < 256 && K >= 4096) ? 2580 : 0;
 }
 
 }  // namespace mapa_gemm_impl

@@ -268,8 +268,10 @@ def test_memory_efficient_dense_head_chunks_match(model):
     imgs = torch.cat([v["img"] for v in _views(dict(views=3, h=224, w=224, seed=9))], 0).cuda()
     full = eng.run(imgs)
     part = eng.run(imgs, dpt_chunk=2)
+    # the fp32-exact head convs take K-split (stream-K) schedules whose split points depend on the chunk's row
+    # count, so chunked and unchunked results agree to fp32 summation-order rounding, not bit for bit
     for k in ("pts3d", "conf", "depth_along_ray", "non_ambiguous_mask_logits"):
-        assert rel_l2(part[k].float().cpu().numpy(), full[k].float().cpu().numpy()) < 1e-6, k
+        assert rel_l2(part[k].float().cpu().numpy(), full[k].float().cpu().numpy()) < 2e-5, k
     out = model.infer(_views(dict(views=3, h=224, w=224, seed=9)), memory_efficient_inference=True)
     assert len(out) == 3 and out[0]["pts3d"].shape == (1, 224, 224, 3)
 

@@ -29,6 +29,13 @@ if ONLY:
     GEMMS = [g for g in GEMMS if g[0] in ONLY.split(",")]
 CONVS = [("rn1.c@148", V, 148, 148, 256, 256), ("reg.c2@518", V, 518, 518, 128, 128),
          ("reg.c1@296", V, 296, 296, 256, 128), ("rn2.c@74", V, 74, 74, 256, 256)]
+if os.environ.get("KB_CONVS"):  # "name,n,H,W,C,Co;..." ad-hoc 3x3 conv shapes (C = per-pixel operand width)
+    CONVS = [(f[0], *map(int, f[1:])) for f in (t.split(",") for t in os.environ["KB_CONVS"].split(";"))]
+if os.environ.get("KB_HEADS"):  # the split-precision (3C-wide operand) head convs at 8 views
+    CONVS = [("l1rn@148", V, 148, 148, 288, 256), ("l2rn@74", V, 74, 74, 576, 256), ("l3rn@37", V, 37, 37, 1152, 256),
+             ("l4rn@19", V, 19, 19, 2304, 256), ("rn4@19", V, 19, 19, 768, 256), ("rn3@37", V, 37, 37, 768, 256),
+             ("rn2@74", V, 74, 74, 768, 256), ("rn1@148", V, 148, 148, 768, 256), ("reg1@296", V, 296, 296, 768, 128),
+             ("reg2@518", V, 518, 518, 384, 128)]
 if ONLY:
     CONVS = [c for c in CONVS if c[0] in ONLY.split(",")]
 
@@ -73,7 +80,11 @@ def main():
             M = n * H * W_
             for var in VARIANTS:
                 nat.gemm_set_variant(var)
-                ms = timeit(lambda: nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1)), reps)
+                try:
+                    ms = timeit(lambda: nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1)), reps)
+                except nat.NativeError as e:
+                    print(f"conv {name:10s} v{var:<4d}: {e}", flush=True)
+                    continue
                 print(f"conv {name:10s} v{var:<4d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
                       f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
             nat.gemm_set_variant(0)
