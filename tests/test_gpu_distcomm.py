@@ -1,0 +1,40 @@
+"""Two processes (torch.distributed.run children of this test, both on the box's one GPU, gloo process group)
+drive MapAnything.enable_view_sharding() through the real DistComm: the asynchronous all-gather handle of the
+overlapped global layers, the rank-0 scale-token broadcast and the rank-0 output gather (tests/dist_worker.py).
+RCCL itself refuses two ranks on one device, so the group is gloo here; the code path above the collective calls is
+the production one."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_process_view_sharding_over_distcomm(tmp_path):
+    prefix = str(tmp_path / "res")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "dist_worker.py"), prefix]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = [json.load(open(f"{prefix}.{k}.json")) for k in range(2)]
+    for ov in ("1", "0"):
+        s = res[0][f"scales_{ov}"]
+        assert s[0] == s[1], s  # one metric scale on every rank (rank 0's scale token)
+        assert res[0][f"n_views_{ov}"] == 3 and res[1][f"n_views_{ov}"] == 1  # gathered on rank 0 only
+        err = res[0][f"err_{ov}"]
+        assert all(e < 2e-5 for e in err.values()), (ov, err)
