@@ -22,7 +22,7 @@ extern "C" {
 
 typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
 
-/* MAPA_BF16X3: split-precision bf16 operand rows [hi | hi | lo] (3x the logical width; see mapa_split_bf16x3),
+/* MAPA_BF16X3: split-precision bf16 operand rows [hi | lo] (2x the logical width; see mapa_split_bf16x3),
  * accepted as an OUTPUT dtype by mapa_layernorm (y_lp) and mapa_bilinear_ac */
 enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2 };
 enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
@@ -71,13 +71,18 @@ typedef struct {
    * again when each call completes.  NULL / too small -> the data-parallel schedule (same results to rounding). */
   void* workspace;
   int64_t workspace_bytes;
-  /* Split-precision operand outputs (dtype BF16 only; NULL = off): row r of out_s3 is 3*ld bf16 wide (ld = ldo, or
-   * ps_cout in PIXSHUF mode) and holds [hi | hi | lo] of the output row, hi = bf16(v), lo = bf16(v - hi) — the
-   * mapa_split_bf16x3 layout, so the next GEMM/conv (conv_C = 3*C, weights [hi | lo | hi] per tap) computes the
-   * fp32 product to ~2^-16.  out_s3_relu: the same of max(v, 0).  Used for the downstream heads, which the reference
-   * runs with autocast disabled (model.py:1774). */
+  /* Split-precision operand outputs (dtype BF16 only; NULL = off): row r of out_s3 is 2*ld bf16 wide (ld = ldo, or
+   * ps_cout in PIXSHUF mode) and holds [hi | lo] of the output row, hi = bf16(v), lo = bf16(v - hi) — the
+   * mapa_split_bf16x3 layout, so the next GEMM/conv (a_split, conv_C = 3*C, weights [hi | lo | hi] per tap) computes
+   * the fp32 product to ~2^-16.  out_s3_relu: the same of max(v, 0).  Used for the downstream heads, which the
+   * reference runs with autocast disabled (model.py:1774). */
   void* out_s3;
   void* out_s3_relu;
+  /* a_split != 0: A is a split-precision operand stored compact, [hi | lo] (2C bf16 per row, or per pixel in conv
+   * mode), read as the logical K layout [hi | hi | lo] (K = 3C for dense A with lda >= 2C; conv_C = 3C per tap)
+   * against weights packed [hi | lo | hi] — what out_s3 / mapa_split_bf16x3 / the split LayerNorm and bilinear
+   * outputs store.  C % 8 == 0. */
+  int a_split;
 } mapa_gemm_desc;
 
 int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
@@ -134,7 +139,7 @@ int mapa_attn_merge(const void* o_a, const float* lse_a, const void* o_b, const 
 
 /* LayerNorm over the last dim (nn.LayerNorm eps=1e-6): y = (x-mean)/sqrt(var+eps)*w + b.
  * x: f32 rows (row stride ldx); outputs optional: y_f32 (ldy), y_lp (bf16 or f32 per lp_dtype, ldy; MAPA_BF16X3:
- * split rows of 3*ldy bf16).
+ * split rows of 2*ldy bf16).
  * Output row r reads input row (in_group > 0 ? (r / in_group) * in_group_stride + r % in_group : r) + in_row_off
  * (e.g. drop the DINOv2 cls row of every view: group T, stride T+1, offset 1). */
 int mapa_layernorm(const float* x, int64_t ldx, int rows, int dim, const float* w, const float* b, float eps,
@@ -157,7 +162,7 @@ int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, const float*
 
 /* Bilinear resize, align_corners=True, NHWC.  Output grid is the full (OHf, OWf) grid of F.interpolate; only
  * rows < OH and cols < OW are written (fused crop, dpt.py:213).  in: f32 or bf16 (in_dtype), out: out_dtype
- * (MAPA_BF16X3: split rows [hi | hi | lo] of 3*C bf16 per pixel). */
+ * (MAPA_BF16X3: split rows [hi | lo] of 2*C bf16 per pixel). */
 int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH, int OW,
                      void* out, int out_dtype, mapa_stream_t stream);
 
@@ -232,9 +237,10 @@ int mapa_denorm_image(const float* img, int n, int H, int W, const float* mean, 
 int mapa_convert_rows(const float* src, int64_t lds, int rows, int cols, void* dst, int dst_dtype, int64_t ldd,
                       mapa_stream_t stream);
 
-/* Split-precision operand for the fp32 geometric encoders in bf16 mode: x fp32 [rows][cols] (row stride ldx) ->
- * y bf16 [rows][3*cols_padded] = [hi | hi | lo] blocks (hi = bf16(x), lo = bf16(x - hi), zero past cols); paired
- * with weights packed [hi | lo | hi] a bf16 GEMM over K = 3*cols_padded gives the fp32 product to ~2^-16.
+/* Split-precision operand of fp32 rows (the fp32-exact geometric encoders and heads in bf16 mode): x fp32
+ * [rows][cols] (row stride ldx) -> y bf16 [rows][2*cols_padded] = [hi | lo] blocks (hi = bf16(x), lo = bf16(x - hi),
+ * zero past cols); read by mapa_gemm with a_split as the logical K blocks [hi | hi | lo] against weights packed
+ * [hi | lo | hi], a bf16 GEMM over K = 3*cols_padded gives the fp32 product to ~2^-16.
  * Replaces the fp32 conv/linear operands of DenseRepresentationEncoder (dense_rep_encoder.py:234-287). */
 int mapa_split_bf16x3(const float* x, int64_t ldx, int64_t rows, int cols, int cols_padded, void* y,
                       mapa_stream_t stream);

@@ -114,7 +114,7 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 // One thread = 8 channels of one output pixel (16-B bf16 accesses); consecutive threads walk the channels of a
 // pixel, so a wave reads each of the 4 source taps and writes the output as contiguous row segments.  32-bit
 // indexing (the caller checks the element count).
-template <typename TI, typename TO, bool S3 = false>  // S3: split operand rows [hi | hi | lo] (3C wide)
+template <typename TI, typename TO, bool S3 = false>  // S3: split operand rows [hi | lo] (2C wide)
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                    int OW, TO* __restrict__ out) {
   const int c8 = C / 8;
@@ -135,7 +135,7 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
     const TI* base = in + (size_t)im * IH * IW * C + c;
     const size_t o00 = ((size_t)y0 * IW + x0) * C, o01 = ((size_t)y0 * IW + x1) * C;
     const size_t o10 = ((size_t)y1 * IW + x0) * C, o11 = ((size_t)y1 * IW + x1) * C;
-    TO* op = out + (((size_t)im * OH + oy) * OW + ox) * (S3 ? 3 * C : C) + c;
+    TO* op = out + (((size_t)im * OH + oy) * OW + ox) * (S3 ? 2 * C : C) + c;
     f32x4 a0, a1, b0, b1, c0, c1, d0, d1;
     load8(base + o00, a0, a1);
     load8(base + o01, b0, b1);
@@ -329,9 +329,9 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, 
   }
 }
 
-// fp32 rows -> [hi | hi | lo] bf16 column blocks of width cp (zero-padded past cols), hi = bf16(x),
-// lo = bf16(x - hi): with weights packed [hi | lo | hi] one bf16 GEMM over K = 3*cp accumulates
-// x_hi*w_hi + x_hi*w_lo + x_lo*w_hi (the split-precision form of an fp32 product, ~2^-16 relative).
+// fp32 rows -> [hi | lo] bf16 column blocks of width cp (zero-padded past cols), hi = bf16(x), lo = bf16(x - hi):
+// read by a bf16 GEMM as the logical K blocks [hi | hi | lo] (mapa_gemm_desc.a_split) against weights packed
+// [hi | lo | hi], it accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi (the split form of an fp32 product, ~2^-16).
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int cols, int cp,
                                     bf16_t* __restrict__ y) {
   const int g4 = cp / 4;
@@ -339,23 +339,8 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ x, int64_t ldx, in
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = e / g4;
     const int c = (int)(e - r * g4) * 4;
-    const float4 v = c < cols ? *reinterpret_cast<const float4*>(x + r * ldx + c) : float4{0.f, 0.f, 0.f, 0.f};
-    const float f[4] = {v.x, v.y, v.z, v.w};
-    bf16_t hi[4], lo[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      hi[j] = f32_to_bf16(f[j]);
-      lo[j] = f32_to_bf16(f[j] - bf16_to_f32(hi[j]));
-    }
-    uint2 h, l;
-    h.x = (uint32_t)hi[0] | ((uint32_t)hi[1] << 16);
-    h.y = (uint32_t)hi[2] | ((uint32_t)hi[3] << 16);
-    l.x = (uint32_t)lo[0] | ((uint32_t)lo[1] << 16);
-    l.y = (uint32_t)lo[2] | ((uint32_t)lo[3] << 16);
-    bf16_t* o = y + r * 3 * cp + c;
-    *reinterpret_cast<uint2*>(o) = h;
-    *reinterpret_cast<uint2*>(o + cp) = h;
-    *reinterpret_cast<uint2*>(o + 2 * cp) = l;
+    const f32x4 v = c < cols ? *reinterpret_cast<const f32x4*>(x + r * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    store_split3(y + r * 2 * cp + c, cp, v);
   }
 }
 

@@ -112,14 +112,14 @@ __device__ __forceinline__ void stage_tile(const GemmArgs& p, char* lds, int buf
     const bool kin = k_exact || kc < p.K;
     const char* src;
     if constexpr (AMODE == 0) {
-      src = kin ? a_src[i] + koff : zero;
+      src = kin ? a_src[i] + koff - split_koff(p, kc, (int)sizeof(T)) : zero;
     } else {
-      const int tap = kc / p.cv_C, ci = kc - tap * p.cv_C;
+      const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
       const int ky = tap / 3, kx = tap - ky * 3;
       const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
       const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
       src = ok ? reinterpret_cast<const char*>(p.A) +
-                     ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * sizeof(T)
+                     ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_Cp + ci) * sizeof(T)
                : zero;
     }
     __builtin_amdgcn_global_load_lds(src, As + off, 16, 0, 0);
@@ -339,9 +339,16 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
                    "mapa_gemm: conv M must be images * OH * OW");
   } else {
     MAPA_CHECK_ARG(d->a_mode == MAPA_A_DENSE, "mapa_gemm: bad a_mode");
-    MAPA_CHECK_ARG(d->lda >= d->K && d->lda % E == 0, "mapa_gemm: lda must be >= K and keep 16-B rows");
+    MAPA_CHECK_ARG((d->a_split || d->lda >= d->K) && d->lda % E == 0, "mapa_gemm: lda must be >= K and keep 16-B rows");
   }
   MAPA_CHECK_ARG(d->ldw >= d->K && d->ldw % E == 0, "mapa_gemm: ldw must be >= K and keep 16-B rows");
+  if (d->a_split) {
+    const int lw = d->a_mode == MAPA_A_CONV3X3 ? d->conv_C : d->K;  // logical [hi | hi | lo] width
+    MAPA_CHECK_ARG(d->dtype == MAPA_BF16 && lw % 3 == 0 && (lw / 3) % 8 == 0,
+                   "mapa_gemm: a_split needs bf16 and a logical width 3*C with C %% 8 == 0 (got %d)", lw);
+    MAPA_CHECK_ARG(d->a_mode == MAPA_A_CONV3X3 || d->lda >= 2 * (d->K / 3),
+                   "mapa_gemm: a_split lda must be >= the stored width 2K/3");
+  }
   if (d->out_mode == MAPA_OUT_PIXSHUF) {
     MAPA_CHECK_ARG(d->ps_s > 0 && d->ps_cout > 0 && d->N == d->ps_s * d->ps_s * d->ps_cout &&
                        d->M % (d->ps_h * d->ps_w) == 0 && d->ps_cout % 4 == 0,
@@ -354,6 +361,12 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   a.M = d->M; a.N = d->N; a.K = d->K;
   a.cv_C = d->conv_C; a.cv_IH = d->conv_IH; a.cv_IW = d->conv_IW; a.cv_OH = d->conv_OH; a.cv_OW = d->conv_OW;
   a.cv_stride = d->conv_stride;
+  a.sp_half = 0x7fffffff;
+  a.cv_Cp = d->conv_C;
+  if (d->a_split) {
+    a.sp_half = (d->a_mode == MAPA_A_CONV3X3 ? d->conv_C : d->K) / 3;
+    if (d->a_mode == MAPA_A_CONV3X3) a.cv_Cp = 2 * a.sp_half;
+  }
   a.bias = d->bias; a.bias_mod = d->bias_mod > 0 ? d->bias_mod : d->N;
   a.gamma = d->gamma; a.act = d->act;
   a.resid1 = d->resid1; a.resid2 = d->resid2;

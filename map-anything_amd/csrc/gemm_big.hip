@@ -65,13 +65,13 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
     const bool kin = k_exact || kc < p.K;
     const char* src;
     if constexpr (AMODE == 0) {
-      src = kin ? a_src[i] + koff : zero;
+      src = kin ? a_src[i] + koff - split_koff(p, kc, 2) : zero;
     } else {
-      const int tap = kc / p.cv_C, ci = kc - tap * p.cv_C;
+      const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
       const int ky = tap / 3, kx = tap - ky * 3;
       const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
       const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-      src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * 2
+      src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_Cp + ci) * 2
                : zero;
     }
     __builtin_amdgcn_global_load_lds(src, As + lds_wave + i * 8192, 16, 0, 0);
@@ -308,13 +308,13 @@ __global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
       const bool kin = k_exact || kc < p.K;
       const char* src;
       if constexpr (AMODE == 0) {
-        src = kin ? a_src[i] + (int64_t)kt * C::BK * 2 : zero;
+        src = kin ? a_src[i] + (int64_t)kt * C::BK * 2 - split_koff(p, kc, 2) : zero;
       } else {
-        const int tap = kc / p.cv_C, ci = kc - tap * p.cv_C;
+        const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
         const int ky = tap / 3, kx = tap - ky * 3;
         const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
         const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-        src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_C + ci) * 2
+        src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_Cp + ci) * 2
                  : zero;
       }
       __builtin_amdgcn_global_load_lds(src, As + lds_wave + i * 8192, 16, 0, 0);

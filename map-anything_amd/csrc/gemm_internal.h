@@ -12,6 +12,10 @@ struct GemmArgs {
   int64_t ldw;
   int M, N, K;
   int cv_C, cv_IH, cv_IW, cv_OH, cv_OW, cv_stride;
+  // split-precision A operand stored compact: logical K layout [hi | hi | lo] (blocks of sp_half per row or per
+  // conv tap), physical [hi | lo] (2 * sp_half per row / pixel, cv_Cp); sp_half = INT_MAX when A is plain
+  int sp_half;
+  int cv_Cp;  // physical elements per input pixel (conv): cv_C, or 2 * sp_half for a compact split operand
   const float* bias;
   int bias_mod;
   const float* gamma;
@@ -21,7 +25,7 @@ struct GemmArgs {
   float* out_f32;
   void* out_lp;
   void* out_lp_relu;
-  void* out_s3;       // split-precision operand outputs (bf16 kernels): [hi | hi | lo] of v, row stride 3*ld
+  void* out_s3;       // split-precision operand outputs (bf16 kernels): [hi | lo] of v, row stride 2*ld
   void* out_s3_relu;
   int64_t ldo;
   int out_mode;  // 0 row-major, 1 pixel shuffle
@@ -47,6 +51,14 @@ __device__ __forceinline__ void tile_coords(int b, int ntm, int ntn, int& tm, in
   const int in = t - group * GM * ntn;
   tm = first + in % rows;
   tn = in / rows;
+}
+
+// Logical A column (within a row, or within a conv tap) -> physical column of a compact split operand: the
+// logical blocks [hi | hi | lo] map onto the stored [hi | lo] (the second hi block re-reads the first).
+__device__ __forceinline__ int split_col(const GemmArgs& p, int c) { return c - (c >= p.sp_half ? p.sp_half : 0); }
+// Byte correction of a dense A row address for logical column kc (0 for plain operands).
+__device__ __forceinline__ int64_t split_koff(const GemmArgs& p, int kc, int esz) {
+  return kc >= p.sp_half ? (int64_t)p.sp_half * esz : 0;
 }
 
 __device__ __forceinline__ float epi_act(float v, int act) {
@@ -102,7 +114,7 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
     ld = p.ps_cout;
   }
   const int64_t off = orow * ld + c.col_off;
-  const int64_t off3 = orow * 3 * ld + c.col_off;  // split-operand rows are [hi | hi | lo], 3*ld wide
+  const int64_t off3 = orow * 2 * ld + c.col_off;  // split-operand rows are stored [hi | lo], 2*ld wide
   f32x4 v;
 #pragma unroll
   for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + c.bv[e], p.act) * c.gv[e];

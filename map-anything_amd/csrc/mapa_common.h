@@ -48,9 +48,10 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-// Split-precision operand of 4 consecutive values: hi = bf16(v) at [0, ld), again at [ld, 2ld), lo = bf16(v - hi)
-// at [2ld, 3ld) — with weights packed [hi | lo | hi] a bf16 GEMM over the 3x wider K accumulates
-// v_hi*w_hi + v_hi*w_lo + v_lo*w_hi, the fp32 product to ~2^-16 (mapa_split_bf16x3's layout).
+// Split-precision operand of 4 consecutive values, stored compact: hi = bf16(v) at [0, ld), lo = bf16(v - hi) at
+// [ld, 2ld).  A bf16 GEMM reads it as the logical K blocks [hi | hi | lo] (the A loader maps the second hi block back
+// onto the first) against weights packed [hi | lo | hi]: v_hi*w_hi + v_hi*w_lo + v_lo*w_hi, the fp32 product to
+// ~2^-16 (mapa_split_bf16x3's layout).
 __device__ __forceinline__ void store_split3(bf16_t* p, int64_t ld, f32x4 v) {
   uint2 h, l;
   const bf16_t h0 = f32_to_bf16(v[0]), h1 = f32_to_bf16(v[1]), h2 = f32_to_bf16(v[2]), h3 = f32_to_bf16(v[3]);
@@ -59,14 +60,12 @@ __device__ __forceinline__ void store_split3(bf16_t* p, int64_t ld, f32x4 v) {
   l.x = pack_bf16x2(v[0] - bf16_to_f32(h0), v[1] - bf16_to_f32(h1));
   l.y = pack_bf16x2(v[2] - bf16_to_f32(h2), v[3] - bf16_to_f32(h3));
   *reinterpret_cast<uint2*>(p) = h;
-  *reinterpret_cast<uint2*>(p + ld) = h;
-  *reinterpret_cast<uint2*>(p + 2 * ld) = l;
+  *reinterpret_cast<uint2*>(p + ld) = l;
 }
 __device__ __forceinline__ void store_split1(bf16_t* p, int64_t ld, float x) {
   const bf16_t h = f32_to_bf16(x);
   p[0] = h;
-  p[ld] = h;
-  p[2 * ld] = f32_to_bf16(x - bf16_to_f32(h));
+  p[ld] = f32_to_bf16(x - bf16_to_f32(h));
 }
 
 __device__ __forceinline__ float gelu_erf(float x) {

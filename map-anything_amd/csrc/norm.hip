@@ -46,8 +46,8 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     for (int j = 0; j < 4; ++j) y[j] = (v[i][j] - mean) * rstd * wv[j] + bv[j];
     if (yf) *reinterpret_cast<f32x4*>(yf + (int64_t)row * ldy + c) = y;
     if (ylp) {
-      if (lp_bf16 == 2) {  // split operand row: [hi | hi | lo], 3*ldy wide
-        store_split3(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 3 * ldy + c, ldy, y);
+      if (lp_bf16 == 2) {  // split operand row: [hi | lo], 2*ldy wide
+        store_split3(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y);
       } else if (lp_bf16) {
         uint2 pk;
         pk.x = pack_bf16x2(y[0], y[1]);

@@ -44,7 +44,7 @@ class GemmDesc(ctypes.Structure):
         ("out_lp", ctypes.c_void_p), ("out_lp_relu", ctypes.c_void_p), ("ldo", ctypes.c_int64),
         ("out_mode", ctypes.c_int), ("ps_s", ctypes.c_int), ("ps_h", ctypes.c_int), ("ps_w", ctypes.c_int),
         ("ps_cout", ctypes.c_int), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
-        ("out_s3", ctypes.c_void_p), ("out_s3_relu", ctypes.c_void_p),
+        ("out_s3", ctypes.c_void_p), ("out_s3_relu", ctypes.c_void_p), ("a_split", ctypes.c_int),
     ]
 
 
@@ -243,13 +243,17 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
          out_f32=None, out_lp=None, out_lp_relu=None, out_s3=None, out_s3_relu=None, ldo=None, conv=None,
          pixshuf=None):
     """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout).
-    out_s3 / out_s3_relu: split-precision operand outputs (bf16 [rows][3*ldo], [hi | hi | lo])."""
+    out_s3 / out_s3_relu: split-precision operand outputs (bf16 [rows][2*ldo], [hi | lo]).  A weight packed for split
+    operands (W._mapa_split, engine._split_pack) marks A as a compact split operand (mapa_gemm_desc.a_split): K is
+    then the logical 3C, the stored A row 2C wide."""
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype
     d.M, d.N, d.K = M, N, K
     d.A = A.data_ptr()
-    d.lda = lda if lda is not None else K
+    split_a = W.dtype == torch.bfloat16 and getattr(W, "_mapa_split", False)
+    d.a_split = 1 if split_a else 0
+    d.lda = lda if lda is not None else (2 * K // 3 if split_a else K)
     d.W = W.data_ptr()
     d.ldw = W.stride(0)
     if conv is not None:
@@ -267,7 +271,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     d.out_lp_relu = None if out_lp_relu is None else out_lp_relu.data_ptr()
     for t in (out_s3, out_s3_relu):
         if t is not None and t.dtype != torch.bfloat16:
-            raise NativeError("split outputs are bf16 [rows][3*ld]")
+            raise NativeError("split outputs are bf16 [rows][2*ld]")
     d.out_s3 = None if out_s3 is None else out_s3.data_ptr()
     d.out_s3_relu = None if out_s3_relu is None else out_s3_relu.data_ptr()
     d.ldo = ldo if ldo is not None else N
@@ -318,7 +322,7 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
 
 def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, y_s3=None, ldy=None, group=0,
               group_stride=0, row_off=0):
-    """y_s3: split-precision operand rows (bf16 [rows][3*ldy]) instead of y_lp."""
+    """y_s3: split-precision operand rows (bf16 [rows][2*ldy], [hi | lo]) instead of y_lp."""
     if y_s3 is not None:
         if y_lp is not None or y_s3.dtype != torch.bfloat16:
             raise NativeError("layernorm: y_s3 (bf16) replaces y_lp")
@@ -346,7 +350,7 @@ def add_rowvec(x, ldx, r0, r1, dim, vec):
 
 
 def bilinear_ac(inp, n, IH, IW, C, OHf, OWf, OH, OW, out, split_out=False):
-    """split_out: out is a split-precision operand (bf16 [pixels][3*C], [hi | hi | lo])."""
+    """split_out: out is a split-precision operand (bf16 [pixels][2*C], [hi | lo])."""
     if split_out and out.dtype != torch.bfloat16:
         raise NativeError("bilinear_ac: split output is bf16")
     check(lib().mapa_bilinear_ac(ptr(inp), dt_code(inp.dtype), n, IH, IW, C, OHf, OWf, OH, OW, ptr(out),
@@ -380,9 +384,9 @@ def convert_rows(src, lds, rows, cols, dst, ldd):
 
 
 def split_bf16x3(x, rows, cols, cols_padded, y, ldx=None):
-    """x fp32 [rows][cols] -> y bf16 [rows][3*cols_padded] = [hi | hi | lo] (mapa.h mapa_split_bf16x3)."""
-    if x.dtype != torch.float32 or y.dtype != torch.bfloat16 or y.numel() < rows * 3 * cols_padded:
-        raise AssertionError("split_bf16x3: fp32 input, bf16 output of rows x 3*cols_padded")
+    """x fp32 [rows][cols] -> y bf16 [rows][2*cols_padded] = [hi | lo] (mapa.h mapa_split_bf16x3)."""
+    if x.dtype != torch.float32 or y.dtype != torch.bfloat16 or y.numel() < rows * 2 * cols_padded:
+        raise AssertionError("split_bf16x3: fp32 input, bf16 output of rows x 2*cols_padded")
     check(lib().mapa_split_bf16x3(ptr(x), cols if ldx is None else ldx, rows, cols, cols_padded, ptr(y), stream()),
           "mapa_split_bf16x3")
 

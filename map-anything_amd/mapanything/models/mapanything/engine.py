@@ -71,7 +71,8 @@ class GeoInputs:
 
 def _split_pack(w: np.ndarray, dev) -> torch.Tensor:
     """[out][taps][cin] fp32 -> bf16 [out][taps * 3 * ceil8(cin)] = [hi | lo | hi] per tap: the weight side of a
-    split-precision GEMM against activations [hi | hi | lo] (mapa_split_bf16x3 / the GEMM's out_s3 epilogue)."""
+    split-precision GEMM against activations stored [hi | lo] and read as [hi | hi | lo] (mapa_split_bf16x3 / the
+    GEMM's out_s3 epilogue; nat.gemm sets mapa_gemm_desc.a_split for weights tagged _mapa_split)."""
     o, taps, cin = w.shape
     wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
     hi = wt.to(torch.bfloat16)
@@ -306,14 +307,14 @@ class MapaEngine:
 
     # ------------------------------------------------------------------------- head operands (model.py:1774)
     def _hop(self, rows, C):
-        """Operand buffer of a head GEMM/conv input with C logical channels: split rows [hi | hi | lo] (bf16,
-        3C wide) when the heads run at the reference's fp32 in bf16 mode, else lp rows."""
+        """Operand buffer of a head GEMM/conv input with C channels: split rows [hi | lo] (bf16, 2C wide; read as
+        the logical K blocks [hi | hi | lo]) when the heads run at the reference's fp32 in bf16 mode, else lp rows."""
         if self.hsplit:
-            return torch.empty(rows, 3 * C, dtype=torch.bfloat16, device=self.device)
+            return torch.empty(rows, 2 * C, dtype=torch.bfloat16, device=self.device)
         return self._empty(rows, C)
 
     def _hw(self, C):
-        """Per-pixel operand width of a head input with C logical channels."""
+        """Logical per-pixel K width of a head input with C channels (3C for split operands)."""
         return 3 * C if self.hsplit else C
 
     def _hout(self, buf=None, relu=None):
@@ -501,11 +502,11 @@ class MapaEngine:
         M = n * hp * wp
         cin = C * PATCH * PATCH
 
-        def operand(x, c):  # GEMM A operand and its per-tap width: fp32 as is, or [hi | hi | lo] bf16
+        def operand(x, c):  # GEMM A operand and its logical per-tap width: fp32 as is, or split [hi | lo] bf16
             if not g["split"]:
                 return x, c
             cp = _ceil8(c)
-            y = self._empty(M, 3 * cp, dtype=torch.bfloat16)
+            y = self._empty(M, 2 * cp, dtype=torch.bfloat16)
             nat.split_bf16x3(x, M, c, cp, y)
             return y, 3 * cp
 

@@ -435,75 +435,78 @@ def test_attention_partials_merge_to_full(nat, dtype, tol):
 # ------------------------------------------------------------------------------------- split-precision operands
 @pytest.mark.parametrize("rows,cols,cp", [(37, 588, 592), (1369, 196, 200), (10, 1024, 1024)])
 def test_split_bf16x3_is_bit_exact(nat, rows, cols, cp):
-    """[hi | hi | lo] blocks: hi = bf16(x) (RNE), lo = bf16(x - hi), zero padding — bit-exact vs torch."""
+    """[hi | lo] blocks: hi = bf16(x) (RNE), lo = bf16(x - hi), zero padding — bit-exact vs torch."""
     x = _rand(rows, cols, scale=3.0, seed=11)
-    y = torch.full((rows, 3 * cp), 7.0, dtype=torch.bfloat16, device="cuda")
+    y = torch.full((rows, 2 * cp), 7.0, dtype=torch.bfloat16, device="cuda")
     nat.split_bf16x3(x, rows, cols, cp, y)
     hi = x.to(torch.bfloat16)
     lo = (x - hi.float()).to(torch.bfloat16)
-    ref = torch.zeros(rows, 3, cp, dtype=torch.bfloat16, device="cuda")
-    ref[:, 0, :cols], ref[:, 1, :cols], ref[:, 2, :cols] = hi, hi, lo
+    ref = torch.zeros(rows, 2, cp, dtype=torch.bfloat16, device="cuda")
+    ref[:, 0, :cols], ref[:, 1, :cols] = hi, lo
     assert torch.equal(y.view(torch.int16), ref.reshape(rows, -1).view(torch.int16))
 
 
 def test_split_precision_conv_matches_fp32(nat):
-    """A 3x3 conv run as one bf16 implicit-GEMM over [hi | hi | lo] activations and [hi | lo | hi] weights (the
-    geometric encoders' bf16-mode path) stays within ~1e-5 of the fp32 conv (plain bf16: ~3e-3)."""
+    """A 3x3 conv run as one bf16 implicit-GEMM over split activations (stored [hi | lo], read [hi | hi | lo]) and
+    [hi | lo | hi] weights (the geometric encoders' bf16-mode path) stays within ~1e-5 of the fp32 conv (plain
+    bf16: ~3e-3)."""
     n, h, w, C, Co = 2, 37, 37, 588, 768
     x = _rand(n, C, h, w, seed=12)
     wt = _rand(Co, C, 3, 3, scale=C ** -0.5 / 3, seed=13)
     ref = F.conv2d(x.cpu().double(), wt.cpu().double(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
     M, cp = n * h * w, 592
     xr = x.permute(0, 2, 3, 1).reshape(M, C).contiguous()
-    a = torch.empty(M, 3 * cp, dtype=torch.bfloat16, device="cuda")
+    a = torch.empty(M, 2 * cp, dtype=torch.bfloat16, device="cuda")
     nat.split_bf16x3(xr, M, C, cp, a)
     wk = wt.permute(0, 2, 3, 1).reshape(Co, 9, C)
     whi = wk.to(torch.bfloat16)
     wlo = (wk - whi.float()).to(torch.bfloat16)
     wp = torch.zeros(Co, 9, 3, cp, dtype=torch.bfloat16, device="cuda")
     wp[:, :, 0, :C], wp[:, :, 1, :C], wp[:, :, 2, :C] = whi, wlo, whi
+    wp = wp.reshape(Co, -1)
+    wp._mapa_split = True  # A is a compact split operand
     out = torch.empty(M, Co, device="cuda")
-    nat.gemm(a, wp.reshape(Co, -1), M, Co, 9 * 3 * cp, out_f32=out, conv=(3 * cp, h, w, h, w, 1))
+    nat.gemm(a, wp, M, Co, 9 * 3 * cp, out_f32=out, conv=(3 * cp, h, w, h, w, 1))
     assert rel_l2(out.cpu(), ref) < 2e-5
 
 
 # ------------------------------------------------------------- split-precision operand outputs (fp32 heads)
 def _split_expect(v):
-    """[hi | hi | lo] of fp32 rows v [R][C] (mapa_split_bf16x3's layout)."""
+    """[hi | lo] of fp32 rows v [R][C] (mapa_split_bf16x3's layout)."""
     hi = v.to(torch.bfloat16)
     lo = (v - hi.float()).to(torch.bfloat16)
-    return torch.cat([hi, hi, lo], 1)
+    return torch.cat([hi, lo], 1)
 
 
 @pytest.mark.parametrize("M,N,K", [(333, 384, 192), (100, 6, 24), (257, 130, 64)])
 def test_gemm_split_outputs_bit_exact(nat, M, N, K):
-    """out_s3 / out_s3_relu rows are exactly [hi | hi | lo] of the fp32 epilogue value (the out_f32 output)."""
+    """out_s3 / out_s3_relu rows are exactly [hi | lo] of the fp32 epilogue value (the out_f32 output)."""
     A = _rand(M, K, seed=31).to(torch.bfloat16)
     W = _rand(N, K, scale=K ** -0.5, seed=32).to(torch.bfloat16)
     b, r1 = _rand(N, seed=33), _rand(M, N, seed=34)
     of = torch.empty(M, N, device="cuda")
-    s3 = torch.full((M, 3 * N), 7.0, device="cuda", dtype=torch.bfloat16)
-    s3r = torch.full((M, 3 * N), 7.0, device="cuda", dtype=torch.bfloat16)
+    s3 = torch.full((M, 2 * N), 7.0, device="cuda", dtype=torch.bfloat16)
+    s3r = torch.full((M, 2 * N), 7.0, device="cuda", dtype=torch.bfloat16)
     nat.gemm(A, W, M, N, K, bias=b, resid1=r1, out_f32=of, out_s3=s3, out_s3_relu=s3r)
     assert torch.equal(s3, _split_expect(of))
     assert torch.equal(s3r, _split_expect(torch.relu(of)))
 
 
 def test_gemm_split_output_pixel_shuffle(nat):
-    """ConvTranspose k=s=2 through the pixel-shuffle epilogue into split rows (3*cout per output pixel)."""
+    """ConvTranspose k=s=2 through the pixel-shuffle epilogue into split rows (2*cout per output pixel)."""
     n, h, w, ci, co, s = 2, 5, 7, 64, 48, 2
     A = _rand(n * h * w, ci, seed=35).to(torch.bfloat16)
     W = _rand(s * s * co, ci, scale=ci ** -0.5, seed=36).to(torch.bfloat16)
     b = _rand(co, seed=37)
     of = torch.empty(n * h * s * w * s, co, device="cuda")
-    s3 = torch.empty(n * h * s * w * s, 3 * co, device="cuda", dtype=torch.bfloat16)
+    s3 = torch.empty(n * h * s * w * s, 2 * co, device="cuda", dtype=torch.bfloat16)
     nat.gemm(A, W, n * h * w, s * s * co, ci, bias=b, bias_mod=co, out_f32=of, out_s3=s3, pixshuf=(s, h, w, co))
     assert torch.equal(s3, _split_expect(of))
 
 
 def test_split_chain_matches_fp32(nat):
-    """A split-output GEMM feeding a split-operand conv3x3 ([hi | lo | hi] weights): the fp32 product to ~2^-16
-    (plain bf16 operands: ~3e-3) — the precision of the heads in bf16 mode."""
+    """A split-output GEMM feeding a split-operand conv3x3 ([hi | lo | hi] weights, A stored [hi | lo]): the fp32
+    product to ~2^-16 (plain bf16 operands: ~3e-3) — the precision of the heads in bf16 mode."""
     from mapanything.models.mapanything.engine import _split_pack
 
     n, H, W_, C, Co = 2, 9, 11, 64, 40
@@ -511,10 +514,10 @@ def test_split_chain_matches_fp32(nat):
     w1 = _rand(C, C, scale=C ** -0.5, seed=39)
     b1 = _rand(C, seed=40)
     wc = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=41)
-    xs = torch.empty(n * H * W_, 3 * C, device="cuda", dtype=torch.bfloat16)
+    xs = torch.empty(n * H * W_, 2 * C, device="cuda", dtype=torch.bfloat16)
     nat.split_bf16x3(x, n * H * W_, C, C, xs)
     w1s = _split_pack(w1.cpu().numpy().reshape(C, 1, C), "cuda")
-    y = torch.empty(n * H * W_, 3 * C, device="cuda", dtype=torch.bfloat16)
+    y = torch.empty(n * H * W_, 2 * C, device="cuda", dtype=torch.bfloat16)
     nat.gemm(xs, w1s, n * H * W_, C, 3 * C, bias=b1, act=nat.ACT_RELU, out_s3=y)
     wcs = _split_pack(wc.permute(0, 2, 3, 1).reshape(Co, 9, C).cpu().numpy(), "cuda")
     out = torch.empty(n * H * W_, Co, device="cuda")
@@ -529,7 +532,7 @@ def test_layernorm_split_output(nat):
     x = _rand(rows, dim, seed=42)
     w, b = _rand(dim, seed=43), _rand(dim, seed=44)
     yf = torch.empty(rows, dim, device="cuda")
-    ys = torch.empty(rows, 3 * dim, device="cuda", dtype=torch.bfloat16)
+    ys = torch.empty(rows, 2 * dim, device="cuda", dtype=torch.bfloat16)
     nat.layernorm(x, rows, dim, w, b, y_f32=yf, y_s3=ys)
     assert torch.equal(ys, _split_expect(yf))
 
@@ -538,7 +541,7 @@ def test_bilinear_split_output(nat):
     n, IH, IW, C, OH, OW = 2, 19, 23, 128, 38, 46
     x = _rand(n * IH * IW, C, seed=45)
     yf = torch.empty(n * OH * OW, C, device="cuda")
-    ys = torch.empty(n * OH * OW, 3 * C, device="cuda", dtype=torch.bfloat16)
+    ys = torch.empty(n * OH * OW, 2 * C, device="cuda", dtype=torch.bfloat16)
     nat.bilinear_ac(x, n, IH, IW, C, OH, OW, OH, OW, yf)
     nat.bilinear_ac(x, n, IH, IW, C, OH, OW, OH, OW, ys, split_out=True)
     assert torch.equal(ys, _split_expect(yf))
