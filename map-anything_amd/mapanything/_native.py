@@ -198,6 +198,17 @@ def _toc(tok, kind, flops=0.0):
     _timing.setdefault(kind, []).append((tok, e, flops))
 
 
+# Optional launch log for profiling (MAPA_LAUNCH_LOG=<path>): the kind of every GEMM / attention call in launch
+# order, written at exit, so tools/profile_summary.py can name each rocprofv3 dispatch the way bench.py does (the
+# split-precision head GEMMs share kernel symbols with the plain ones).
+_LAUNCH_LOG = [] if os.environ.get("MAPA_LAUNCH_LOG") else None
+if _LAUNCH_LOG is not None:
+    import atexit
+    import json as _json
+
+    atexit.register(lambda: open(os.environ["MAPA_LAUNCH_LOG"], "w").write(_json.dumps(_LAUNCH_LOG)))
+
+
 # ------------------------------------------------------------------------------------------------ wrappers
 _WS_NEED = {}
 _WS = {}
@@ -288,8 +299,10 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     tok = _tic()
     check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
     # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops
-    split = "_split" if (W.dtype == torch.bfloat16 and getattr(W, "_mapa_split", False)) else ""
-    _toc(tok, ("conv3x3" if conv is not None else "gemm") + split, 2.0 * M * N * K)
+    kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if split_a else "")
+    if _LAUNCH_LOG is not None:
+        _LAUNCH_LOG.append(kind)
+    _toc(tok, kind, 2.0 * M * N * K)
 
 
 def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, k_bstride, k_rstride,
@@ -315,6 +328,8 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
         d.kv_nseg = len(kv_segments)
         for i, (st, ln) in enumerate(kv_segments):
             d.kv_seg_start[i], d.kv_seg_len[i] = st, ln
+    if _LAUNCH_LOG is not None:
+        _LAUNCH_LOG.append(kind)
     tok = _tic()
     check(lib().mapa_attention(ctypes.byref(d), stream()), "mapa_attention")
     _toc(tok, kind, 4.0 * batch * heads * seq_q * seq_kv * 64)

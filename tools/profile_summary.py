@@ -3,7 +3,13 @@
   python tools/profile_summary.py stats <kernel_stats.csv> [bench.json]      -> per-group calls / avg / total
   python tools/profile_summary.py traffic <fetch_pmc.csv> <write_pmc.csv>    -> HBM bytes per launch per group
   python tools/profile_summary.py mfma <kernel-regex> <pmc.csv>...           -> MFMA-pipe utilisation at the real clock
-  python tools/profile_summary.py mfma_groups <pmc.csv>                      -> the same per kernel group (bench run)
+  python tools/profile_summary.py mfma_groups <pmc.csv> [launch_log.json]   -> the same per kernel group (bench run)
+  python tools/profile_summary.py kinds <kernel_trace.csv> <launch_log.json> -> per bench.py kind (calls / avg / total)
+
+With a launch log (MAPA_LAUNCH_LOG, mapanything/_native.py) every GEMM / attention dispatch is named exactly as
+bench.py names it ("gemm", "gemm_split", "conv3x3", "conv3x3_split", "attention", "attention_global"): the n-th
+GEMM-kernel dispatch of the trace is the n-th GEMM call of the log (one dispatch per mapa_gemm call), the n-th
+attn_fwd dispatch the n-th attention call.
 
 Groups: "gemm" = dense GEMM instantiations (A mode 0), "conv3x3" = implicit-GEMM convs (A mode 1), "attention",
 "layernorm", "other".  FETCH_SIZE / WRITE_SIZE are rocprofv3 derived counters in KiB; on gfx950 FETCH_SIZE counts
@@ -30,6 +36,44 @@ def group(name: str) -> str:
     return "other"
 
 
+def _is_gemm(name):
+    return "gemm_big_kernel" in name or "gemm_kernel<" in name or "gemm_sk_kernel" in name or \
+        "gemm_pp_kernel" in name or "gemm_w4" in name
+
+
+def dispatch_kinds(names, log_path):
+    """names: kernel names of the dispatches in order -> the bench kind of each (None for other kernels)."""
+    log = json.load(open(log_path))
+    g_log = [k for k in log if k.startswith(("gemm", "conv3x3"))]
+    a_log = [k for k in log if k.startswith("attention")]
+    gi = ai = 0
+    out = []
+    for n in names:
+        if _is_gemm(n):
+            out.append(g_log[gi] if gi < len(g_log) else None)
+            gi += 1
+        elif "attn_fwd" in n:
+            out.append(a_log[ai] if ai < len(a_log) else None)
+            ai += 1
+        else:
+            out.append(None)
+    if gi != len(g_log) or ai != len(a_log):
+        raise SystemExit(f"launch log does not match the trace: {gi}/{len(g_log)} gemm, {ai}/{len(a_log)} attention")
+    return out
+
+
+def kinds(trace_csv, log_path):
+    rows = list(csv.DictReader(open(trace_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ks = dispatch_kinds([r["Kernel_Name"] for r in rows], log_path)
+    g = defaultdict(lambda: {"calls": 0, "total_ns": 0.0})
+    for r, k in zip(rows, ks):
+        k = k or group(r["Kernel_Name"])
+        g[k]["calls"] += 1
+        g[k]["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    return {k: dict(v, avg_us=v["total_ns"] / v["calls"] / 1e3) for k, v in g.items()}
+
+
 def stats(path, bench=None):
     g = defaultdict(lambda: {"calls": 0, "total_ns": 0.0})
     for r in csv.DictReader(open(path)):
@@ -47,13 +91,14 @@ def stats(path, bench=None):
     return out
 
 
-def traffic(fetch_csv, write_csv):
+def traffic(fetch_csv, write_csv, fetch_log=None, write_log=None):
     acc = defaultdict(lambda: defaultdict(list))
-    for path, counter in ((fetch_csv, "FETCH_SIZE"), (write_csv, "WRITE_SIZE")):
-        for r in csv.DictReader(open(path)):
-            if r["Counter_Name"] != counter:
-                continue
-            acc[group(r["Kernel_Name"])][counter].append(float(r["Counter_Value"]))
+    for path, counter, log in ((fetch_csv, "FETCH_SIZE", fetch_log), (write_csv, "WRITE_SIZE", write_log)):
+        rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+        rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+        ks = dispatch_kinds([r["Kernel_Name"] for r in rows], log) if log else [None] * len(rows)
+        for r, k in zip(rows, ks):
+            acc[k or group(r["Kernel_Name"])][counter].append(float(r["Counter_Value"]))
     out = {}
     for k, c in acc.items():
         f = c.get("FETCH_SIZE", [])
@@ -107,7 +152,11 @@ def mfma(pattern, paths):
     return out
 
 
-def mfma_groups(path):
+def _dispatch_order(per):
+    return sorted(per, key=lambda d: int(d))
+
+
+def mfma_groups(path, log_path=None):
     """Per kernel group (as bench.py names them): MFMA-pipe busy fraction over the sequencer-busy cycles and the
     clock (see mfma()), time-weighted over every dispatch of a PMC pass with SQ_BUSY_CYCLES +
     SQ_VALU_MFMA_BUSY_CYCLES."""
@@ -115,8 +164,14 @@ def mfma_groups(path):
     for r in csv.DictReader(open(path)):
         d = per[r["Dispatch_Id"]]
         d["group"] = group(r["Kernel_Name"])
+        d["name"] = r["Kernel_Name"]
         d[r["Counter_Name"]] = float(r["Counter_Value"])
         d["dur_ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    if log_path:
+        order = _dispatch_order(per)
+        for did, k in zip(order, dispatch_kinds([per[i]["name"] for i in order], log_path)):
+            if k:
+                per[did]["group"] = k
     acc = defaultdict(lambda: {"launches": 0, "busy": 0.0, "sq_busy": 0.0, "ns": 0.0})
     for d in per.values():
         if "SQ_BUSY_CYCLES" not in d or "SQ_VALU_MFMA_BUSY_CYCLES" not in d or d["dur_ns"] <= 0:
@@ -133,11 +188,14 @@ def mfma_groups(path):
 
 
 if __name__ == "__main__":
-    if sys.argv[1] == "mfma_groups":
-        print(json.dumps(mfma_groups(sys.argv[2]), indent=1))
-    elif sys.argv[1] == "mfma":
-        print(json.dumps(mfma(sys.argv[2], sys.argv[3:]), indent=1))
-    elif sys.argv[1] == "stats":
-        print(json.dumps(stats(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None), indent=1))
+    a = sys.argv
+    if a[1] == "mfma_groups":
+        print(json.dumps(mfma_groups(a[2], a[3] if len(a) > 3 else None), indent=1))
+    elif a[1] == "mfma":
+        print(json.dumps(mfma(a[2], a[3:]), indent=1))
+    elif a[1] == "stats":
+        print(json.dumps(stats(a[2], a[3] if len(a) > 3 else None), indent=1))
+    elif a[1] == "kinds":
+        print(json.dumps(kinds(a[2], a[3]), indent=1))
     else:
-        print(json.dumps(traffic(sys.argv[2], sys.argv[3]), indent=1))
+        print(json.dumps(traffic(a[2], a[3], *(a[4:6] if len(a) > 5 else (None, None))), indent=1))
