@@ -60,12 +60,13 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--geometric", action="store_true",
                     help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r2", "pmc_traffic.json"),
                     help="HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_summary.py)")
-    ap.add_argument("--mfma-pmc-json", default=os.path.join(REPO, "profiles", "r1", "pmc_mfma.json"),
+    ap.add_argument("--mfma-pmc-json", default=os.path.join(REPO, "profiles", "r2", "pmc_mfma.json"),
                     help="per-kernel-group MFMA busy fraction + clock from a rocprofv3 SQ pass (tools/gpu_pmc.sh)")
-    ap.add_argument("--attn-pmc-json", default=os.path.join(REPO, "profiles", "r1", "attn_global_pmc.json"),
-                    help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh)")
+    ap.add_argument("--attn-pmc-json", default=None,
+                    help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh); default: "
+                         "profiles/r2/attn_global_pmc.json (8 views) or attn_global_v100_pmc.json (>= 100 views)")
     ap.add_argument("--lib", default=None, help="A/B only: load this libmapa.so build (tools/ab_build.sh)")
     args = ap.parse_args()
     if args.lib:
@@ -199,7 +200,8 @@ def main():
                 mfma_pmc = json.load(open(args.mfma_pmc_json)).get(kind)
             roofline = {"kernel": kind, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                         "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
-                        "traffic": traffic, "traffic_unit": "bytes/launch (rocprofv3 PMC, profiles/)",
+                        "traffic": traffic,
+                        "traffic_unit": "bytes/launch: L2 fabric fetch (FETCH_SIZE x2, Infinity-Cache hits included) + WRITE_SIZE, rocprofv3 PMC, profiles/r2/pmc_traffic.json",
                         "pmc": mfma_pmc,
                         "launches": kt["count"], "avg_launch_us": kt["ms"] * 1e3 / kt["count"],
                         "timing_pass": {"ms_per_step": instr_ms, "launch": "eager, event pair per native call",
@@ -215,12 +217,15 @@ def main():
             xattn = {"kernel": "attn_fwd_bf16 (global AAT layers, L = V*1369+1 keys)", "achieved": tf,
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS, "target_frac": 0.40,
                      "ms_per_step": v["ms"] / args.steps, "launches_per_step": v["count"] / args.steps}
-            if os.path.exists(args.attn_pmc_json):
+            attn_pmc = args.attn_pmc_json or os.path.join(
+                REPO, "profiles", "r2", "attn_global_v100_pmc.json" if V_total >= 100 else "attn_global_pmc.json")
+            if os.path.exists(attn_pmc):
                 # MFMA-pipe busy fraction at the clock the chip really ran (rocprofv3 PMC pass, tools/attn_pmc.sh)
-                pj = json.load(open(args.attn_pmc_json))
+                pj = json.load(open(attn_pmc))
                 xattn["pmc"] = {k: pj.get(k) for k in ("mfma_busy_frac", "mfma_busy_frac_lower", "clock_ghz",
                                                        "clock_ghz_upper", "valu_insts_per_mfma",
                                                        "valu_coexec_frac_of_mfma_busy")}
+                xattn["pmc"]["source"] = os.path.relpath(attn_pmc, REPO)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.geometric:
             cpu = cpu_baseline(model, imgs, H, W)
