@@ -40,6 +40,19 @@ if ONLY:
     CONVS = [c for c in CONVS if c[0] in ONLY.split(",")]
 
 
+ROUNDS = int(os.environ.get("KB_ROUNDS", "1"))
+
+
+def interleaved(fns, reps):
+    """Median time of each fn over KB_ROUNDS rounds, the fns interleaved inside every round (the guide's rule: A/B
+    in one process, interleaved, so clock drift and the first-run penalty hit every variant alike)."""
+    ts = [[] for _ in fns]
+    for _ in range(ROUNDS):
+        for i, f in enumerate(fns):
+            ts[i].append(timeit(f, reps))
+    return [sorted(t)[len(t) // 2] for t in ts]
+
+
 def timeit(fn, reps):
     for _ in range(3):
         fn()
@@ -63,13 +76,21 @@ def main():
             W = (torch.randn(N, K, device="cuda") * K ** -0.5).to(dt)
             b = torch.randn(N, device="cuda")
             o = torch.empty(M, N, device="cuda", dtype=dt)
-            for var in VARIANTS:
-                nat.gemm_set_variant(var)
-                ms = timeit(lambda: nat.gemm(A, W, M, N, K, bias=b, out_lp=o), reps)
-                ms_t = (timeit(lambda: torch.nn.functional.linear(A, W, b.to(dt)), reps)
-                        if "torch" in sys.argv and var == VARIANTS[0] else 0)
-                print(f"gemm {name:10s} v{var:<4d} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s"
-                      + (f"   [hipBLASLt via torch: {2*M*N*K/ms_t/1e9:7.1f} TF/s]" if ms_t else ""), flush=True)
+            def run(var):
+                def f():
+                    nat.gemm_set_variant(var)
+                    nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
+                return f
+            fns = [run(v) for v in VARIANTS]
+            if "torch" in sys.argv:
+                fns.append(lambda: torch.nn.functional.linear(A, W, b.to(dt)))
+            mss = interleaved(fns, reps)
+            for var, ms in zip(VARIANTS, mss):
+                print(f"gemm {name:10s} v{var:<4d} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s",
+                      flush=True)
+            if "torch" in sys.argv:
+                print(f"gemm {name:10s} hipBLASLt via torch: {mss[-1]*1e3:8.1f} us  {2*M*N*K/mss[-1]/1e9:7.1f} TF/s",
+                      flush=True)
             nat.gemm_set_variant(0)
     if what in ("conv", "all"):
         for name, n, H, W_, C, Co in CONVS:
@@ -78,13 +99,12 @@ def main():
             b = torch.randn(Co, device="cuda")
             o = torch.empty(n * H * W_, Co, device="cuda", dtype=dt)
             M = n * H * W_
-            for var in VARIANTS:
-                nat.gemm_set_variant(var)
-                try:
-                    ms = timeit(lambda: nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1)), reps)
-                except nat.NativeError as e:
-                    print(f"conv {name:10s} v{var:<4d}: {e}", flush=True)
-                    continue
+            def runc(var):
+                def f():
+                    nat.gemm_set_variant(var)
+                    nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1))
+                return f
+            for var, ms in zip(VARIANTS, interleaved([runc(v) for v in VARIANTS], reps)):
                 print(f"conv {name:10s} v{var:<4d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
                       f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
             nat.gemm_set_variant(0)
