@@ -258,6 +258,9 @@ class PackedWeights:
             names = ("encoder.0.0.0.0", "encoder.0.0.1", "encoder.0.1", "encoder.1")
             geo[enc] = dict(lin=[(t(f"{enc}.{n}.weight"), t(f"{enc}.{n}.bias")) for n in names],
                             nw=t(f"{enc}.norm_layer.weight"), nb=t(f"{enc}.norm_layer.bias"))
+        # lazily built device state is shared by every stream that uses this engine (ranks on threads in the tests,
+        # a captured graph's side stream): finish building it before any other stream can read it
+        torch.cuda.current_stream(dev).synchronize()
         self._geo = geo
         return geo
 
@@ -278,7 +281,9 @@ class PackedWeights:
                                       antialias=False, scale_factor=(float(h0 + 0.1) / M, float(w0 + 0.1) / M))
                 patch = patch.permute(0, 2, 3, 1).reshape(-1, ENC_DIM)
                 out = torch.cat([pe[0, :1], patch], 0)
-            self.pos_cache[key] = out.contiguous().to(self.device)
+            out = out.contiguous().to(self.device)
+            torch.cuda.current_stream(self.device).synchronize()  # shared lazily built state (see geometric())
+            self.pos_cache[key] = out
         return self.pos_cache[key]
 
 
@@ -629,7 +634,9 @@ class MapaEngine:
     def _ones(self, n):
         o = getattr(self, "_ones_buf", None)
         if o is None or o.numel() < n:
-            o = self._ones_buf = torch.ones(max(n, 64), dtype=torch.float32, device=self.device)
+            o = torch.ones(max(n, 64), dtype=torch.float32, device=self.device)
+            torch.cuda.current_stream(self.device).synchronize()  # shared lazily built state (see geometric())
+            self._ones_buf = o
         return o
 
     def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, scale=None):
