@@ -83,6 +83,11 @@ typedef struct {
    * against weights packed [hi | lo | hi] — what out_s3 / mapa_split_bf16x3 / the split LayerNorm and bilinear
    * outputs store.  C % 8 == 0. */
   int a_split;
+  /* conv K order (MAPA_A_CONV3X3): 0 = tap-major, k = tap*C + c; B > 0 (B % 8 == 0, C % B == 0) = channel-block-major,
+   * k = (c / B)*9B + tap*B + c % B, with W's columns packed in the same order.  Consecutive K tiles then walk the 9
+   * taps of one B-channel slice, so the slice of the input window stays L2-resident across the taps instead of being
+   * re-fetched per tap (the head convs' fabric traffic: 9-20x their algorithmic bytes tap-major). */
+  int conv_kblock;
 } mapa_gemm_desc;
 
 int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);

@@ -114,7 +114,8 @@ __device__ __forceinline__ void stage_tile(const GemmArgs& p, char* lds, int buf
     if constexpr (AMODE == 0) {
       src = kin ? a_src[i] + koff - split_koff(p, kc, (int)sizeof(T)) : zero;
     } else {
-      const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
+      int tap, ci;
+      conv_kmap(p, kc, tap, ci);
       const int ky = tap / 3, kx = tap - ky * 3;
       const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
       const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
@@ -337,6 +338,9 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
                    d->conv_OH, d->conv_OW, oh, ow);
     MAPA_CHECK_ARG((int64_t)d->conv_OH * d->conv_OW > 0 && d->M % (d->conv_OH * d->conv_OW) == 0,
                    "mapa_gemm: conv M must be images * OH * OW");
+    MAPA_CHECK_ARG(d->conv_kblock == 0 || (d->conv_kblock > 0 && d->conv_kblock % 8 == 0 && d->conv_C % d->conv_kblock == 0),
+                   "mapa_gemm: conv_kblock=%d must be 0 or a multiple of 8 dividing conv_C=%d", d->conv_kblock,
+                   d->conv_C);
   } else {
     MAPA_CHECK_ARG(d->a_mode == MAPA_A_DENSE, "mapa_gemm: bad a_mode");
     MAPA_CHECK_ARG((d->a_split || d->lda >= d->K) && d->lda % E == 0, "mapa_gemm: lda must be >= K and keep 16-B rows");
@@ -363,6 +367,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   a.cv_stride = d->conv_stride;
   a.sp_half = 0x7fffffff;
   a.cv_Cp = d->conv_C;
+  a.cv_kb = d->a_mode == MAPA_A_CONV3X3 ? d->conv_kblock : 0;
   if (d->a_split) {
     a.sp_half = (d->a_mode == MAPA_A_CONV3X3 ? d->conv_C : d->K) / 3;
     if (d->a_mode == MAPA_A_CONV3X3) a.cv_Cp = 2 * a.sp_half;
@@ -384,6 +389,8 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
   if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
+  } else if (d->dtype == MAPA_BF16 && variant >= 2575 && variant <= 2579 && launch_gemm_8p(a, conv, variant - 2575, stream)) {
+    // launched
   } else if (d->dtype == MAPA_BF16 && (variant == 2590 || variant == 2591) &&
              launch_gemm_w4(a, conv, variant - 2590, stream)) {
     // launched
@@ -403,7 +410,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582) ||
+                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2582) ||
                      variant == 2590 || variant == 2591,
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;

@@ -67,7 +67,8 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
     if constexpr (AMODE == 0) {
       src = kin ? a_src[i] + koff - split_koff(p, kc, 2) : zero;
     } else {
-      const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
+      int tap, ci;
+      conv_kmap(p, kc, tap, ci);
       const int ky = tap / 3, kx = tap - ky * 3;
       const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
       const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
@@ -310,7 +311,8 @@ __global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
       if constexpr (AMODE == 0) {
         src = kin ? a_src[i] + (int64_t)kt * C::BK * 2 - split_koff(p, kc, 2) : zero;
       } else {
-        const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
+        int tap, ci;
+      conv_kmap(p, kc, tap, ci);
         const int ky = tap / 3, kx = tap - ky * 3;
         const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
         const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;

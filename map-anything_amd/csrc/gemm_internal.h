@@ -16,6 +16,7 @@ struct GemmArgs {
   // conv tap), physical [hi | lo] (2 * sp_half per row / pixel, cv_Cp); sp_half = INT_MAX when A is plain
   int sp_half;
   int cv_Cp;  // physical elements per input pixel (conv): cv_C, or 2 * sp_half for a compact split operand
+  int cv_kb;  // conv K order: 0 tap-major, else channel blocks of cv_kb (mapa_gemm_desc.conv_kblock)
   const float* bias;
   int bias_mod;
   const float* gamma;
@@ -59,6 +60,26 @@ __device__ __forceinline__ int split_col(const GemmArgs& p, int c) { return c - 
 // Byte correction of a dense A row address for logical column kc (0 for plain operands).
 __device__ __forceinline__ int64_t split_koff(const GemmArgs& p, int kc, int esz) {
   return kc >= p.sp_half ? (int64_t)p.sp_half * esz : 0;
+}
+
+// Logical K column kc of a 3x3 conv -> tap (0..8) and physical input column (split-aware), in the K order of
+// mapa_gemm_desc.conv_kblock.
+__device__ __forceinline__ void conv_kmap(const GemmArgs& p, int kc, int& tap, int& ci) {
+  int c;
+  if (p.cv_kb == 32) {  // the head convs' block: divisions by constants
+    const int blk = kc / 288, r = kc - blk * 288;
+    tap = r >> 5;
+    c = blk * 32 + (r & 31);
+  } else if (p.cv_kb > 0) {
+    const int span = 9 * p.cv_kb;
+    const int blk = kc / span, r = kc - blk * span;
+    tap = r / p.cv_kb;
+    c = blk * p.cv_kb + (r - tap * p.cv_kb);
+  } else {
+    tap = kc / p.cv_C;
+    c = kc - tap * p.cv_C;
+  }
+  ci = split_col(p, c);
 }
 
 __device__ __forceinline__ float epi_act(float v, int act) {
@@ -178,6 +199,9 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
 // 256-row bf16 kernel (gemm_big.hip): variant 0 = 256x256 tile, 1 = 256x128 tile.  Returns false if it does not
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
+
+// 256x256 bf16 kernel with the phase-interleaved (ping-pong, half-tile ring) main loop (gemm_8p.hip).
+bool launch_gemm_8p(const GemmArgs& a, bool conv, int diag, hipStream_t stream);
 
 // Four-wave 256-column bf16 kernel (gemm_w4.hip): variant 0 = 256x256 tile, 1 = 192x256 tile; 1 workgroup/CU.
 bool launch_gemm_w4(const GemmArgs& a, bool conv, int variant, hipStream_t stream);

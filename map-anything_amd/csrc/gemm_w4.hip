@@ -54,7 +54,8 @@ __device__ __forceinline__ void w4_stage(const GemmArgs& p, char* lds, int buf, 
     if constexpr (AMODE == 0) {
       src = kin ? a_src[i] + koff - split_koff(p, kc, 2) : zero;
     } else {
-      const int tap = kc / p.cv_C, ci = split_col(p, kc - tap * p.cv_C);
+      int tap, ci;
+      conv_kmap(p, kc, tap, ci);
       const int ky = tap / 3, kx = tap - ky * 3;
       const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
       const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;

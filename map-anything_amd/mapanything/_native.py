@@ -45,6 +45,7 @@ class GemmDesc(ctypes.Structure):
         ("out_mode", ctypes.c_int), ("ps_s", ctypes.c_int), ("ps_h", ctypes.c_int), ("ps_w", ctypes.c_int),
         ("ps_cout", ctypes.c_int), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("out_s3", ctypes.c_void_p), ("out_s3_relu", ctypes.c_void_p), ("a_split", ctypes.c_int),
+        ("conv_kblock", ctypes.c_int),
     ]
 
 
@@ -256,7 +257,8 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout).
     out_s3 / out_s3_relu: split-precision operand outputs (bf16 [rows][2*ldo], [hi | lo]).  A weight packed for split
     operands (W._mapa_split, engine._split_pack) marks A as a compact split operand (mapa_gemm_desc.a_split): K is
-    then the logical 3C, the stored A row 2C wide."""
+    then the logical 3C, the stored A row 2C wide.  A conv weight tagged W._mapa_kblock = B holds its columns in the
+    channel-block-major K order (mapa_gemm_desc.conv_kblock)."""
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype
@@ -270,6 +272,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     if conv is not None:
         d.a_mode = A_CONV3X3
         d.conv_C, d.conv_IH, d.conv_IW, d.conv_OH, d.conv_OW, d.conv_stride = conv
+        d.conv_kblock = getattr(W, "_mapa_kblock", 0)  # weights packed channel-block-major (engine.hconv3)
         d.lda = K
     d.bias = None if bias is None else bias.data_ptr()
     d.bias_mod = bias_mod

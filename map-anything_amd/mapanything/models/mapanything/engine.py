@@ -69,6 +69,9 @@ class GeoInputs:
         return not self.ray_views and not self.depth_views and not any(self.cam_mask)
 
 
+KBLOCK = 32  # channel block of the head convs' K order (include/mapa.h conv_kblock)
+
+
 def _split_pack(w: np.ndarray, dev) -> torch.Tensor:
     """[out][taps][cin] fp32 -> bf16 [out][taps * 3 * ceil8(cin)] = [hi | lo | hi] per tap: the weight side of a
     split-precision GEMM against activations stored [hi | lo] and read as [hi | hi | lo] (mapa_split_bf16x3 / the
@@ -126,8 +129,18 @@ class PackedWeights:
             return hpack(w.reshape(w.shape[0], 1, -1))
 
         def hconv3(name):
+            # columns in channel-block-major K order (mapa_gemm_desc.conv_kblock = KBLOCK): [out][C/B][tap][B] of
+            # the per-tap (logical, split-packed) channels, so each B-channel slice of the input window stays
+            # L2-resident across the 9 taps
             w = _np(g(f"{name}.weight"))
-            return hpack(w.transpose(0, 2, 3, 1).reshape(w.shape[0], 9, w.shape[1]))
+            t = hpack(w.transpose(0, 2, 3, 1).reshape(w.shape[0], 9, w.shape[1]))
+            o, c = t.shape[0], t.shape[1] // 9
+            if not KBLOCK or c % KBLOCK:
+                return t
+            r = t.view(o, 9, c // KBLOCK, KBLOCK).permute(0, 2, 1, 3).contiguous().reshape(o, -1)
+            r._mapa_split = getattr(t, "_mapa_split", False)
+            r._mapa_kblock = KBLOCK
+            return r
 
         def hconvT(name):
             w = _np(g(f"{name}.weight"))

@@ -62,7 +62,7 @@ def test_gemm_epilogues(nat):
     assert rel_l2(x.cpu(), (r1 + g * acc).cpu()) < 1e-4
 
 
-@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2590, 2591])
+@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2575, 2576, 2577, 2578, 2590, 2591])
 @pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72)])
 def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
     """Every 256-row schedule, incl. the stream-K ones (split tiles summed by the last arriver), on the path's
@@ -89,7 +89,7 @@ def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
         assert ws.numel() > 0 and int(ws[: 4 * 65536].count_nonzero()) == 0
 
 
-@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574, 2590, 2591])
+@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574, 2575, 2576, 2577, 2578, 2590, 2591])
 def test_conv3x3_big_variants(nat, variant):
     n, H, W, C, Co = 2, 37, 37, 256, 256
     x = _rand(n, C, H, W, seed=26).to(torch.bfloat16)
@@ -103,6 +103,32 @@ def test_conv3x3_big_variants(nat, variant):
     finally:
         nat.gemm_set_variant(0)
     assert rel_l2(out.view(n, H, W, Co).permute(0, 3, 1, 2).cpu(), ref.cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("variant,dtype", [(0, torch.bfloat16), (0, torch.float32), (2568, torch.bfloat16),
+                                           (2571, torch.bfloat16), (2575, torch.bfloat16), (2580, torch.bfloat16)])
+@pytest.mark.parametrize("n,H,W,C,Co,stride", [(2, 37, 37, 96, 256, 1), (1, 19, 19, 768, 128, 2)])
+def test_conv3x3_channel_block_k_order(nat, variant, dtype, n, H, W, C, Co, stride):
+    """conv_kblock = 32: the K index walks the 9 taps of each 32-channel slice (weights packed [out][C/32][tap][32])
+    and gives the conv of the tap-major packing, for every tile schedule."""
+    x = _rand(n, C, H, W, seed=40)
+    w = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=41)
+    b = _rand(Co, seed=42)
+    xl, wl = x.to(dtype), w.to(dtype)
+    ref = F.conv2d(xl.float(), wl.float(), b, stride=stride, padding=1)
+    OH, OW = ref.shape[-2:]
+    x_nhwc = xl.permute(0, 2, 3, 1).contiguous()
+    wkb = wl.permute(0, 2, 3, 1).reshape(Co, 9, C // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
+    wkb._mapa_kblock = 32
+    out = torch.empty(n * OH * OW, Co, device="cuda")
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(x_nhwc, wkb, n * OH * OW, Co, 9 * C, bias=b, out_f32=out, conv=(C, H, W, OH, OW, stride))
+        torch.cuda.synchronize()
+    finally:
+        nat.gemm_set_variant(0)
+    got = out.view(n, OH, OW, Co).permute(0, 3, 1, 2)
+    assert rel_l2(got.cpu(), ref.cpu()) < (1e-5 if dtype == torch.float32 else 1e-4)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
@@ -446,7 +472,8 @@ def test_split_bf16x3_is_bit_exact(nat, rows, cols, cp):
     assert torch.equal(y.view(torch.int16), ref.reshape(rows, -1).view(torch.int16))
 
 
-def test_split_precision_conv_matches_fp32(nat):
+@pytest.mark.parametrize("variant", [0, 2568, 2575, 2576])
+def test_split_precision_conv_matches_fp32(nat, variant):
     """A 3x3 conv run as one bf16 implicit-GEMM over split activations (stored [hi | lo], read [hi | hi | lo]) and
     [hi | lo | hi] weights (the geometric encoders' bf16-mode path) stays within ~1e-5 of the fp32 conv (plain
     bf16: ~3e-3)."""
@@ -466,7 +493,11 @@ def test_split_precision_conv_matches_fp32(nat):
     wp = wp.reshape(Co, -1)
     wp._mapa_split = True  # A is a compact split operand
     out = torch.empty(M, Co, device="cuda")
-    nat.gemm(a, wp, M, Co, 9 * 3 * cp, out_f32=out, conv=(3 * cp, h, w, h, w, 1))
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(a, wp, M, Co, 9 * 3 * cp, out_f32=out, conv=(3 * cp, h, w, h, w, 1))
+    finally:
+        nat.gemm_set_variant(0)
     assert rel_l2(out.cpu(), ref) < 2e-5
 
 

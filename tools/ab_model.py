@@ -1,0 +1,59 @@
+"""Same-process A/B of whole-model infer() on one GPU (the guide's rule: interleaved rounds, medians), for packing-time
+switches.  Usage: python tools/ab_model.py kblock [views] [rounds] [steps]
+  kblock: head convs with the channel-block-major K order (engine.KBLOCK = 32) vs tap-major (0)."""
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "map-anything_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+import torch  # noqa: E402
+
+from mapanything.models import MapAnything  # noqa: E402
+from mapanything.models.mapanything import engine  # noqa: E402
+from mapanything.utils import synthetic  # noqa: E402
+from tests_helpers import released_config  # noqa: E402
+
+
+def main():
+    what = sys.argv[1]
+    V = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    steps = int(sys.argv[4]) if len(sys.argv) > 4 else 5
+    dev = torch.device("cuda", 0)
+    imgs = synthetic.synthetic_images(V, 518, 518, seed=2)
+    views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in imgs]
+    if what == "kblock":
+        arms = [("kblock32", lambda: setattr(engine, "KBLOCK", 32)), ("tapmajor", lambda: setattr(engine, "KBLOCK", 0))]
+    else:
+        raise SystemExit(f"unknown A/B {what}")
+    models, sd = [], None
+    for name, setup in arms:
+        setup()
+        m = MapAnything(**released_config()).to(dev).eval()
+        if sd is None:
+            m.load_synthetic_weights()
+            sd = m._sd
+        else:
+            m._sd = sd
+        for _ in range(2):
+            m.infer(views)  # packs the weights under this arm's switch, captures the graph
+        models.append((name, m))
+    torch.cuda.synchronize()
+    ts = {n: [] for n, _ in models}
+    for _ in range(rounds):
+        for n, m in models:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                m.infer(views)
+            torch.cuda.synchronize()
+            ts[n].append((time.perf_counter() - t0) / steps * 1e3)
+    for n, t in ts.items():
+        t = sorted(t)
+        print(f"{what} {n:10s} median {t[len(t) // 2]:7.2f} ms/infer  min {t[0]:7.2f}  ({V * 1e3 / t[len(t) // 2]:.1f} views/s)")
+
+
+if __name__ == "__main__":
+    main()

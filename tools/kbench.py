@@ -1,6 +1,7 @@
 """Kernel micro-benchmark: TFLOP/s of the hot GEMM / conv / attention shapes of the 8-view 518x518 workload
 (HIP-event timing, random data).  Usage: python tools/kbench.py [gemm|attn|conv|all] [reps]
-KB_VARIANTS=0,2580,2568 sweeps GEMM/conv kernel variants (0 = the automatic choice; include/mapa.h)."""
+KB_VARIANTS=0,2580,2568 sweeps GEMM/conv kernel variants (0 = the automatic choice; include/mapa.h); KB_KBLOCK=0,32 runs
+the convs in the tap-major and the channel-block-major K order (interleaved)."""
 import os
 import sys
 
@@ -41,6 +42,7 @@ if ONLY:
 
 
 ROUNDS = int(os.environ.get("KB_ROUNDS", "1"))
+KBLOCKS = [int(v) for v in os.environ.get("KB_KBLOCK", "0").split(",")]
 
 
 def interleaved(fns, reps):
@@ -95,17 +97,25 @@ def main():
     if what in ("conv", "all"):
         for name, n, H, W_, C, Co in CONVS:
             x = (torch.randn(n, H, W_, C, device="cuda") * 0.5).to(dt)
-            w = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(dt)
+            w0 = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(dt)
             b = torch.randn(Co, device="cuda")
             o = torch.empty(n * H * W_, Co, device="cuda", dtype=dt)
             M = n * H * W_
-            def runc(var):
+            combos = []
+            for kb in KBLOCKS:  # channel-block-major K order (mapa_gemm_desc.conv_kblock)
+                w = w0
+                if kb and C % kb == 0:
+                    w = w0.view(Co, 9, C // kb, kb).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
+                    w._mapa_kblock = kb
+                combos += [(var, kb, w) for var in VARIANTS]
+
+            def runc(var, w):
                 def f():
                     nat.gemm_set_variant(var)
                     nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1))
                 return f
-            for var, ms in zip(VARIANTS, interleaved([runc(v) for v in VARIANTS], reps)):
-                print(f"conv {name:10s} v{var:<4d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
+            for (var, kb, _), ms in zip(combos, interleaved([runc(v, w) for v, _, w in combos], reps)):
+                print(f"conv {name:10s} v{var:<4d} kb{kb:<3d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
                       f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
             nat.gemm_set_variant(0)
     if what in ("attn", "all"):
