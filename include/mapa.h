@@ -95,9 +95,13 @@ int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
 int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
 /* Tuning / test hook: force one kernel variant for every later mapa_gemm call (0 = automatic per-shape choice,
  * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
- * 2560..2574 = 256-row tiles, 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without
- * one the automatic choice runs), 2590/2591 = four-wave 256x256 / 192x256 tiles. */
+ * 2560..2574 = 256-row tiles, 2575..2578 = phase-interleaved 256x256 tiles (2579 / 2583 timing diagnostics),
+ * 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one the automatic choice runs),
+ * 2584..2586 = LDS halo-window conv, 2590/2591 = four-wave 256x256 / 192x256 tiles. */
 int mapa_gemm_set_variant(int variant);
+/* Tuning / A-B hook: 0 keeps the stride-1 head convs (conv_kblock = 32) on the implicit-GEMM kernels instead of the
+ * LDS halo-window conv (default 1; 2584 / 2585 / 2586 force it: auto / 256- / 128-wide tiles). */
+int mapa_gemm_set_conv_halo(int on);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Flash attention forward, head_dim 64, non-causal, softmax scale `scale` (default 1/8; F.scaled_dot_product_attention at

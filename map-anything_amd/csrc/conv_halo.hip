@@ -1,0 +1,234 @@
+// 3x3 stride-1 convolution (pad 1) as an MFMA GEMM whose A operand is read from an LDS halo window, for gfx950.
+//
+//   out[img][oy][ox][n] = sum_{ky,kx,c} X[img][oy+ky-1][ox+kx-1][c] * W[n][c/32][ky*3+kx][c%32]   (+ fused epilogue)
+//
+// Why: the implicit-GEMM conv (gemm_big.hip, A mode 1) stages every input pixel once per tap — 9 copies of the
+// 256-pixel tile's neighbourhood per 32-channel slice through L2 -> LDS.  Timing without that A staging measured
+// 1.5-1.6x faster on the DPT head convs (rn1/l1rn at 148^2), so here the tile's 18x18 input window of a 32-channel
+// slice is DMA'd ONCE (20.7 KiB) and the 9 taps read their A fragments from it at shifted addresses: 7x less
+// operand staging for A.  Weights use the channel-block-major K order of mapa_gemm_desc.conv_kblock = 32, so K tile
+// kt is (slice kt / 9, tap kt % 9) and the W tile of kt is 32 contiguous columns.
+//  * Output tile: a 16x16 pixel block (M = 256 rows, pixel (py, px) = row py*16 + px) x BN output channels.
+//    BN = 256: 8 waves as 2 (M) x 4 (N), wave tile 128x64 (1 workgroup / CU); BN = 128: 4 x 2, wave tile 64x64,
+//    <= 128 VGPRs (2 workgroups / CU: one tile's epilogue overlaps the other's main loop).
+//  * A fragment (16x16x32 MFMA) for block row py and tap (ky, kx): lane (px, g) reads 16 B = channels 8g..8g+7 of
+//    window pixel wp = (py+ky)*18 + px+kx.  Window image: pixel-major, 64 B per pixel, 16-B chunk g stored at
+//    chunk g ^ ((wp >> 2) & 3): the 16 lanes of a row group hit 16 distinct 16-B bank slots (conflict-free).
+//  * W tiles (BN x 64 B, 16-B chunks XOR-swizzled as gemm_big's 64-B rows) stream through a ring of S slots,
+//    each DMA'd S-1 K tiles ahead; the window of slice c+1 rides in the DMA group of K tile 9(c+1) (two window
+//    buffers).  Counted vmcnt over the groups still in flight + raw s_barrier (no drain in the loop).
+#include "gemm_internal.h"
+
+namespace mapa_gemm_impl {
+namespace {
+
+constexpr int HT = 512;           // threads
+constexpr int HB = 16;            // output block edge (pixels)
+constexpr int WE = HB + 2;        // window edge
+constexpr int WPIX = WE * WE;     // 324 window pixels
+constexpr int WPIECES = WPIX * 4; // 16-B pieces per window (64 B per pixel)
+constexpr int WROUNDS = (WPIECES + HT - 1) / HT;  // 3 DMA instructions per thread per window
+constexpr int WBYTES = WROUNDS * HT * 16;         // 24 KiB per window buffer (tail pieces land in padding)
+constexpr int H_ELD = 68;
+
+template <int BN>
+struct HCfg {
+  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
+  static constexpr int TM = 256 / WM, TN = BN / WN;  // 128x64 or 64x64
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int S = BN == 256 ? 6 : 4;        // W ring slots
+  static constexpr int WT = BN * 64;                 // W tile bytes (32 bf16 per row)
+  static constexpr int NWG = WT / (HT * 16);         // W DMA instructions per thread per K tile (2 or 1)
+  static constexpr int LDS = S * WT + 2 * WBYTES;    // 144 KiB or 80 KiB
+  static constexpr int MINB = BN == 256 ? 1 : 2;
+  static_assert(TN == 64 && FM % 2 == 0, "epilogue: 64-column wave tiles, 32-row passes");
+  static_assert(8 * 32 * H_ELD * 4 <= LDS, "epilogue staging");
+};
+
+__device__ __forceinline__ int swz64(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
+
+template <int N>
+__device__ __forceinline__ void vm_wait_le() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// s_waitcnt vmcnt(n) for a runtime n in [0, 15]
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: vm_wait_le<0>(); break;
+    case 1: vm_wait_le<1>(); break;
+    case 2: vm_wait_le<2>(); break;
+    case 3: vm_wait_le<3>(); break;
+    case 4: vm_wait_le<4>(); break;
+    case 5: vm_wait_le<5>(); break;
+    case 6: vm_wait_le<6>(); break;
+    case 7: vm_wait_le<7>(); break;
+    case 8: vm_wait_le<8>(); break;
+    case 9: vm_wait_le<9>(); break;
+    case 10: vm_wait_le<10>(); break;
+    case 11: vm_wait_le<11>(); break;
+    case 12: vm_wait_le<12>(); break;
+    case 13: vm_wait_le<13>(); break;
+    case 14: vm_wait_le<14>(); break;
+    default: vm_wait_le<15>(); break;
+  }
+}
+
+// DMA group of K tile kt: its W tile (ring slot kt % S) and, on a slice's first tap, that slice's window (a device
+// function, not a lambda in the kernel: with a lambda the host pass drops the kernel's launch stub)
+template <int BN>
+__device__ __forceinline__ void halo_stage(const GemmArgs& p, char* wring, char* wins, int kt, int wave,
+                                           const char* const* w_src, const int64_t* wsrc, const bool* wok) {
+  using C = HCfg<BN>;
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  const char* abase = reinterpret_cast<const char*>(p.A);
+  char* dst = wring + (kt % C::S) * C::WT + wave * 1024;
+#pragma unroll
+  for (int i = 0; i < C::NWG; ++i)
+    __builtin_amdgcn_global_load_lds(w_src[i] + (int64_t)kt * 64, dst + i * 8192, 16, 0, 0);
+  const int slice = kt / 9;
+  if (kt - slice * 9 == 0) {
+    const int64_t ch = split_col(p, slice * 32);
+    char* wd = wins + (slice & 1) * WBYTES + wave * 1024;
+#pragma unroll
+    for (int r = 0; r < WROUNDS; ++r)
+      __builtin_amdgcn_global_load_lds(wok[r] ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16, 0, 0);
+  }
+}
+
+template <int BN>
+__global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs p) {
+  using C = HCfg<BN>;
+  __shared__ __attribute__((aligned(1024))) char lds[C::LDS];
+  char* const wring = lds;
+  char* const wins = lds + C::S * C::WT;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / C::WN, wn = wave % C::WN;
+  // ---- tile: (img, block row, block col, column tile), XCD-contiguous ranges of neighbouring blocks
+  const int nbx = (p.cv_OW + HB - 1) / HB, nby = (p.cv_OH + HB - 1) / HB, ntn = p.N / BN;
+  const int imgs = p.M / (p.cv_OH * p.cv_OW);
+  int t = xcd_remap(blockIdx.x, imgs * nby * nbx * ntn);
+  const int tn = t % ntn;
+  t /= ntn;
+  const int bx = t % nbx;
+  t /= nbx;
+  const int by = t % nby, img = t / nby;
+  const int bn = tn * BN;
+  const int nk = p.K / 32;  // 9 taps x (logical channels / 32)
+
+  // ---- window staging geometry (this thread's WROUNDS pieces; pixel offsets are slice-invariant)
+  int64_t wsrc[WROUNDS];
+  bool wok[WROUNDS];
+#pragma unroll
+  for (int r = 0; r < WROUNDS; ++r) {
+    const int q = r * HT + tid;
+    const int wp = q >> 2, cl = q & 3;
+    const int cs = cl ^ ((wp >> 2) & 3);
+    const int wy = wp / WE, wx = wp - wy * WE;
+    const int iy = by * HB - 1 + wy, ix = bx * HB - 1 + wx;
+    wok[r] = q < WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+    wsrc[r] = wok[r] ? ((int64_t)(img * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
+  }
+  // ---- W staging geometry: instruction i of this wave covers ring rows (i*8 + wave)*16 + [0, 16)
+  const char* w_src[C::NWG];
+#pragma unroll
+  for (int i = 0; i < C::NWG; ++i) {
+    const int r = (i * 8 + wave) * 16 + (lane >> 2);
+    const int sc = (lane & 3) ^ swz64(r);
+    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)(bn + r) * p.ldw + sc * 8) * 2;
+  }
+  f32x4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  const int g = lane >> 4, r16 = lane & 15;
+  int b_off[C::FN];
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) {
+    const int rb = wn * C::TN + j * 16 + r16;
+    b_off[j] = rb * 64 + ((g ^ swz64(rb)) << 4);
+  }
+  const int wp0 = (wm * C::FM) * WE + r16;  // window pixel of (block row wm*FM, px = r16) at tap (0, 0)
+
+#pragma unroll
+  for (int s0 = 0; s0 < C::S - 1; ++s0)
+    if (s0 < nk) halo_stage<BN>(p, wring, wins, s0, wave, w_src, wsrc, wok);
+  for (int kt = 0; kt < nk; ++kt) {
+    // groups issued after kt's: W tiles kt+1 .. kt+after, plus a window if one of them starts a slice
+    const int after = min(C::S - 2, nk - 1 - kt);
+    const int next9 = (kt / 9 + 1) * 9;
+    vm_wait(C::NWG * after + (next9 <= kt + after ? WROUNDS : 0));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + C::S - 1 < nk) halo_stage<BN>(p, wring, wins, kt + C::S - 1, wave, w_src, wsrc, wok);
+    const int slice = kt / 9, tap = kt - slice * 9;
+    const int ky = tap / 3, kx = tap - ky * 3;
+    const char* Ws = wring + (kt % C::S) * C::WT;
+    const char* Win = wins + (slice & 1) * WBYTES;
+    b8 b[C::FN];
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const b8*>(Ws + b_off[j]);
+    const int wpt = wp0 + ky * WE + kx;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const int wp = wpt + i * WE;
+      const b8 a = *reinterpret_cast<const b8*>(Win + ((wp << 2) + (g ^ ((wp >> 2) & 3))) * 16);
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // LDS becomes the epilogue staging area
+
+  // ---- epilogue: 32 rows (two block rows) x 64 fp32 per wave per pass through LDS, 16-B stores
+  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * H_ELD;
+  const int c4 = (lane & 15) * 4;
+  const int n0 = bn + wn * C::TN + c4;
+  const EpiCol ec = epi_col_setup(p, n0);
+#pragma unroll
+  for (int part = 0; part < C::FM / 2; ++part) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * H_ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 2
+    for (int pass = 0; pass < 8; ++pass) {
+      const int rloc = pass * 4 + g;  // row of the 32-row pass: block row wm*FM + part*2 + rloc/16, px rloc%16
+      const int oy = by * HB + wm * C::FM + part * 2 + (rloc >> 4), ox = bx * HB + (rloc & 15);
+      if (oy < p.cv_OH && ox < p.cv_OW)
+        epi_store_row<bf16_t>(p, ec, (img * p.cv_OH + oy) * p.cv_OW + ox,
+                              *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c4));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+}  // namespace
+
+// bn: 256 or 128 output channels per tile (0 = 256 when N % 256 == 0, else 128).  Needs a bf16 stride-1 conv in the
+// channel-block-major K order with 32-channel slices (conv_kblock == 32); returns false otherwise.
+bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream) {
+  if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
+  if (bn == 0) bn = a.N % 256 == 0 ? 256 : 128;
+  if (a.N % bn != 0 || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
+  const int hw = a.cv_OH * a.cv_OW;
+  const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + HB - 1) / HB) * ((a.cv_OW + HB - 1) / HB) * (a.N / bn);
+  if (tiles >= (int64_t(1) << 31)) return false;
+  if (bn == 256) hipLaunchKernelGGL(conv_halo_kernel<256>, dim3((unsigned)tiles), dim3(HT), 0, stream, a);
+  else hipLaunchKernelGGL(conv_halo_kernel<128>, dim3((unsigned)tiles), dim3(HT), 0, stream, a);
+  return true;
+}
+
+}  // namespace mapa_gemm_impl

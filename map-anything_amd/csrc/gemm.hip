@@ -288,6 +288,18 @@ int pick_variant(int dtype, bool conv, int M, int N, int K) {
   return 2571;
 }
 
+// LDS halo-window conv (conv_halo.hip) for stride-1 bf16 convs in the 32-channel-slice K order, when its 16x16-pixel
+// blocks fill the CUs (the 148^2 .. 518^2 DPT head convs); the small-image convs keep the implicit GEMM / stream-K.
+// Measured (kbench, 8 views): the 128-wide tile at 2 workgroups / CU beats the 256-wide one on every head conv
+// (reg2@518 1794 vs 2567 us, rn1@148 652 vs 781) and the implicit GEMM from 148^2 up (2207 / 734 us); at 74^2 and
+// below (<= 400 tiles) the implicit GEMM / stream-K stay ahead.
+static int g_halo = 1;  // mapa_gemm_set_conv_halo (tuning / A-B hook)
+static bool pick_halo(int M, int N, int OH, int OW, int kb) {
+  if (kb != 32 || !g_halo || N % 128 != 0) return false;
+  const int64_t blocks = (int64_t)(M / (OH * OW)) * ((OH + 15) / 16) * ((OW + 15) / 16);
+  return blocks * (N / 128) >= 512;
+}
+
 static int g_forced = -1;  // -1: not read yet; 0: automatic; else a kernel variant code (tuning / tests)
 
 static int forced_variant() {
@@ -387,9 +399,14 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int forced = forced_variant();
   const int variant = forced ? forced : pick_variant(d->dtype, conv, d->M, d->N, d->K);
   const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
+  const bool halo = conv && d->dtype == MAPA_BF16 &&
+                    (forced ? (forced >= 2584 && forced <= 2586) : pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb));
   if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
-  } else if (d->dtype == MAPA_BF16 && variant >= 2575 && variant <= 2579 && launch_gemm_8p(a, conv, variant - 2575, stream)) {
+  } else if (halo && launch_conv_halo(a, forced == 2585 ? 256 : 128, stream)) {
+    // launched (LDS halo-window conv)
+  } else if (d->dtype == MAPA_BF16 && ((variant >= 2575 && variant <= 2579) || variant == 2583) &&
+             launch_gemm_8p(a, conv, variant == 2583 ? 5 : variant - 2575, stream)) {
     // launched
   } else if (d->dtype == MAPA_BF16 && (variant == 2590 || variant == 2591) &&
              launch_gemm_w4(a, conv, variant - 2590, stream)) {
@@ -408,9 +425,14 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   return 0;
 }
 
+extern "C" int mapa_gemm_set_conv_halo(int on) {
+  g_halo = on ? 1 : 0;
+  return 0;
+}
+
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2582) ||
+                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2586) ||
                      variant == 2590 || variant == 2591,
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;

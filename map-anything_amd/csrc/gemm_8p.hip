@@ -154,8 +154,10 @@ __device__ __forceinline__ void p8_phase(const GemmArgs& p, char* lds, int blk, 
   // ---- DMA of half-tile ph + D
   {
     const int h = ph + C::D;
-    if ((DIAG & 1) == 0 && h < H)
-      p8_stage<AMODE, (P + C::D) & 3>(p, lds + ((P + C::D) % C::S) * P8_HALF + lds_wave, h >> 2, k_exact, s, w_sc);
+    constexpr int JS = (P + C::D) & 3;
+    constexpr bool SKIP = (DIAG & 1) != 0 || ((DIAG & 4) != 0 && (JS == 0 || JS == 3));  // diagnostics
+    if (!SKIP && h < H)
+      p8_stage<AMODE, JS>(p, lds + ((P + C::D) % C::S) * P8_HALF + lds_wave, h >> 2, k_exact, s, w_sc);
   }
   p8_vmwait(min(C::KF, H - 3 - C::BAL - ph));  // every half-tile <= ph + 2 + BAL landed
   __builtin_amdgcn_sched_barrier(0);
@@ -325,7 +327,8 @@ __global__ void __launch_bounds__(P8_THREADS, 1) gemm_8p_kernel(GemmArgs p) {
 }  // namespace
 
 // cfg: 0 = 10-slot ring (160 KiB) with balanced reads, 1 = 10 slots / W0 read with A0, 2 = 8 slots (128 KiB) /
-// balanced, 3 = 8 slots / W0 with A0; 4 = timing diagnostic of cfg 0 without the main-loop DMA (wrong results).
+// balanced, 3 = 8 slots / W0 with A0; 4 = timing diagnostic of cfg 0 without the main-loop DMA, 5 = of cfg 1
+// without the main-loop A DMA (both wrong results).
 bool launch_gemm_8p(const GemmArgs& a, bool conv, int cfg, hipStream_t stream) {
   const int nblk = ((a.M + 255) / 256) * ((a.N + 255) / 256);
   void (*k)(GemmArgs) = nullptr;
@@ -337,6 +340,9 @@ bool launch_gemm_8p(const GemmArgs& a, bool conv, int cfg, hipStream_t stream) {
     case 4:
       if (conv) return false;
       k = gemm_8p_kernel<P8Cfg<10, 1>, 0, 1>;
+      break;
+    case 5:  // timing diagnostic of cfg 1 without the main-loop A DMA (wrong results)
+      k = conv ? gemm_8p_kernel<P8Cfg<10, 0>, 1, 4> : gemm_8p_kernel<P8Cfg<10, 0>, 0, 4>;
       break;
     default: return false;
   }

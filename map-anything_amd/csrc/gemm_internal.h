@@ -203,6 +203,10 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
 // 256x256 bf16 kernel with the phase-interleaved (ping-pong, half-tile ring) main loop (gemm_8p.hip).
 bool launch_gemm_8p(const GemmArgs& a, bool conv, int diag, hipStream_t stream);
 
+// Stride-1 3x3 conv with its A operand read from an LDS halo window (conv_halo.hip); bn = 256 / 128 / 0 (auto).
+// Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).
+bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream);
+
 // Four-wave 256-column bf16 kernel (gemm_w4.hip): variant 0 = 256x256 tile, 1 = 192x256 tile; 1 workgroup/CU.
 bool launch_gemm_w4(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
 

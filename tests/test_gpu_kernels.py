@@ -131,6 +131,69 @@ def test_conv3x3_channel_block_k_order(nat, variant, dtype, n, H, W, C, Co, stri
     assert rel_l2(got.cpu(), ref.cpu()) < (1e-5 if dtype == torch.float32 else 1e-4)
 
 
+@pytest.mark.parametrize("variant", [2584, 2585, 2586])
+@pytest.mark.parametrize("n,H,W,C,Co", [(2, 37, 29, 96, 256), (1, 50, 48, 256, 128), (3, 16, 16, 32, 256),
+                                        (1, 148, 148, 256, 256)])
+def test_conv3x3_halo_window(nat, variant, n, H, W, C, Co):
+    """The LDS halo-window conv (16x16-pixel blocks, 18x18 window per 32-channel slice, the 9 taps read at shifted
+    window addresses): ragged blocks at the image edges, zero padding, fused epilogue (bias, ReLU, residual, bf16 +
+    fp32 + split outputs), both tile widths."""
+    x = _rand(n, C, H, W, seed=50)
+    w = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=51)
+    b, r = _rand(Co, seed=52), _rand(n * H * W, Co, seed=53)
+    xl, wl = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    ref = F.conv2d(xl.float(), wl.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    ref = r + torch.relu(ref)
+    x_nhwc = xl.permute(0, 2, 3, 1).contiguous()
+    wkb = wl.permute(0, 2, 3, 1).reshape(Co, 9, C // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
+    wkb._mapa_kblock = 32
+    M = n * H * W
+    out = torch.empty(M, Co, device="cuda")
+    lp = torch.empty(M, Co, device="cuda", dtype=torch.bfloat16)
+    s3 = torch.empty(M, 2 * Co, device="cuda", dtype=torch.bfloat16)
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(x_nhwc, wkb, M, Co, 9 * C, bias=b, act=nat.ACT_RELU, resid1=r, out_f32=out, out_lp=lp, out_s3=s3,
+                 conv=(C, H, W, H, W, 1))
+        again = torch.empty_like(out)
+        nat.gemm(x_nhwc, wkb, M, Co, 9 * C, bias=b, act=nat.ACT_RELU, resid1=r, out_f32=again,
+                 conv=(C, H, W, H, W, 1))
+        torch.cuda.synchronize()
+    finally:
+        nat.gemm_set_variant(0)
+    assert rel_l2(out.cpu(), ref.cpu()) < 1e-4
+    assert rel_l2(lp.float().cpu(), ref.cpu()) < 5e-3
+    assert torch.equal(s3, _split_expect(out))
+    assert torch.equal(out, again)
+
+
+def test_split_precision_conv_halo_window(nat):
+    """Split-precision activations ([hi | lo] stored, [hi | hi | lo] logical, 32-channel slices mapped per slice)
+    through the halo-window conv stay within ~1e-5 of the fp64 conv."""
+    n, h, w, C, Co = 2, 37, 37, 256, 256
+    x = _rand(n, C, h, w, seed=54)
+    wt = _rand(Co, C, 3, 3, scale=C ** -0.5 / 3, seed=55)
+    ref = F.conv2d(x.cpu().double(), wt.cpu().double(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    M = n * h * w
+    xr = x.permute(0, 2, 3, 1).reshape(M, C).contiguous()
+    a = torch.empty(M, 2 * C, dtype=torch.bfloat16, device="cuda")
+    nat.split_bf16x3(xr, M, C, C, a)
+    wk = wt.permute(0, 2, 3, 1).reshape(Co, 9, C)
+    whi = wk.to(torch.bfloat16)
+    wlo = (wk - whi.float()).to(torch.bfloat16)
+    wp = torch.stack([whi, wlo, whi], 2).reshape(Co, 9, 3 * C)  # [out][tap][hi | lo | hi]
+    wp = wp.reshape(Co, 9, 3 * C // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
+    wp._mapa_split = True
+    wp._mapa_kblock = 32
+    out = torch.empty(M, Co, device="cuda")
+    nat.gemm_set_variant(2584)
+    try:
+        nat.gemm(a, wp, M, Co, 9 * 3 * C, out_f32=out, conv=(3 * C, h, w, h, w, 1))
+    finally:
+        nat.gemm_set_variant(0)
+    assert rel_l2(out.cpu(), ref) < 2e-5
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("n,H,W,C,Co,stride", [(2, 19, 19, 96, 256, 1), (1, 37, 37, 768, 768, 2),
                                               (3, 16, 20, 128, 128, 1), (1, 8, 8, 256, 6, 1)])

@@ -1,6 +1,7 @@
 """Same-process A/B of whole-model infer() on one GPU (the guide's rule: interleaved rounds, medians), for packing-time
 switches.  Usage: python tools/ab_model.py kblock [views] [rounds] [steps]
-  kblock: head convs with the channel-block-major K order (engine.KBLOCK = 32) vs tap-major (0)."""
+  kblock: head convs with the channel-block-major K order (engine.KBLOCK = 32) vs tap-major (0);
+  halo: stride-1 head convs on the LDS halo-window kernel vs the implicit GEMM."""
 import os
 import sys
 import time
@@ -24,8 +25,12 @@ def main():
     dev = torch.device("cuda", 0)
     imgs = synthetic.synthetic_images(V, 518, 518, seed=2)
     views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in imgs]
+    from mapanything import _native as nat
+
     if what == "kblock":
         arms = [("kblock32", lambda: setattr(engine, "KBLOCK", 32)), ("tapmajor", lambda: setattr(engine, "KBLOCK", 0))]
+    elif what == "halo":  # the kernel choice is baked into each model's captured graph at its first infer
+        arms = [("halo", lambda: nat.gemm_set_conv_halo(True)), ("implicit", lambda: nat.gemm_set_conv_halo(False))]
     else:
         raise SystemExit(f"unknown A/B {what}")
     models, sd = [], None
@@ -39,11 +44,12 @@ def main():
             m._sd = sd
         for _ in range(2):
             m.infer(views)  # packs the weights under this arm's switch, captures the graph
-        models.append((name, m))
+        models.append((name, m, setup))
     torch.cuda.synchronize()
-    ts = {n: [] for n, _ in models}
+    ts = {n: [] for n, _, _ in models}
     for _ in range(rounds):
-        for n, m in models:
+        for n, m, setup in models:
+            setup()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(steps):

@@ -7,6 +7,6 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_s
 for i in 1 2; do
   for v in new $MAPA_AB_BENCH; do
     if [ $v = new ]; then lib=; else lib=$PWD/ab_libs/$v/libmapa.so; fi
-    echo "== $v"; timeout -k 10 120 MAPA_AB_LIB=$lib python tools/kbench.py attn 40 || exit 1
+    echo "== $v"; MAPA_AB_LIB=$lib timeout -k 10 120 python tools/kbench.py attn 40 || exit 1
   done
 done
