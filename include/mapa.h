@@ -99,9 +99,13 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
  * 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one the automatic choice runs),
  * 2584..2586 = LDS halo-window conv, 2590/2591 = four-wave 256x256 / 192x256 tiles. */
 int mapa_gemm_set_variant(int variant);
-/* Tuning / A-B hook: 0 keeps the stride-1 head convs (conv_kblock = 32) on the implicit-GEMM kernels instead of the
- * LDS halo-window conv (default 1; 2584 / 2585 / 2586 force it: auto / 256- / 128-wide tiles). */
-int mapa_gemm_set_conv_halo(int on);
+/* Tuning / A-B hooks of the automatic kernel choice (process-wide):
+ *   MAPA_TUNE_CONV_HALO (default 1): stride-1 bf16 convs in the 32-channel-slice K order (conv_kblock = 32) run on
+ *     the LDS halo-window conv; 0 keeps them on the implicit GEMM (variants 2584 / 2585 / 2586 force it);
+ *   MAPA_TUNE_TAIL_STREAMK (default 0): dense bf16 GEMMs whose 256x128 tiles leave a nearly empty last wave use
+ *     the tail-only stream-K schedule (2582) when a workspace is passed. */
+enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1 };
+int mapa_gemm_tune(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Flash attention forward, head_dim 64, non-causal, softmax scale `scale` (default 1/8; F.scaled_dot_product_attention at

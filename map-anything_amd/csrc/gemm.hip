@@ -293,7 +293,8 @@ int pick_variant(int dtype, bool conv, int M, int N, int K) {
 // Measured (kbench, 8 views): the 128-wide tile at 2 workgroups / CU beats the 256-wide one on every head conv
 // (reg2@518 1794 vs 2567 us, rn1@148 652 vs 781) and the implicit GEMM from 148^2 up (2207 / 734 us); at 74^2 and
 // below (<= 400 tiles) the implicit GEMM / stream-K stay ahead.
-static int g_halo = 1;  // mapa_gemm_set_conv_halo (tuning / A-B hook)
+static int g_halo = 1;     // mapa_gemm_tune(MAPA_TUNE_CONV_HALO, .)
+static int g_tail_sk = 0;  // mapa_gemm_tune(MAPA_TUNE_TAIL_STREAMK, .)
 static bool pick_halo(int M, int N, int OH, int OW, int kb) {
   if (kb != 32 || !g_halo || N % 128 != 0) return false;
   const int64_t blocks = (int64_t)(M / (OH * OW)) * ((OH + 15) / 16) * ((OW + 15) / 16);
@@ -323,8 +324,15 @@ int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   if (f) return f >= 2580 && f <= 2582 ? f : 0;
   if (dtype != MAPA_BF16) return 0;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
-  (void)conv;
-  return (big_tiles < 256 && K >= 4096) ? 2580 : 0;
+  if (big_tiles < 256 && K >= 4096) return 2580;
+  // tail-only stream-K where the 256x128 data-parallel schedule leaves a nearly empty last wave (enc.qkv / aat.fc1
+  // at 8 views: 1032 tiles on 512 slots -> a third wave of 8 tiles)
+  if (g_tail_sk && !conv) {
+    const int slots = gemm_streamk_slots(2);
+    const int64_t rem = big_tiles % slots;
+    if (big_tiles > slots && rem > 0 && rem * 8 < slots) return 2582;
+  }
+  return 0;
 }
 
 }  // namespace mapa_gemm_impl
@@ -425,8 +433,10 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   return 0;
 }
 
-extern "C" int mapa_gemm_set_conv_halo(int on) {
-  g_halo = on ? 1 : 0;
+extern "C" int mapa_gemm_tune(int key, int value) {
+  MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK, "mapa_gemm_tune: unknown key %d", key);
+  if (key == MAPA_TUNE_CONV_HALO) g_halo = value ? 1 : 0;
+  else g_tail_sk = value ? 1 : 0;
   return 0;
 }
 

@@ -29,7 +29,7 @@ EXPORTED = (
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
-    "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_set_conv_halo",
+    "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_tune",
 )
 
 
@@ -88,7 +88,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_gemm_workspace_bytes.argtypes = [ctypes.POINTER(GemmDesc)]
     L.mapa_gemm_workspace_bytes.restype = i64
     L.mapa_gemm_set_variant.argtypes = [i]
-    L.mapa_gemm_set_conv_halo.argtypes = [i]
+    L.mapa_gemm_tune.argtypes = [i, i]
     L.mapa_attention.argtypes = [ctypes.POINTER(AttnDesc), vp]
     L.mapa_attention_workspace_bytes.argtypes = [ctypes.POINTER(AttnDesc)]
     L.mapa_attention_workspace_bytes.restype = i64
@@ -246,9 +246,14 @@ def attention_workspace(d) -> torch.Tensor:
     return ws
 
 
-def gemm_set_conv_halo(on: bool = True):
-    """A-B hook: route the stride-1 head convs to the LDS halo-window kernel (default) or the implicit GEMM."""
-    check(lib().mapa_gemm_set_conv_halo(1 if on else 0), "mapa_gemm_set_conv_halo")
+TUNE_CONV_HALO, TUNE_TAIL_STREAMK = 0, 1
+
+
+def gemm_tune(key: int, value: int):
+    """A-B hooks of the automatic kernel choice (include/mapa.h mapa_gemm_tune): TUNE_CONV_HALO (stride-1 head convs
+    on the LDS halo-window kernel, default on), TUNE_TAIL_STREAMK (tail-only stream-K for nearly empty last waves)."""
+    check(lib().mapa_gemm_tune(key, value), "mapa_gemm_tune")
+    _WS_NEED.clear()
 
 
 def gemm_set_variant(variant: int = 0):

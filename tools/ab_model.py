@@ -1,7 +1,8 @@
 """Same-process A/B of whole-model infer() on one GPU (the guide's rule: interleaved rounds, medians), for packing-time
 switches.  Usage: python tools/ab_model.py kblock [views] [rounds] [steps]
   kblock: head convs with the channel-block-major K order (engine.KBLOCK = 32) vs tap-major (0);
-  halo: stride-1 head convs on the LDS halo-window kernel vs the implicit GEMM."""
+  halo: stride-1 head convs on the LDS halo-window kernel vs the implicit GEMM;
+  tailsk: tail-only stream-K for the GEMMs with a nearly empty last wave vs data-parallel."""
 import os
 import sys
 import time
@@ -30,7 +31,11 @@ def main():
     if what == "kblock":
         arms = [("kblock32", lambda: setattr(engine, "KBLOCK", 32)), ("tapmajor", lambda: setattr(engine, "KBLOCK", 0))]
     elif what == "halo":  # the kernel choice is baked into each model's captured graph at its first infer
-        arms = [("halo", lambda: nat.gemm_set_conv_halo(True)), ("implicit", lambda: nat.gemm_set_conv_halo(False))]
+        arms = [("halo", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 1)),
+                ("implicit", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 0))]
+    elif what == "tailsk":
+        arms = [("tailsk", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 1)),
+                ("dataparallel", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 0))]
     else:
         raise SystemExit(f"unknown A/B {what}")
     models, sd = [], None
