@@ -23,7 +23,9 @@ from collections import defaultdict
 
 
 def group(name: str) -> str:
-    m = re.search(r"gemm_big_kernel<(\d)", name)
+    if "conv_halo_kernel" in name:
+        return "conv3x3"
+    m = re.search(r"gemm_(?:big|8p|w4)_kernel<(?:[^,<>]*P8Cfg<[^>]*>, )?(\d)", name)
     if m:
         return "conv3x3" if m.group(1) == "1" else "gemm"
     m = re.search(r"gemm_kernel<[^,]*Traits\w+, (\d)", name)
@@ -38,7 +40,7 @@ def group(name: str) -> str:
 
 def _is_gemm(name):
     return "gemm_big_kernel" in name or "gemm_kernel<" in name or "gemm_sk_kernel" in name or \
-        "gemm_pp_kernel" in name or "gemm_w4" in name
+        "gemm_pp_kernel" in name or "gemm_w4" in name or "gemm_8p_kernel" in name or "conv_halo_kernel" in name
 
 
 def dispatch_kinds(names, log_path):

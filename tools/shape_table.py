@@ -46,6 +46,8 @@ def mean(xs, key):
 
 
 def tile_of(name):
+    if "conv_halo_kernel" in name:
+        return None  # halo conv: staged bytes are not (BM + BN) x K
     m = re.search(r"gemm_big_kernel<(\d), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)>", name)
     if m:
         return int(m.group(8)), int(m.group(2))
@@ -95,7 +97,8 @@ def table(root, kind):
             row["hipblaslt_us"], row["hipblaslt_tflops"] = blas_t[name]
             row["vs_hipblaslt"] = row["hipblaslt_us"] / row["us"]
         k = cf[i][0]["name"] if cf[i] else ""
-        row["kernel"] = re.sub(r"\(.*", "", k).replace("void mapa_gemm_impl::(anonymous namespace)::", "")
+        row["kernel"] = re.sub(r"\(mapa_gemm_impl::GemmArgs.*|\(mapa_gemm_impl::\(anonymous.*", "", k).replace(
+            "void mapa_gemm_impl::(anonymous namespace)::", "")
         fb, wb = mean(cf[i], "FETCH_SIZE"), mean(cw[i], "WRITE_SIZE")
         if fb is not None and wb is not None:
             row["fabric_bytes"] = 2048.0 * fb + 1024.0 * wb
