@@ -118,6 +118,17 @@ def main():
                 print(f"conv {name:10s} v{var:<4d} kb{kb:<3d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
                       f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
             nat.gemm_set_variant(0)
+    if what == "bil":  # the DPT resizes: 2x align_corners upsamples and the regressor's 296^2 -> 518^2 split resize
+        cases = [("up148", 74, 74, 148, 256, torch.float32, torch.float32), ("reg518", 296, 296, 518, 128,
+                                                                              torch.float32, "s3")]
+        for name, IH, IW, O, C, ti, to in cases:
+            x = torch.randn(V, IH, IW, C, device="cuda", dtype=ti)
+            o = torch.empty(V, O, O, 2 * C if to == "s3" else C, device="cuda",
+                            dtype=torch.bfloat16 if to == "s3" else to)
+            f = lambda: nat.bilinear_ac(x, V, IH, IW, C, O, O, O, O, o, split_out=(to == "s3"))  # noqa: E731
+            ms = timeit(f, reps)
+            nbytes = x.numel() * x.element_size() + o.numel() * o.element_size()
+            print(f"bil {name:8s} {IH}->{O} C={C}: {ms*1e3:8.1f} us  {nbytes/ms/1e9:6.2f} TB/s (in + out once)", flush=True)
     if what in ("attn", "all"):
         cases = [("enc", V, 16, T + 1), ("frame", V, 12, T), ("global", 1, 12, L)]
         if os.environ.get("KB_ATTN_WIDE"):

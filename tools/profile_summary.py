@@ -25,7 +25,7 @@ from collections import defaultdict
 def group(name: str) -> str:
     if "conv_halo_kernel" in name:
         return "conv3x3"
-    m = re.search(r"gemm_(?:big|8p|w4)_kernel<(?:[^,<>]*P8Cfg<[^>]*>, )?(\d)", name)
+    m = re.search(r"gemm_(?:big|8p|w4|sk)_kernel<(?:[^,<>]*P8Cfg<[^>]*>, )?(\d)", name)
     if m:
         return "conv3x3" if m.group(1) == "1" else "gemm"
     m = re.search(r"gemm_kernel<[^,]*Traits\w+, (\d)", name)
