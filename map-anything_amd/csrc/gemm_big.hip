@@ -833,6 +833,9 @@ bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, in
     s.dp_tiles = (dp_env && tiles >= 2 * g) ? (int)((tiles / g - 1) * g) : 0;
     s.base = s.dp_tiles * s.nk;
     s.per = (s.total - s.base + g - 1) / g;
+    // at least a tenth of a tile's K per block: past ~10 contributors per tile the last arriver's serial slab sum
+    // dominates (kbench, 8 views: rn4@19 80 -> 55 us, layer4_rn 119 -> 87; the 37^2 convs already split coarser)
+    s.per = std::max(s.per, s.nk / 10);
     static const int per_env = getenv("MAPA_SK_PER") ? atoi(getenv("MAPA_SK_PER")) : 0;  // tuning: iterations/block
     if (per_env > s.per) s.per = per_env;  // only coarser: G stays within the workspace's slab count
     G = (s.total - s.base + s.per - 1) / s.per;
