@@ -422,10 +422,13 @@ __global__ void __launch_bounds__(256) attn_split_merge(AttnArgs p, SplitArgs sp
   const int qrow = qt * QBLK_WG + r;
   if (qrow >= p.seq_q) return;
   const int s0 = tt * sp.chunks;
+  // unrolled so the chunks' loads are in flight together (the merge is latency-bound: ~43 chunks per row)
   float mx = -INFINITY;
+#pragma unroll 8
   for (int c = 0; c < sp.chunks; ++c) mx = fmaxf(mx, sp.part_lse[(int64_t)(s0 + c) * QBLK_WG + r]);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   float wsum = 0.f;
+#pragma unroll 8
   for (int c = 0; c < sp.chunks; ++c) {
     const float w = __expf(sp.part_lse[(int64_t)(s0 + c) * QBLK_WG + r] - mx);
     wsum += w;

@@ -7,6 +7,9 @@ import torch  # noqa: E402
 
 from mapanything import _native as nat  # noqa: E402
 
+if os.environ.get("MAPA_AB_LIB"):  # A/B builds: load before any other call
+    nat.load_library(os.environ["MAPA_AB_LIB"])
+
 B, Hh, S, reps = (int(x) for x in (sys.argv[1:5] if len(sys.argv) >= 5 else (1, 12, 8 * 1369 + 1, 10)))
 C = Hh * 64
 qkv = torch.randn(B * S, 3 * C, device="cuda").to(torch.bfloat16)
