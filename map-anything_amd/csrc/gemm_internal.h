@@ -207,6 +207,10 @@ bool launch_gemm_8p(const GemmArgs& a, bool conv, int diag, hipStream_t stream);
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).
 bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream);
 
+// Four-wave bf16 kernel with inline-asm MFMAs on AGPR accumulators and an explicitly ordered main loop
+// (gemm_w4a.hip): variant 0 = 256x256, 1 = 192x256; dense A with K % 32 == 0.  false if it does not take the shape.
+bool launch_gemm_w4a(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
+
 // Four-wave 256-column bf16 kernel (gemm_w4.hip): variant 0 = 256x256 tile, 1 = 192x256 tile; 1 workgroup/CU.
 bool launch_gemm_w4(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
 
