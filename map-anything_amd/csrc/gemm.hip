@@ -272,6 +272,7 @@ void launch_variant(int variant, int nblk, hipStream_t stream, const GemmArgs& a
 //   2568 = 256x256 tile, 1 workgroup/CU, s_setprio around the MFMA bursts (long K, wide convs)
 //   2570/2571 = 256x128 tile, 2 workgroups/CU (one tile's epilogue overlaps the other's main loop)
 //   2574 = 192x256 tile, 1 workgroup/CU (tile quantization: more tiles in the one wave)
+//   2587 = 192x192 tile, 1 workgroup/CU (N = 768: a fuller single wave)
 //   1282 / 643 = 128x128 tiles (fp32 parity mode; problems too small to fill the chip with 256-row tiles)
 int pick_variant(int dtype, bool conv, int M, int N, int K) {
   if (dtype != MAPA_BF16) return (conv || K < 1024) ? 643 : 1282;
@@ -281,6 +282,10 @@ int pick_variant(int dtype, bool conv, int M, int N, int K) {
   // N <= 1024 linears at 8 views (M = 10960: 58 vs 43 row tiles) and the 74x74 DPT convs
   const int64_t t192 = (int64_t)((M + 191) / 192) * ((N + 255) / 256);
   const int64_t t256 = (int64_t)((M + 255) / 256) * ((N + 255) / 256);
+  // 192x192 when it still fits one wave and N is a multiple of 192 (N = 768 at 8 views: 232 tiles instead of 174
+  // of 192x256; kbench aat.proj 29.3 -> 27.3 us, aat.fc2 68.8 -> 62.1)
+  const int64_t t192sq = (int64_t)((M + 191) / 192) * ((N + 191) / 192);
+  if (!conv && N % 192 == 0 && t192sq <= 256 && t192sq > t192) return 2587;
   if (t192 <= 256 && t256 <= 192 && N >= 256) return 2574;
   if (conv) return N >= 256 ? 2568 : 2571;
   if (K >= 4096) return 2568;
@@ -422,8 +427,8 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   } else if (d->dtype == MAPA_BF16 && (variant == 2590 || variant == 2591) &&
              launch_gemm_w4(a, conv, variant - 2590, stream)) {
     // launched
-  } else if (d->dtype == MAPA_BF16 && variant >= 2560 && variant <= 2574 &&
-             launch_gemm_big(a, conv, variant - 2560, stream)) {
+  } else if (d->dtype == MAPA_BF16 && ((variant >= 2560 && variant <= 2574) || variant == 2587) &&
+             launch_gemm_big(a, conv, variant == 2587 ? 15 : variant - 2560, stream)) {
     // launched
   } else if (d->dtype == MAPA_BF16) {
     if (conv) launch_variant<TraitsBF16, 1>(variant, nblk, stream, a);
@@ -445,7 +450,7 @@ extern "C" int mapa_gemm_tune(int key, int value) {
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2586) ||
+                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2587) ||
                      variant == 2590 || variant == 2591 || variant == 2592 || variant == 2593,
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;

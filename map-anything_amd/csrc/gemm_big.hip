@@ -24,7 +24,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));                 
 
 template <int BN, int RB, int BM = BBM>
 struct Cfg {
-  static constexpr int WM = BN == 256 ? 2 : 4;
+  static constexpr int WM = (BN == 256 || BN == 192) ? 2 : 4;
   static constexpr int WN = 8 / WM;
   static constexpr int TM = BM / WM, TN = BN / WN;  // TN = 64 (256-wide) or 32..64
   static constexpr int FM = TM / 16, FN = TN / 16;
@@ -36,7 +36,7 @@ struct Cfg {
   static constexpr int STAGE = A_BYTES + B_BYTES;
   static constexpr int NLA = BM / (8 * RPI), NLB = BN / (8 * RPI);  // wave instructions per thread per tile
   static_assert(BM % (8 * RPI) == 0 && BN % (8 * RPI) == 0, "whole 1-KiB wave instructions per operand");
-  static_assert(TN == 64 && FM % 2 == 0, "epilogue: 64-column wave tiles, 32-row passes");
+  static_assert(TN <= 64 && TN % 16 == 0 && FM % 2 == 0, "epilogue: <= 64-column wave tiles, 32-row passes");
   static constexpr int EPI = 8 * 32 * ELD * 4;
 };
 
@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (n0 < p.N) {
+    if (n0 < p.N && c4 < C::TN) {
 #pragma unroll 2
       for (int pass = 0; pass < 8; ++pass) {
         const int rloc = pass * 4 + g;
@@ -725,9 +725,9 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream) {
   // variant: 0 = 256x256 / 128-B rows / 2 stages, 1 = 256x128 / 128 / 2, 2 = 256x256 / 64-B rows / 4 stages,
   //          3 = 256x128 / 64 / 4, 4 = 256x128 / 64 / 6, 5 = 256x128 / 128 / 3
-  static const int bns[15] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128, 256, 256, 256};
-  static const int bms[15] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 192};
-  if (variant < 0 || variant > 14) return false;
+  static const int bns[16] = {256, 128, 256, 128, 128, 128, 256, 256, 256, 128, 128, 128, 256, 256, 256, 192};
+  static const int bms[16] = {256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 256, 192, 192};
+  if (variant < 0 || variant > 15) return false;
   if (conv && (variant == 6 || variant == 7)) return false;  // diagnostics exist for dense A only
   const int BN = bns[variant];
   const int BMv = bms[variant];
@@ -756,6 +756,10 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
     // 192-row tiles: 10960 rows -> 58 row tiles, so N = 1024 gives 232 tiles for 256 CUs (256-row: 172)
     case 14:
       k = conv ? gemm_big_kernel<1, 256, 128, 2, 0, 1, 1, 192> : gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192>;
+      break;
+    // 192x192 tiles (wave tile 96x48): N = 768 at 8 views -> 232 tiles, one wave on the CUs (192x256: 174 tiles)
+    case 15:
+      k = conv ? gemm_big_kernel<1, 192, 128, 2, 0, 1, 1, 192> : gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192>;
       break;
   }
 #undef MAPA_BIG

@@ -63,7 +63,7 @@ def test_gemm_epilogues(nat):
 
 
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2575, 2576, 2577, 2578, 2590, 2591,
-                                     2592, 2593])
+                                     2592, 2593, 2587])
 @pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72)])
 def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
     """Every 256-row schedule, incl. the stream-K ones (split tiles summed by the last arriver), on the path's
