@@ -118,6 +118,14 @@ def main():
                 print(f"conv {name:10s} v{var:<4d} kb{kb:<3d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
                       f"{2*M*Co*9*C/ms/1e9:7.1f} TF/s", flush=True)
             nat.gemm_set_variant(0)
+    if what == "ln":  # the path's LayerNorms: fp32 residual rows -> bf16 GEMM operand
+        for name, rows, dim in (("enc", R, 1024), ("aat", L - 1, 768)):
+            x = torch.randn(rows, dim, device="cuda")
+            w, b = torch.randn(dim, device="cuda"), torch.randn(dim, device="cuda")
+            y = torch.empty(rows, dim, device="cuda", dtype=torch.bfloat16)
+            f = lambda: nat.layernorm(x, rows, dim, w, b, y_lp=y)  # noqa: E731
+            ms = timeit(f, reps)
+            print(f"ln {name:6s} rows={rows} dim={dim}: {ms*1e3:7.1f} us  {rows*dim*6/ms/1e9:6.2f} TB/s", flush=True)
     if what == "bil":  # the DPT resizes: 2x align_corners upsamples and the regressor's 296^2 -> 518^2 split resize
         cases = [("up148", 74, 74, 148, 256, torch.float32, torch.float32), ("reg518", 296, 296, 518, 128,
                                                                               torch.float32, "s3")]
