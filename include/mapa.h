@@ -99,6 +99,15 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
  * 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one the automatic choice runs),
  * 2584..2586 = LDS halo-window conv, 2590/2591 = four-wave 256x256 / 192x256 tiles. */
 int mapa_gemm_set_variant(int variant);
+/* The regressor tail in one launch (DPTRegressionProcessor conv2 + the dense head, dpt.py:285-311 and model.py:
+ * 1865-2150): d describes the 3x3 conv 128 -> 128 (bf16, stride 1, conv_kblock 32, act MAPA_ACT_RELU, bias; no
+ * outputs of its own); its ReLU'd hidden map never leaves the chip — the epilogue applies the 1x1 conv w6 [6][128] +
+ * b6, the ray / depth / confidence / mask adaptors and the output assembly of mapa_dense_head_out (pose_out: the
+ * launch's views' rows, scale: the metric scale; outputs as there).  Replaces mapa_gemm + mapa_dense_head_out. */
+int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const float* b6, const float* pose_out,
+                            const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                            float* conf, float* logits, uint8_t* mask, mapa_stream_t stream);
+
 /* Tuning / A-B hooks of the automatic kernel choice (process-wide):
  *   MAPA_TUNE_CONV_HALO (default 1): stride-1 bf16 convs in the 32-channel-slice K order (conv_kblock = 32) run on
  *     the LDS halo-window conv; 0 keeps them on the implicit GEMM (variants 2584 / 2585 / 2586 force it);

@@ -45,6 +45,17 @@ struct HCfg {
   static_assert(8 * 32 * H_ELD * 4 <= LDS, "epilogue staging");
 };
 
+// Fused regressor tail (HO = true, BN = 128): instead of the ReLU'd 128-channel hidden map, the epilogue computes the
+// 1x1 conv 128 -> 6 of every pixel and the dense-head adaptors / output assembly (dense_head_pixel).
+struct HeadOut {
+  const float* w6;    // [6][128]
+  const float* b6;    // [6]
+  const float* pose;  // [views][19] pose_out rows of this launch's views
+  const float* scale; // [1] metric scale
+  float *pts3d, *pts3d_cam, *rays, *depth, *conf, *logits;
+  uint8_t* mask;
+};
+
 __device__ __forceinline__ int swz64(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
 
 template <int N>
@@ -95,8 +106,8 @@ __device__ __forceinline__ void halo_stage(const GemmArgs& p, char* wring, char*
   }
 }
 
-template <int BN>
-__global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs p) {
+template <int BN, bool HO = false>
+__global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs p, HeadOut ho) {
   using C = HCfg<BN>;
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS];
   char* const wring = lds;
@@ -185,6 +196,70 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // LDS becomes the epilogue staging area
 
+  if constexpr (HO) {
+    // ---- fused regressor tail.  Lane (r16, g) holds relu(acc + bias) of pixels g*4 + r of block rows wm*FM + i at
+    // channels wn*64 + j*16 + r16: per block row it forms the 6 partial dot products of its 4 pixels over its 4
+    // channels, a reduce-scatter over the 16 lanes of its group (then a pairwise sum) leaves 3 of them per lane
+    // pair, and the two channel halves (waves wn = 0, 1) meet in LDS.
+    static_assert(BN == 128 && C::FM == 4 && C::FN == 4, "head-out tail: 128-wide tiles");
+    float* part = reinterpret_cast<float*>(lds);  // [256 pixels][2 halves][6]
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // one block row (16 pixels of which this lane group holds 4) at a time
+      float v[24];
+#pragma unroll
+      for (int k = 0; k < 24; ++k) v[k] = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = wn * 64 + j * 16 + r16;
+        const float bj = p.bias[ch];
+        float wv[6];
+#pragma unroll
+        for (int o = 0; o < 6; ++o) wv[o] = ho.w6[o * 128 + ch];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = fmaxf(acc[i][j][r] + bj, 0.f);
+#pragma unroll
+          for (int o = 0; o < 6; ++o) v[r * 6 + o] += x * wv[o];
+        }
+      }
+#define HO_STAGE(M, HALF)                                                \
+  {                                                                      \
+    const bool up = (r16 & (M)) != 0;                                    \
+    _Pragma("unroll") for (int t = 0; t < (HALF); ++t) {                 \
+      const float mine = up ? v[(HALF) + t] : v[t];                      \
+      const float other = up ? v[t] : v[(HALF) + t];                     \
+      v[t] = mine + __shfl_xor(other, (M), 64);                          \
+    }                                                                    \
+  }
+      HO_STAGE(8, 12) HO_STAGE(4, 6) HO_STAGE(2, 3)
+#undef HO_STAGE
+      // lanes r16 and r16 ^ 1 hold partial sums of the same 3 values: segment s = r16 >> 1 (row s >> 1, outputs
+      // (s & 1)*3 ..) of this block row
+#pragma unroll
+      for (int t = 0; t < 3; ++t) v[t] += __shfl_xor(v[t], 1, 64);
+      if ((r16 & 1) == 0) {
+        const int sgm = r16 >> 1;
+        const int pix = wm * 64 + i * 16 + g * 4 + (sgm >> 1);
+        float* dst = part + (pix * 2 + wn) * 6 + (sgm & 1) * 3;
+        dst[0] = v[0];
+        dst[1] = v[1];
+        dst[2] = v[2];
+      }
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int py = tid >> 4, px = tid & 15;
+      const int oy = by * HB + py, ox = bx * HB + px;
+      if (oy < p.cv_OH && ox < p.cv_OW) {
+        float raw[6];
+#pragma unroll
+        for (int o = 0; o < 6; ++o) raw[o] = ho.b6[o] + part[(tid * 2) * 6 + o] + part[(tid * 2 + 1) * 6 + o];
+        const int64_t q = ((int64_t)img * p.cv_OH + oy) * p.cv_OW + ox;
+        dense_head_pixel(raw, ho.pose + img * 19, ho.scale[0], q, ho.pts3d, ho.pts3d_cam, ho.rays, ho.depth, ho.conf,
+                         ho.logits, ho.mask);
+      }
+    }
+  } else {
   // ---- epilogue: 32 rows (two block rows) x 64 fp32 per wave per pass through LDS, 16-B stores
   float* ep = reinterpret_cast<float*>(lds) + wave * 32 * H_ELD;
   const int c4 = (lane & 15) * 4;
@@ -213,6 +288,7 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  }
 }
 
 }  // namespace
@@ -226,8 +302,25 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream) {
   const int hw = a.cv_OH * a.cv_OW;
   const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + HB - 1) / HB) * ((a.cv_OW + HB - 1) / HB) * (a.N / bn);
   if (tiles >= (int64_t(1) << 31)) return false;
-  if (bn == 256) hipLaunchKernelGGL(conv_halo_kernel<256>, dim3((unsigned)tiles), dim3(HT), 0, stream, a);
-  else hipLaunchKernelGGL(conv_halo_kernel<128>, dim3((unsigned)tiles), dim3(HT), 0, stream, a);
+  const HeadOut none{};
+  if (bn == 256) hipLaunchKernelGGL((conv_halo_kernel<256>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+  else hipLaunchKernelGGL((conv_halo_kernel<128>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+  return true;
+}
+
+bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b6, const float* pose,
+                              const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                              float* conf, float* logits, uint8_t* mask, hipStream_t stream) {
+  if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
+  if (a.N != 128 || !a.bias || a.act != MAPA_ACT_RELU || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
+  const int hw = a.cv_OH * a.cv_OW;
+  const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + HB - 1) / HB) * ((a.cv_OW + HB - 1) / HB);
+  if (tiles >= (int64_t(1) << 31)) return false;
+  HeadOut h;
+  h.w6 = w6; h.b6 = b6; h.pose = pose; h.scale = scale;
+  h.pts3d = pts3d; h.pts3d_cam = pts3d_cam; h.rays = rays; h.depth = depth; h.conf = conf; h.logits = logits;
+  h.mask = mask;
+  hipLaunchKernelGGL((conv_halo_kernel<128, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h);
   return true;
 }
 

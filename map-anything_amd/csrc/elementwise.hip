@@ -270,25 +270,8 @@ __global__ void __launch_bounds__(256) dense_head_out_kernel(
                   hv[3] * sw[c * 128 + k + 3];
     }
     const int v = (int)(p / HW);
-    const float* po = pose_out + v * 19;
     const float sc = scale[v % batch];  // rows are view-major: v = view * batch + b
-    float rx = acc[0], ry = acc[1], rz = acc[2];
-    const float nr = fmaxf(sqrtf(rx * rx + ry * ry + rz * rz), 1e-8f);
-    rx /= nr; ry /= nr; rz /= nr;
-    const float d = expf(acc[3]);
-    const float cx = rx * d, cy = ry * d, cz = rz * d;
-    const float* R = po + 7;
-    const float* t = po + 16;
-    const float wx = R[0] * cx + R[1] * cy + R[2] * cz + t[0];
-    const float wy = R[3] * cx + R[4] * cy + R[5] * cz + t[1];
-    const float wz = R[6] * cx + R[7] * cy + R[8] * cz + t[2];
-    pts3d[p * 3 + 0] = wx * sc; pts3d[p * 3 + 1] = wy * sc; pts3d[p * 3 + 2] = wz * sc;
-    pts3d_cam[p * 3 + 0] = cx * sc; pts3d_cam[p * 3 + 1] = cy * sc; pts3d_cam[p * 3 + 2] = cz * sc;
-    rays[p * 3 + 0] = rx; rays[p * 3 + 1] = ry; rays[p * 3 + 2] = rz;
-    depth[p] = d * sc;
-    conf[p] = 1.f + expf(acc[4]);
-    logits[p] = acc[5];
-    mask[p] = (1.f / (1.f + expf(-acc[5]))) > 0.5f ? 1 : 0;
+    dense_head_pixel(acc, pose_out + v * 19, sc, p, pts3d, pts3d_cam, rays, depth, conf, logits, mask);
   }
 }
 

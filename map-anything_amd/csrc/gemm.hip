@@ -343,14 +343,13 @@ int pick_streamk(int dtype, bool conv, int M, int N, int K) {
 }  // namespace mapa_gemm_impl
 using namespace mapa_gemm_impl;
 
-extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
+static int gemm_args(const mapa_gemm_desc* d, GemmArgs& a) {
   MAPA_CHECK_ARG(d != nullptr, "mapa_gemm: null descriptor");
   MAPA_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "mapa_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
   MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32, "mapa_gemm: dtype must be bf16 or f32");
   const int E = d->dtype == MAPA_BF16 ? 8 : 4;
   MAPA_CHECK_ARG(d->K % E == 0, "mapa_gemm: K=%d must be a multiple of %d", d->K, E);
   MAPA_CHECK_ARG(d->A && d->W, "mapa_gemm: null operand");
-  MAPA_CHECK_ARG(d->out_f32 || d->out_lp || d->out_lp_relu || d->out_s3 || d->out_s3_relu, "mapa_gemm: no output");
   MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || (!d->out_s3 && !d->out_s3_relu), "mapa_gemm: split outputs need dtype bf16");
   MAPA_CHECK_ARG(d->act >= MAPA_ACT_NONE && d->act <= MAPA_ACT_GELU_POST, "mapa_gemm: bad act %d", d->act);
   MAPA_CHECK_ARG(d->act != MAPA_ACT_GELU_POST || !d->gamma, "mapa_gemm: GELU_POST takes no gamma");
@@ -385,7 +384,6 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   } else {
     MAPA_CHECK_ARG(d->ldo >= d->N, "mapa_gemm: ldo < N");
   }
-  GemmArgs a;
   a.A = d->A; a.lda = d->lda; a.W = d->W; a.ldw = d->ldw;
   a.M = d->M; a.N = d->N; a.K = d->K;
   a.cv_C = d->conv_C; a.cv_IH = d->conv_IH; a.cv_IW = d->conv_IW; a.cv_OH = d->conv_OH; a.cv_OW = d->conv_OW;
@@ -405,6 +403,13 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   a.out_mode = d->out_mode; a.ps_s = d->ps_s; a.ps_h = d->ps_h; a.ps_w = d->ps_w; a.ps_cout = d->ps_cout;
   a.vec_ok = (d->N % 4 == 0) && (d->out_mode == MAPA_OUT_PIXSHUF || d->ldo % 4 == 0);
   MAPA_CHECK_ARG(a.vec_ok || d->out_mode == MAPA_OUT_ROWMAJOR, "mapa_gemm: pixel shuffle needs N %% 4 == 0");
+  return 0;
+}
+
+extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
+  GemmArgs a;
+  if (int rc = gemm_args(d, a)) return rc;
+  MAPA_CHECK_ARG(d->out_f32 || d->out_lp || d->out_lp_relu || d->out_s3 || d->out_s3_relu, "mapa_gemm: no output");
   const int nblk = ((d->M + BM - 1) / BM) * ((d->N + BN - 1) / BN);
   const bool conv = d->a_mode == MAPA_A_CONV3X3;
   // Tile-pipeline variant (RB*10 + STAGES).  Measured on MI355X (tools/kbench.py): 64-B rows x 3 stages (occupancy
@@ -438,6 +443,24 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
     else launch_variant<TraitsF32, 0>(variant, nblk, stream, a);
   }
   MAPA_CHECK_LAUNCH("mapa_gemm");
+  return 0;
+}
+
+extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const float* b6,
+                                       const float* pose_out, const float* scale, float* pts3d, float* pts3d_cam,
+                                       float* rays, float* depth, float* conf, float* logits, uint8_t* mask,
+                                       hipStream_t stream) {
+  GemmArgs a;
+  if (int rc = gemm_args(d, a)) return rc;
+  MAPA_CHECK_ARG(w6 && b6 && pose_out && scale && pts3d && pts3d_cam && rays && depth && conf && logits && mask,
+                 "mapa_regressor_head_out: null output or parameter");
+  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 && d->a_mode == MAPA_A_CONV3X3 && !d->out_f32 && !d->out_lp &&
+                     !d->out_lp_relu && !d->out_s3 && !d->out_s3_relu && !d->resid1 && !d->resid2 && !d->gamma,
+                 "mapa_regressor_head_out: needs a bf16 3x3 conv descriptor without other outputs");
+  MAPA_CHECK_ARG(launch_conv_halo_headout(a, w6, b6, pose_out, scale, pts3d, pts3d_cam, rays, depth, conf, logits,
+                                          mask, stream),
+                 "mapa_regressor_head_out: conv must be stride 1, conv_kblock 32, N 128, ReLU with bias");
+  MAPA_CHECK_LAUNCH("mapa_regressor_head_out");
   return 0;
 }
 

@@ -207,6 +207,12 @@ bool launch_gemm_8p(const GemmArgs& a, bool conv, int diag, hipStream_t stream);
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).
 bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream);
 
+// The halo conv with the regressor tail fused into its epilogue (conv_halo.hip): conv3x3 128->128 + ReLU, 1x1 128->6,
+// adaptors and output assembly.  false unless the conv qualifies (bf16, stride 1, conv_kblock 32, N 128, ReLU, bias).
+bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b6, const float* pose,
+                              const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                              float* conf, float* logits, uint8_t* mask, hipStream_t stream);
+
 // Four-wave bf16 kernel with inline-asm MFMAs on AGPR accumulators and an explicitly ordered main loop
 // (gemm_w4a.hip): variant 0 = 256x256, 1 = 192x256; dense A with K % 32 == 0.  false if it does not take the shape.
 bool launch_gemm_w4a(const GemmArgs& a, bool conv, int variant, hipStream_t stream);

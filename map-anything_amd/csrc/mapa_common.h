@@ -77,6 +77,31 @@ __device__ __forceinline__ T ceil_div(T a, T b) {
   return (a + b - 1) / b;
 }
 
+// Dense-head tail for one pixel (model.py:1865-2150 via the adaptors): raw = conv1x1 128->6 output; po = the view's
+// pose_out row (19 floats: cam_trans, cam_quats, R (row-major 3x3) at 7, t at 16); sc = metric scale.  Unit ray, exp
+// depth, pts3d_cam = ray * depth, pts3d = R pts3d_cam + t, both scaled; conf = 1 + exp; mask = sigmoid(logit) > 0.5.
+__device__ __forceinline__ void dense_head_pixel(const float* raw, const float* po, float sc, int64_t p,
+                                                 float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                                                 float* conf, float* logits, uint8_t* mask) {
+  float rx = raw[0], ry = raw[1], rz = raw[2];
+  const float nr = fmaxf(sqrtf(rx * rx + ry * ry + rz * rz), 1e-8f);
+  rx /= nr; ry /= nr; rz /= nr;
+  const float d = expf(raw[3]);
+  const float cx = rx * d, cy = ry * d, cz = rz * d;
+  const float* R = po + 7;
+  const float* t = po + 16;
+  const float wx = R[0] * cx + R[1] * cy + R[2] * cz + t[0];
+  const float wy = R[3] * cx + R[4] * cy + R[5] * cz + t[1];
+  const float wz = R[6] * cx + R[7] * cy + R[8] * cz + t[2];
+  pts3d[p * 3 + 0] = wx * sc; pts3d[p * 3 + 1] = wy * sc; pts3d[p * 3 + 2] = wz * sc;
+  pts3d_cam[p * 3 + 0] = cx * sc; pts3d_cam[p * 3 + 1] = cy * sc; pts3d_cam[p * 3 + 2] = cz * sc;
+  rays[p * 3 + 0] = rx; rays[p * 3 + 1] = ry; rays[p * 3 + 2] = rz;
+  depth[p] = d * sc;
+  conf[p] = 1.f + expf(raw[4]);
+  logits[p] = raw[5];
+  mask[p] = (1.f / (1.f + expf(-raw[5]))) > 0.5f ? 1 : 0;
+}
+
 // Wave-level reductions (64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

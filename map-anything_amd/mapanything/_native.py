@@ -30,6 +30,7 @@ EXPORTED = (
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
     "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_tune",
+    "mapa_regressor_head_out",
 )
 
 
@@ -101,6 +102,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_linear_small.argtypes = [vp, i, i, vp, vp, i, i, vp, vp]
     L.mapa_pose_scale_finalize.argtypes = [vp, vp, i, i, vp, vp, vp, vp]
     L.mapa_dense_head_out.argtypes = [vp, i, i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.mapa_regressor_head_out.argtypes = [vp] + [vp] * 11 + [vp]
     L.mapa_convert_rows.argtypes = [vp, i64, i, i, vp, i, i64, vp]
     L.mapa_fill_splitmix.argtypes = [vp, i64, u64, f, f, vp]
     L.mapa_postprocess_mask.argtypes = [vp, vp, vp, vp, i, i, i, f, f, i, vp, vp]
@@ -264,12 +266,14 @@ def gemm_set_variant(variant: int = 0):
 
 def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_NONE, resid1=None, resid2=None,
          out_f32=None, out_lp=None, out_lp_relu=None, out_s3=None, out_s3_relu=None, ldo=None, conv=None,
-         pixshuf=None):
+         pixshuf=None, head_out=None):
     """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout).
     out_s3 / out_s3_relu: split-precision operand outputs (bf16 [rows][2*ldo], [hi | lo]).  A weight packed for split
     operands (W._mapa_split, engine._split_pack) marks A as a compact split operand (mapa_gemm_desc.a_split): K is
     then the logical 3C, the stored A row 2C wide.  A conv weight tagged W._mapa_kblock = B holds its columns in the
-    channel-block-major K order (mapa_gemm_desc.conv_kblock)."""
+    channel-block-major K order (mapa_gemm_desc.conv_kblock).
+    head_out=(w6, b6, pose_out, scale, pts3d, pts3d_cam, rays, depth, conf, logits, mask): the conv is the regressor's
+    conv2 and its hidden map goes straight into the dense head (mapa_regressor_head_out; no other outputs)."""
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype
@@ -311,7 +315,11 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
         ws = gemm_workspace(need)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     tok = _tic()
-    check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
+    if head_out is not None:
+        check(lib().mapa_regressor_head_out(ctypes.byref(d), *(ptr(t) for t in head_out), stream()),
+              "mapa_regressor_head_out")
+    else:
+        check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
     # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops
     kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if split_a else "")
     if _LAUNCH_LOG is not None:

@@ -692,13 +692,21 @@ class MapaEngine:
         nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y)
 
     # ----------------------------------------------------------------------------------------------- DPT
-    def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None):
+    def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None, head=None):
         """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Inputs are head operands (_hop rows); fused_lp
         is the first DPT input — the fused encoder features (ENC_DIM) or, with three info-sharing taps
         (model.py:1748-1768), the first tap; its width comes from the packed weight.  Returns the ReLU'd 128-ch
-        hidden map at HxW (fp32 in split mode, else lp)."""
+        hidden map at HxW (fp32 in split mode, else lp), or None when `head` (see dpt_regress) took the dense head
+        into the last conv."""
         owned = [self.dpt_feature(fused_lp, l11, l17, fin_lp, VB, hp, wp, taps)[0]]
-        return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W)  # freed after its first conv
+        return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W, head)  # freed after its first conv
+
+    def fused_head_out(self):
+        """Whether the regressor's conv2 can carry the dense head in its epilogue (mapa_regressor_head_out: bf16
+        operands, channel-block-major conv weight).  MAPA_FUSED_HEAD=0 keeps the two launches (A/B)."""
+        c2 = self.w.reg_c2
+        return (c2.dtype == torch.bfloat16 and getattr(c2, "_mapa_kblock", 0) == 32
+                and os.environ.get("MAPA_FUSED_HEAD", "1") != "0")
 
     def _hconv3(self, x, n, IH, IW, C, wmat, Cout, stride=1, **epi):
         """3x3 conv of a head operand with C logical channels."""
@@ -766,11 +774,13 @@ class MapaEngine:
         feat_lp = self._upsample_outconv(o, n, h0, w0, 1, lowp=True, taps=t)
         return feat_lp, (t["dpt_feature"] if t is not None else None)
 
-    def dpt_regress(self, feat_lp, n, hf, wf, H, W):
+    def dpt_regress(self, feat_lp, n, hf, wf, H, W, head=None):
         """DPTRegressionProcessor up to the last ReLU (dpt.py:285-311): conv3x3 256->128 at 8x, bilinear
         (align_corners) to HxW, conv3x3 128->128 + ReLU -> hidden [n*H*W][128] (fp32 in split mode, else lp).
         feat_lp (a head operand) may be a one-element list, handed over so that the 8x map is freed as soon as it
-        has been read."""
+        has been read.  head = (pose_out rows, scale, pts3d, pts3d_cam, rays, depth, conf, logits, mask) of these
+        views: the conv's epilogue runs the 1x1 conv 128->6 and the dense head instead (nat.gemm head_out, the
+        hidden map never reaches HBM); returns None then."""
         w = self.w
         if isinstance(feat_lp, list):
             feat_lp = feat_lp.pop()
@@ -781,6 +791,10 @@ class MapaEngine:
         r1u = self._hop(n * H * W, 128)
         nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u, split_out=self.hsplit)
         del r1
+        if head is not None:
+            self._hconv3(r1u, n, H, W, 128, w.reg_c2, 128, bias=w.reg_b2, act=nat.ACT_RELU,
+                         head_out=(w.reg_w6, w.reg_b6) + tuple(head))
+            return None
         hid = self._hmap(n * H * W, 128)
         self._hconv3(r1u, n, H, W, 128, w.reg_c2, 128, bias=w.reg_b2, act=nat.ACT_RELU,
                      **({"out_f32": hid} if self.hsplit else {"out_lp": hid}))
@@ -916,16 +930,17 @@ class MapaEngine:
                 conf=self._empty(VB, H, W, dtype=f), non_ambiguous_mask_logits=self._empty(VB, H, W, dtype=f),
                 non_ambiguous_mask=self._empty(VB, H, W, dtype=torch.bool))  # kernel writes 0/1 bytes
             chunk = VB if not dpt_chunk else max(1, min(int(dpt_chunk), VB))
+            fuse = self.fused_head_out()
             for v0 in range(0, VB, chunk):
                 n = min(chunk, VB - v0)
                 r0, r1 = v0 * T, (v0 + n) * T
+                head = (pose_out[v0:v0 + n], scale) + tuple(
+                    out[k][v0:v0 + n] for k in ("pts3d", "pts3d_cam", "ray_directions", "depth_along_ray", "conf",
+                                                "non_ambiguous_mask_logits", "non_ambiguous_mask"))
                 hid = self.dpt(first[r0:r1], l11[r0:r1], l17[r0:r1], fin_lp[r0:r1], n, hp, wp, H, W,
-                               taps if n == VB else None)
-                nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, pose_out[v0:v0 + n], scale, 1,
-                                   out["pts3d"][v0:v0 + n], out["pts3d_cam"][v0:v0 + n],
-                                   out["ray_directions"][v0:v0 + n], out["depth_along_ray"][v0:v0 + n],
-                                   out["conf"][v0:v0 + n], out["non_ambiguous_mask_logits"][v0:v0 + n],
-                                   out["non_ambiguous_mask"][v0:v0 + n])
+                               taps if n == VB else None, head=head if fuse else None)
+                if not fuse:
+                    nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, *head[:2], 1, *head[2:])
                 del hid
             out["cam_trans"] = pose_out[:, 0:3]
             out["cam_quats"] = pose_out[:, 3:7]

@@ -195,6 +195,59 @@ def test_split_precision_conv_halo_window(nat):
     assert rel_l2(out.cpu(), ref) < 2e-5
 
 
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("n,H,W", [(2, 37, 29), (1, 48, 64), (3, 16, 16)])
+def test_regressor_head_out_fused(nat, split, n, H, W):
+    """mapa_regressor_head_out (regressor conv2 + ReLU + 1x1 128->6 + dense head in one launch) against the two-launch
+    path with an fp32 hidden map (conv out_f32 + mapa_dense_head_out): same fp32 math, other summation order; the
+    mask may differ only where the logit is ~0."""
+    C = 128
+    x = _rand(n, C, H, W, seed=60)
+    wt = _rand(C, C, 3, 3, scale=(9 * C) ** -0.5, seed=61)
+    b2, w6, b6 = _rand(C, seed=62), _rand(6, C, scale=C ** -0.5, seed=63), _rand(6, seed=64)
+    M = n * H * W
+    xr = x.permute(0, 2, 3, 1).reshape(M, C).contiguous()
+    wk = wt.permute(0, 2, 3, 1).reshape(C, 9, C)
+    if split:
+        a = torch.empty(M, 2 * C, dtype=torch.bfloat16, device="cuda")
+        nat.split_bf16x3(xr, M, C, C, a)
+        whi = wk.to(torch.bfloat16)
+        wlo = (wk - whi.float()).to(torch.bfloat16)
+        wp = torch.stack([whi, wlo, whi], 2).reshape(C, 9, 3 * C)
+        Cl = 3 * C
+    else:
+        a, wp, Cl = xr.to(torch.bfloat16), wk.to(torch.bfloat16), C
+    wp = wp.reshape(C, 9, Cl // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(C, -1)
+    wp._mapa_split = split
+    wp._mapa_kblock = 32
+    pose_out = torch.empty(n, 19, device="cuda")
+    scale = torch.empty(1, device="cuda")
+    nat.pose_scale_finalize(_rand(n, 7, seed=65), _rand(1, seed=66), n, 1, pose_out, scale,
+                            torch.empty(n, 4, 4, device="cuda"))
+
+    def outs():
+        f = dict(device="cuda")
+        return [torch.full((n, H, W, 3), float("nan"), **f) for _ in range(3)] + \
+            [torch.full((n, H, W, 1), float("nan"), **f)] + [torch.full((n, H, W), float("nan"), **f) for _ in range(2)] + \
+            [torch.full((n, H, W), 7, dtype=torch.uint8, device="cuda")]
+
+    conv = (Cl, H, W, H, W, 1)
+    hid = torch.empty(M, C, device="cuda")
+    nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, out_f32=hid, conv=conv)
+    ref = outs()
+    nat.dense_head_out(hid, n, H * W, w6, b6, pose_out, scale, 1, *ref)
+    got = outs()
+    nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scale, *got))
+    torch.cuda.synchronize()
+    for r, g in zip(ref[:6], got[:6]):
+        assert torch.isfinite(g).all()
+        assert rel_l2(g.cpu(), r.cpu()) < 1e-5
+    logits = ref[5].cpu()
+    decided = logits.abs() > 1e-4
+    assert torch.equal(got[6].cpu()[decided], ref[6].cpu()[decided])
+    assert int(got[6].cpu().gt(1).sum()) == 0
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("n,H,W,C,Co,stride", [(2, 19, 19, 96, 256, 1), (1, 37, 37, 768, 768, 2),
                                               (3, 16, 20, 128, 128, 1), (1, 8, 8, 256, 6, 1)])

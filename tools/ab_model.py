@@ -2,7 +2,8 @@
 switches.  Usage: python tools/ab_model.py kblock [views] [rounds] [steps]
   kblock: head convs with the channel-block-major K order (engine.KBLOCK = 32) vs tap-major (0);
   halo: stride-1 head convs on the LDS halo-window kernel vs the implicit GEMM;
-  tailsk: tail-only stream-K for the GEMMs with a nearly empty last wave vs data-parallel."""
+  tailsk: tail-only stream-K for the GEMMs with a nearly empty last wave vs data-parallel;
+  fusedhead: the regressor's conv2 carrying the dense head (mapa_regressor_head_out) vs conv + dense_head_out."""
 import os
 import sys
 import time
@@ -36,6 +37,9 @@ def main():
     elif what == "tailsk":
         arms = [("tailsk", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 1)),
                 ("dataparallel", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 0))]
+    elif what == "fusedhead":
+        arms = [("fused", lambda: os.environ.__setitem__("MAPA_FUSED_HEAD", "1")),
+                ("twolaunch", lambda: os.environ.__setitem__("MAPA_FUSED_HEAD", "0"))]
     else:
         raise SystemExit(f"unknown A/B {what}")
     models, sd = [], None
