@@ -804,9 +804,8 @@ class MapaEngine:
         u = self.w.refine[r]["resConfUnit2"]
         c1 = self._hop(n * h * w_, 256)
         self._hconv3(x_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, **self._hout(c1))
-        o = self._hmap(n * h * w_, 256)
-        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=x_f,
-                     **({"out_f32": o} if self.hsplit else {"out_lp": o}))
+        o = self._hop(n * h * w_, 256)  # out_conv's operand (_upsample_outconv)
+        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=x_f, **self._hout(o))
         return o
 
     def _fusion_two(self, n, h, w_, r, path_f, skip_f, skip_r):
@@ -820,28 +819,32 @@ class MapaEngine:
                      **self._hout(relu=s_r))
         u = d["resConfUnit2"]
         self._hconv3(s_r, n, h, w_, 256, u["c1"], 256, bias=u["b1"], act=nat.ACT_RELU, **self._hout(c1))
-        o = self._hmap(n * h * w_, 256)
-        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=s_f,
-                     **({"out_f32": o} if self.hsplit else {"out_lp": o}))
+        o = self._hop(n * h * w_, 256)
+        self._hconv3(c1, n, h, w_, 256, u["c2"], 256, bias=u["b2"], resid1=s_f, **self._hout(o))
         return o
 
     def _upsample_outconv(self, o, n, h, w_, r, crop=None, lowp=False, taps=None):
-        """bilinear x2 (align_corners) [+ crop] then the 1x1 out_conv (dpt_block.py:241-254, dpt.py:213)."""
+        """The fusion block's tail (dpt_block.py:242-254, dpt.py:213): bilinear x2 (align_corners) [+ crop], then the
+        1x1 out_conv.  Run here in the other order — out_conv on the h x w map, then the resize of its fp32 output:
+        a 1x1 conv mixes channels per pixel and the resize mixes pixels per channel with weights that sum to one, so
+        the two commute (bias included; the crop too) up to fp32 rounding, and the GEMM does a quarter of the
+        reference's work.  o: the operand rows [n*h*w] (head operand); returns the fp32 map at 2h x 2w (cropped),
+        or with lowp a head operand (+ the fp32 tap)."""
         d = self.w.refine[r]
         Hf, Wf = 2 * h, 2 * w_
         oh, ow = crop if crop is not None else (Hf, Wf)
-        up = self._hop(n * oh * ow, 256)
-        nat.bilinear_ac(o, n, h, w_, 256, Hf, Wf, oh, ow, up, split_out=self.hsplit)
-        K = self._hw(256)
+        y = self._empty(n * h * w_, 256, dtype=torch.float32)
+        nat.gemm(o, d["out"], n * h * w_, 256, self._hw(256), bias=d["out_b"], out_f32=y)
         if lowp:
             out = self._hop(n * oh * ow, 256)
-            f = self._empty(n * oh * ow, 256, dtype=torch.float32) if taps is not None else None
-            nat.gemm(up, d["out"], n * oh * ow, 256, K, bias=d["out_b"], out_f32=f, **self._hout(out))
+            nat.bilinear_ac(y, n, h, w_, 256, Hf, Wf, oh, ow, out, split_out=self.hsplit)
             if taps is not None:
+                f = self._empty(n * oh * ow, 256, dtype=torch.float32)
+                nat.bilinear_ac(y, n, h, w_, 256, Hf, Wf, oh, ow, f)
                 taps["dpt_feature"] = f.view(n, oh, ow, 256)
             return out
         out = self._empty(n * oh * ow, 256, dtype=torch.float32)
-        nat.gemm(up, d["out"], n * oh * ow, 256, K, bias=d["out_b"], out_f32=out)
+        nat.bilinear_ac(y, n, h, w_, 256, Hf, Wf, oh, ow, out)
         return out
 
     # ------------------------------------------------------------------------------------- pose / scale
