@@ -112,30 +112,34 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 // F.interpolate(mode="bilinear", align_corners=True) as ATen computes it (scale = (in-1)/(out-1) in fp32,
 // h1 = h0 + (h0 < in-1), lambdas 1-l / l), NHWC, 4 channels per thread.
 // One thread = 8 channels of one output pixel (16-B bf16 accesses); consecutive threads walk the channels of a
-// pixel, so a wave reads each of the 4 source taps and writes the output as contiguous row segments.  32-bit
-// indexing (the caller checks the element count).
+// pixel, so a wave reads each of the 4 source taps and writes the output as contiguous row segments.  Grid: x over
+// one output row's (pixel, channel-group) pairs, y over output rows (strided past 65535 rows), so the row's source
+// rows and weights are block-uniform and a thread splits its index with one shift (c8 a power of two) — the
+// grid-stride form spent more on 64-bit index division than on its memory traffic.
 template <typename TI, typename TO, bool S3 = false>  // S3: split operand rows [hi | lo] (2C wide)
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
-                                   int OW, TO* __restrict__ out) {
+                                   int OW, int c8_shift, TO* __restrict__ out) {
   const int c8 = C / 8;
-  const int64_t total = (int64_t)n * OH * OW * c8;  // > 2^31 past ~500 views at 518x518 x 128 channels
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= OW * c8) return;
+  const int ox = c8_shift >= 0 ? idx >> c8_shift : idx / c8;
+  const int c = (idx - ox * c8) * 8;
   const float sh = OHf > 1 ? (float)(IH - 1) / (float)(OHf - 1) : 0.f;
   const float sw = OWf > 1 ? (float)(IW - 1) / (float)(OWf - 1) : 0.f;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int c = (int)(e % c8) * 8;
-    int r = (int)(e / c8);
-    const int ox = r % OW;
-    r /= OW;
-    const int oy = r % OH;
-    const int im = r / OH;
-    const float fy = sh * oy, fx = sw * ox;
-    const int y0 = (int)fy, x0 = (int)fx;
-    const int y1 = y0 + (y0 < IH - 1 ? 1 : 0), x1 = x0 + (x0 < IW - 1 ? 1 : 0);
-    const float ly1 = fy - y0, ly0 = 1.f - ly1, lx1 = fx - x0, lx0 = 1.f - lx1;
+  const float fx = sw * ox;
+  const int x0 = (int)fx;
+  const int x1 = x0 + (x0 < IW - 1 ? 1 : 0);
+  const float lx1 = fx - x0, lx0 = 1.f - lx1;
+  for (int r = blockIdx.y; r < n * OH; r += gridDim.y) {
+    const int im = r / OH, oy = r - im * OH;
+    const float fy = sh * oy;
+    const int y0 = (int)fy;
+    const int y1 = y0 + (y0 < IH - 1 ? 1 : 0);
+    const float ly1 = fy - y0, ly0 = 1.f - ly1;
     const TI* base = in + (size_t)im * IH * IW * C + c;
     const size_t o00 = ((size_t)y0 * IW + x0) * C, o01 = ((size_t)y0 * IW + x1) * C;
     const size_t o10 = ((size_t)y1 * IW + x0) * C, o11 = ((size_t)y1 * IW + x1) * C;
-    TO* op = out + (((size_t)im * OH + oy) * OW + ox) * (S3 ? 2 * C : C) + c;
+    TO* op = out + ((size_t)r * OW + ox) * (S3 ? 2 * C : C) + c;
     f32x4 a0, a1, b0, b1, c0, c1, d0, d1;
     load8(base + o00, a0, a1);
     load8(base + o01, b0, b1);
@@ -391,30 +395,31 @@ extern "C" int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, c
 extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                 int OW, void* out, int out_dtype, hipStream_t stream) {
   MAPA_CHECK_ARG(in && out && C % 8 == 0 && OH <= OHf && OW <= OWf, "mapa_bilinear_ac: bad args (C %% 8 == 0)");
-  const int64_t total = (int64_t)n * OH * OW * (C / 8);
-  MAPA_CHECK_ARG(total < (1LL << 31), "mapa_bilinear_ac: too many outputs for one launch");
-  const dim3 g(grid_for(total)), b(TPB);
+  const int c8 = C / 8, c8_shift = (c8 & (c8 - 1)) == 0 ? __builtin_ctz(c8) : -1;
+  const int rows = n * OH;
+  MAPA_CHECK_ARG((int64_t)OW * c8 < (1LL << 31) && (int64_t)n * OH < (1LL << 31), "mapa_bilinear_ac: too large");
+  const dim3 g((unsigned)((OW * c8 + TPB - 1) / TPB), (unsigned)std::min(rows, 65535)), b(TPB);
   MAPA_CHECK_ARG((in_dtype == MAPA_F32 || in_dtype == MAPA_BF16) &&
                      (out_dtype == MAPA_F32 || out_dtype == MAPA_BF16 || out_dtype == MAPA_BF16X3),
                  "mapa_bilinear_ac: bad dtypes");
   if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32)
     hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, true>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, (bf16_t*)out);
+                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
   else if (out_dtype == MAPA_BF16X3)
     hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, true>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, (bf16_t*)out);
+                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
   else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
     hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
-                       OWf, OH, OW, (bf16_t*)out);
+                       OWf, OH, OW, c8_shift, (bf16_t*)out);
   else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16)
     hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t>), g, b, 0, stream, (const float*)in, n, IH, IW, C, OHf, OWf,
-                       OH, OW, (bf16_t*)out);
+                       OH, OW, c8_shift, (bf16_t*)out);
   else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_F32)
     hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, float>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
-                       OWf, OH, OW, (float*)out);
+                       OWf, OH, OW, c8_shift, (float*)out);
   else
     hipLaunchKernelGGL((bilinear_ac_kernel<float, float>), g, b, 0, stream, (const float*)in, n, IH, IW, C, OHf, OWf,
-                       OH, OW, (float*)out);
+                       OH, OW, c8_shift, (float*)out);
   MAPA_CHECK_LAUNCH("mapa_bilinear_ac");
   return 0;
 }

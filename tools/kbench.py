@@ -127,8 +127,9 @@ def main():
             ms = timeit(f, reps)
             print(f"ln {name:6s} rows={rows} dim={dim}: {ms*1e3:7.1f} us  {rows*dim*6/ms/1e9:6.2f} TB/s", flush=True)
     if what == "bil":  # the DPT resizes: 2x align_corners upsamples and the regressor's 296^2 -> 518^2 split resize
-        cases = [("up148", 74, 74, 148, 256, torch.float32, torch.float32), ("reg518", 296, 296, 518, 128,
-                                                                              torch.float32, "s3")]
+        cases = [("up148", 74, 74, 148, 256, torch.float32, torch.float32),
+                 ("up296s3", 148, 148, 296, 256, torch.float32, "s3"),
+                 ("reg518", 296, 296, 518, 128, torch.float32, "s3")]
         for name, IH, IW, O, C, ti, to in cases:
             x = torch.randn(V, IH, IW, C, device="cuda", dtype=ti)
             o = torch.empty(V, O, O, 2 * C if to == "s3" else C, device="cuda",
