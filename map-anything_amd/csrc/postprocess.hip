@@ -39,13 +39,15 @@ __device__ __forceinline__ float norm3(const float a[3]) {
   return sqrtf(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
 }
 
-// K1: points_to_normals(point, mask) -> normal (H,W,3) and normal_mask (H,W)
+// K1: points_to_normals(point, mask) -> normal (H,W,3) and normal_mask (H,W).  Stored already renormalised
+// (n / (|n| + 1e-12), normals_edge's first step, geometry.py:2216): K2 reads every normal 9 times, and the same
+// float operations applied once per pixel give the same bits.  32-bit pixel indices (the host checks n*H*W).
 __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __restrict__ mask, int n, int H, int W,
                                float* __restrict__ nrm, uint8_t* __restrict__ nmask) {
-  const int64_t total = (int64_t)n * H * W;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int im = (int)(e / ((int64_t)H * W));
-    const int rem = (int)(e - (int64_t)im * H * W);
+  const int total = n * H * W, HW = H * W;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int im = e / HW;
+    const int rem = e - im * HW;
     const int y = rem / W, x = rem - y * W;
     const float* P = pts + (int64_t)im * H * W * 3;
     const uint8_t* M = mask + (int64_t)im * H * W;
@@ -78,8 +80,11 @@ __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __r
       }
     }
     const float ns = norm3(s) + 1e-12f;
-    float* o = nrm + e * 3;
+    float o[3];
     for (int k = 0; k < 3; ++k) o[k] = any ? s[k] / ns : 0.f;
+    const float no = norm3(o) + 1e-12f;
+    float* un = nrm + (int64_t)e * 3;
+    for (int k = 0; k < 3; ++k) un[k] = o[k] / no;
     nmask[e] = any ? 1 : 0;
   }
 }
@@ -94,18 +99,17 @@ __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __r
 // (y+dx, x+dy), both clamped to the image (np.pad mode="edge").
 __global__ void normal_state_kernel(const float* __restrict__ nrm, const uint8_t* __restrict__ nmask, int n, int H,
                                     int W, float cos_thr, uint8_t* __restrict__ state) {
-  const int64_t total = (int64_t)n * H * W;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int im = (int)(e / ((int64_t)H * W));
-    const int rem = (int)(e - (int64_t)im * H * W);
+  const int total = n * H * W, HW = H * W;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int im = e / HW;
+    const int rem = e - im * HW;
     const int y = rem / W, x = rem - y * W;
-    const float* N = nrm + (int64_t)im * H * W * 3;
-    const uint8_t* Mk = nmask + (int64_t)im * H * W;
+    const float* N = nrm + (int64_t)im * HW * 3;  // unit normals (K1)
+    const uint8_t* Mk = nmask + (int64_t)im * HW;
     float c[3];
     {
-      const float* q = N + ((int64_t)y * W + x) * 3;
-      const float nc = norm3(q) + 1e-12f;
-      for (int k = 0; k < 3; ++k) c[k] = q[k] / nc;
+      const float* q = N + (y * W + x) * 3;
+      for (int k = 0; k < 3; ++k) c[k] = q[k];
     }
     bool nan = false, edge = false;
     for (int dy = -1; dy <= 1; ++dy)
@@ -114,10 +118,8 @@ __global__ void normal_state_kernel(const float* __restrict__ nrm, const uint8_t
         const int my = min(max(y + dx, 0), H - 1), mx = min(max(x + dy, 0), W - 1);
         float d = 1.f;  // masked out: angle 0 = arccos(1)
         if (Mk[my * W + mx]) {
-          const float* q = N + ((int64_t)ny * W + nx) * 3;
-          const float nq = norm3(q) + 1e-12f;
-          const float w0 = q[0] / nq, w1 = q[1] / nq, w2 = q[2] / nq;
-          d = c[0] * w0 + c[1] * w1 + c[2] * w2;
+          const float* q = N + (ny * W + nx) * 3;
+          d = c[0] * q[0] + c[1] * q[1] + c[2] * q[2];
           if (!(fabsf(d) <= 1.f)) nan = true;  // arccos -> NaN (also for NaN d)
         }
         edge |= d < cos_thr;
@@ -131,13 +133,13 @@ __global__ void normal_state_kernel(const float* __restrict__ nrm, const uint8_t
 __global__ void mask_combine_kernel(const uint8_t* __restrict__ state, const float* __restrict__ depth_z,
                                     int64_t dz_stride, const uint8_t* __restrict__ m_in, int n, int H, int W,
                                     float rtol, int use_edges, uint8_t* __restrict__ m_out) {
-  const int64_t total = (int64_t)n * H * W;
-  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+  const int total = n * H * W, HW = H * W;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
     const bool mc = m_in[e] != 0;
     bool keep = mc;
     if (use_edges && mc) {
-      const int im = (int)(e / ((int64_t)H * W));
-      const int rem = (int)(e - (int64_t)im * H * W);
+      const int im = e / HW;
+      const int rem = e - im * HW;
       const int y = rem / W, x = rem - y * W;
       const uint8_t* S = state + (int64_t)im * H * W;
       const uint8_t* M = m_in + (int64_t)im * H * W;
@@ -325,6 +327,7 @@ extern "C" int mapa_postprocess_mask(const float* pts3d, const float* pts3d_cam,
                  "mapa_postprocess_mask: bad args");
   MAPA_CHECK_ARG(!use_edges || work, "mapa_postprocess_mask: edges need a work buffer");
   const int64_t P = (int64_t)n * H * W;
+  MAPA_CHECK_ARG(P < (1LL << 31), "mapa_postprocess_mask: more than 2^31 pixels in one call");
   float* nrm = reinterpret_cast<float*>(work);
   uint8_t* nmask = reinterpret_cast<uint8_t*>(nrm + P * 3);
   uint8_t* state = nmask + P;
