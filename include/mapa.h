@@ -97,7 +97,8 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
  * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
  * 2560..2574 = 256-row tiles, 2575..2578 = phase-interleaved 256x256 tiles (2579 / 2583 timing diagnostics),
  * 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one the automatic choice runs),
- * 2584..2586 = LDS halo-window conv, 2590/2591 = four-wave 256x256 / 192x256 tiles. */
+ * 2584..2586 = LDS halo-window conv, 2587 = 192x192 tiles, 2590/2591 = four-wave 256x256 / 192x256 tiles,
+ * 2592/2593 = four-wave inline-asm MFMA tiles. */
 int mapa_gemm_set_variant(int variant);
 /* The regressor tail in one launch (DPTRegressionProcessor conv2 + the dense head, dpt.py:285-311 and model.py:
  * 1865-2150): d describes the 3x3 conv 128 -> 128 (bf16, stride 1, conv_kblock 32, act MAPA_ACT_RELU, bias; no

@@ -78,10 +78,18 @@ def main():
             W = (torch.randn(N, K, device="cuda") * K ** -0.5).to(dt)
             b = torch.randn(N, device="cuda")
             o = torch.empty(M, N, device="cuda", dtype=dt)
+            # the residual linears (attn proj, fc2) update the fp32 stream in place: x = x + gamma * (A W^T + b)
+            resid = name.endswith(("proj", "fc2")) and not os.environ.get("KB_NO_RESID")
+            x = torch.randn(M, N, device="cuda") if resid else None
+            gam = torch.randn(N, device="cuda") * 0.1 if resid else None
+
             def run(var):
                 def f():
                     nat.gemm_set_variant(var)
-                    nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
+                    if resid:
+                        nat.gemm(A, W, M, N, K, bias=b, gamma=gam, resid1=x, out_f32=x)
+                    else:
+                        nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
                 return f
             fns = [run(v) for v in VARIANTS]
             if "torch" in sys.argv:
