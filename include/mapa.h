@@ -111,7 +111,8 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
 
 /* Tuning / A-B hooks of the automatic kernel choice (process-wide):
  *   MAPA_TUNE_CONV_HALO (default 1): stride-1 bf16 convs in the 32-channel-slice K order (conv_kblock = 32) run on
- *     the LDS halo-window conv; 0 keeps them on the implicit GEMM (variants 2584 / 2585 / 2586 force it);
+ *     the LDS halo-window conv (N = 256: 8x16-pixel blocks, 256-wide tiles; else 16x16 blocks); 2 keeps 16x16
+ *     blocks for every N; 0 keeps them on the implicit GEMM (variants 2584 / 2585 / 2586 / 2588 force one);
  *   MAPA_TUNE_TAIL_STREAMK (default 0): dense bf16 GEMMs whose 256x128 tiles leave a nearly empty last wave use
  *     the tail-only stream-K schedule (2582) when a workspace is passed. */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1 };

@@ -23,25 +23,29 @@ namespace mapa_gemm_impl {
 namespace {
 
 constexpr int HT = 512;           // threads
-constexpr int HB = 16;            // output block edge (pixels)
-constexpr int WE = HB + 2;        // window edge
-constexpr int WPIX = WE * WE;     // 324 window pixels
-constexpr int WPIECES = WPIX * 4; // 16-B pieces per window (64 B per pixel)
-constexpr int WROUNDS = (WPIECES + HT - 1) / HT;  // 3 DMA instructions per thread per window
-constexpr int WBYTES = WROUNDS * HT * 16;         // 24 KiB per window buffer (tail pieces land in padding)
+constexpr int BW = 16;            // output block width (pixels): one MFMA row fragment = one block row
+constexpr int WE = BW + 2;        // window width
 constexpr int H_ELD = 68;
 
-template <int BN>
+// BN output channels x a BH x 16 pixel block.  BH = 16: (BN 256) 8 waves 2 x 4 of 128x64, 1 workgroup / CU, or
+// (BN 128) 4 x 2 of 64x64, 2 / CU.  BH = 8 with BN 256: 2 x 4 waves of 64x64, 2 / CU — for 148^2 maps, where 16-row
+// blocks leave 17 % of the pixels idle (160 vs 148 rows) and 1600 tiles fill 3.1 rounds of 512 slots, 8-row blocks
+// cover 152 rows in 1520 tiles (2.97 rounds) and stage each window once for all 256 output channels.
+template <int BN, int BH = 16>
 struct HCfg {
-  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
-  static constexpr int TM = 256 / WM, TN = BN / WN;  // 128x64 or 64x64
+  static constexpr int WM = (BN == 256) ? 2 : 4, WN = 8 / WM;
+  static constexpr int TM = BH * BW / WM, TN = BN / WN;  // 128x64, 64x64 or 64x64
   static constexpr int FM = TM / 16, FN = TN / 16;
-  static constexpr int S = BN == 256 ? 6 : 4;        // W ring slots
-  static constexpr int WT = BN * 64;                 // W tile bytes (32 bf16 per row)
-  static constexpr int NWG = WT / (HT * 16);         // W DMA instructions per thread per K tile (2 or 1)
-  static constexpr int LDS = S * WT + 2 * WBYTES;    // 144 KiB or 80 KiB
-  static constexpr int MINB = BN == 256 ? 1 : 2;
-  static_assert(TN == 64 && FM % 2 == 0, "epilogue: 64-column wave tiles, 32-row passes");
+  static constexpr int S = BH == 8 ? 3 : BN == 256 ? 6 : 4;  // W ring slots
+  static constexpr int WT = BN * 64;                          // W tile bytes (32 bf16 per row)
+  static constexpr int NWG = WT / (HT * 16);                  // W DMA instructions per thread per K tile (2 or 1)
+  static constexpr int WH = BH + 2;                           // window rows
+  static constexpr int WPIECES = WH * WE * 4;                 // 16-B pieces per window (64 B per pixel)
+  static constexpr int WROUNDS = (WPIECES + HT - 1) / HT;     // DMA instructions per thread per window (3 or 2)
+  static constexpr int WBYTES = WROUNDS * HT * 16;            // window buffer (tail pieces land in padding)
+  static constexpr int LDS = S * WT + 2 * WBYTES;             // 144, 80 or 80 KiB
+  static constexpr int MINB = (BN == 256 && BH == 16) ? 1 : 2;
+  static_assert(TN == 64 && FM % 2 == 0 && FM * WM == BH, "epilogue: 64-column wave tiles, 32-row passes");
   static_assert(8 * 32 * H_ELD * 4 <= LDS, "epilogue staging");
 };
 
@@ -86,10 +90,10 @@ __device__ __forceinline__ void vm_wait(int n) {
 
 // DMA group of K tile kt: its W tile (ring slot kt % S) and, on a slice's first tap, that slice's window (a device
 // function, not a lambda in the kernel: with a lambda the host pass drops the kernel's launch stub)
-template <int BN>
+template <int BN, int BH>
 __device__ __forceinline__ void halo_stage(const GemmArgs& p, char* wring, char* wins, int kt, int wave,
                                            const char* const* w_src, const int64_t* wsrc, const bool* wok) {
-  using C = HCfg<BN>;
+  using C = HCfg<BN, BH>;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const char* abase = reinterpret_cast<const char*>(p.A);
   char* dst = wring + (kt % C::S) * C::WT + wave * 1024;
@@ -99,16 +103,16 @@ __device__ __forceinline__ void halo_stage(const GemmArgs& p, char* wring, char*
   const int slice = kt / 9;
   if (kt - slice * 9 == 0) {
     const int64_t ch = split_col(p, slice * 32);
-    char* wd = wins + (slice & 1) * WBYTES + wave * 1024;
+    char* wd = wins + (slice & 1) * C::WBYTES + wave * 1024;
 #pragma unroll
-    for (int r = 0; r < WROUNDS; ++r)
+    for (int r = 0; r < C::WROUNDS; ++r)
       __builtin_amdgcn_global_load_lds(wok[r] ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16, 0, 0);
   }
 }
 
-template <int BN, bool HO = false>
-__global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs p, HeadOut ho) {
-  using C = HCfg<BN>;
+template <int BN, bool HO = false, int BH = 16>
+__global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(GemmArgs p, HeadOut ho) {
+  using C = HCfg<BN, BH>;
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS];
   char* const wring = lds;
   char* const wins = lds + C::S * C::WT;
@@ -117,7 +121,7 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
   // ---- tile: (img, block row, block col, column tile), XCD-contiguous ranges of neighbouring blocks
-  const int nbx = (p.cv_OW + HB - 1) / HB, nby = (p.cv_OH + HB - 1) / HB, ntn = p.N / BN;
+  const int nbx = (p.cv_OW + BW - 1) / BW, nby = (p.cv_OH + BH - 1) / BH, ntn = p.N / BN;
   const int imgs = p.M / (p.cv_OH * p.cv_OW);
   int t = xcd_remap(blockIdx.x, imgs * nby * nbx * ntn);
   const int tn = t % ntn;
@@ -129,16 +133,16 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
   const int nk = p.K / 32;  // 9 taps x (logical channels / 32)
 
   // ---- window staging geometry (this thread's WROUNDS pieces; pixel offsets are slice-invariant)
-  int64_t wsrc[WROUNDS];
-  bool wok[WROUNDS];
+  int64_t wsrc[C::WROUNDS];
+  bool wok[C::WROUNDS];
 #pragma unroll
-  for (int r = 0; r < WROUNDS; ++r) {
+  for (int r = 0; r < C::WROUNDS; ++r) {
     const int q = r * HT + tid;
     const int wp = q >> 2, cl = q & 3;
     const int cs = cl ^ ((wp >> 2) & 3);
     const int wy = wp / WE, wx = wp - wy * WE;
-    const int iy = by * HB - 1 + wy, ix = bx * HB - 1 + wx;
-    wok[r] = q < WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+    const int iy = by * BH - 1 + wy, ix = bx * BW - 1 + wx;
+    wok[r] = q < C::WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
     wsrc[r] = wok[r] ? ((int64_t)(img * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
   }
   // ---- W staging geometry: instruction i of this wave covers ring rows (i*8 + wave)*16 + [0, 16)
@@ -167,20 +171,20 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
 
 #pragma unroll
   for (int s0 = 0; s0 < C::S - 1; ++s0)
-    if (s0 < nk) halo_stage<BN>(p, wring, wins, s0, wave, w_src, wsrc, wok);
+    if (s0 < nk) halo_stage<BN, BH>(p, wring, wins, s0, wave, w_src, wsrc, wok);
   for (int kt = 0; kt < nk; ++kt) {
     // groups issued after kt's: W tiles kt+1 .. kt+after, plus a window if one of them starts a slice
     const int after = min(C::S - 2, nk - 1 - kt);
     const int next9 = (kt / 9 + 1) * 9;
-    vm_wait(C::NWG * after + (next9 <= kt + after ? WROUNDS : 0));
+    vm_wait(C::NWG * after + (next9 <= kt + after ? C::WROUNDS : 0));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + C::S - 1 < nk) halo_stage<BN>(p, wring, wins, kt + C::S - 1, wave, w_src, wsrc, wok);
+    if (kt + C::S - 1 < nk) halo_stage<BN, BH>(p, wring, wins, kt + C::S - 1, wave, w_src, wsrc, wok);
     const int slice = kt / 9, tap = kt - slice * 9;
     const int ky = tap / 3, kx = tap - ky * 3;
     const char* Ws = wring + (kt % C::S) * C::WT;
-    const char* Win = wins + (slice & 1) * WBYTES;
+    const char* Win = wins + (slice & 1) * C::WBYTES;
     b8 b[C::FN];
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const b8*>(Ws + b_off[j]);
@@ -201,7 +205,7 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
     // channels wn*64 + j*16 + r16: per block row it forms the 6 partial dot products of its 4 pixels over its 4
     // channels, a reduce-scatter over the 16 lanes of its group (then a pairwise sum) leaves 3 of them per lane
     // pair, and the two channel halves (waves wn = 0, 1) meet in LDS.
-    static_assert(BN == 128 && C::FM == 4 && C::FN == 4, "head-out tail: 128-wide tiles");
+    static_assert(BN == 128 && BH == 16 && C::FM == 4 && C::FN == 4, "head-out tail: 128-wide 16x16 tiles");
     float* part = reinterpret_cast<float*>(lds);  // [256 pixels][2 halves][6]
 #pragma unroll
     for (int i = 0; i < 4; ++i) {  // one block row (16 pixels of which this lane group holds 4) at a time
@@ -249,7 +253,7 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
     __syncthreads();
     if (tid < 256) {
       const int py = tid >> 4, px = tid & 15;
-      const int oy = by * HB + py, ox = bx * HB + px;
+      const int oy = by * BH + py, ox = bx * BW + px;
       if (oy < p.cv_OH && ox < p.cv_OW) {
         float raw[6];
 #pragma unroll
@@ -279,7 +283,7 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
 #pragma unroll 2
     for (int pass = 0; pass < 8; ++pass) {
       const int rloc = pass * 4 + g;  // row of the 32-row pass: block row wm*FM + part*2 + rloc/16, px rloc%16
-      const int oy = by * HB + wm * C::FM + part * 2 + (rloc >> 4), ox = bx * HB + (rloc & 15);
+      const int oy = by * BH + wm * C::FM + part * 2 + (rloc >> 4), ox = bx * BW + (rloc & 15);
       if (oy < p.cv_OH && ox < p.cv_OW)
         epi_store_row<bf16_t>(p, ec, (img * p.cv_OH + oy) * p.cv_OW + ox,
                               *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c4));
@@ -293,18 +297,24 @@ __global__ void __launch_bounds__(HT, HCfg<BN>::MINB) conv_halo_kernel(GemmArgs 
 
 }  // namespace
 
-// bn: 256 or 128 output channels per tile (0 = 256 when N % 256 == 0, else 128).  Needs a bf16 stride-1 conv in the
+// bn: 256 or 128 output channels per tile (0 = 256 when N % 256 == 0, else 128); bh: block rows (16, or 8 with
+// bn 256).  Needs a bf16 stride-1 conv in the
 // channel-block-major K order with 32-channel slices (conv_kblock == 32); returns false otherwise.
-bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream) {
+bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh) {
   if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
   if (bn == 0) bn = a.N % 256 == 0 ? 256 : 128;
+  if (bh == 8 && bn != 256) return false;
   if (a.N % bn != 0 || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
   const int hw = a.cv_OH * a.cv_OW;
-  const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + HB - 1) / HB) * ((a.cv_OW + HB - 1) / HB) * (a.N / bn);
+  const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + bh - 1) / bh) * ((a.cv_OW + BW - 1) / BW) * (a.N / bn);
   if (tiles >= (int64_t(1) << 31)) return false;
   const HeadOut none{};
-  if (bn == 256) hipLaunchKernelGGL((conv_halo_kernel<256>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
-  else hipLaunchKernelGGL((conv_halo_kernel<128>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+  if (bh == 8)
+    hipLaunchKernelGGL((conv_halo_kernel<256, false, 8>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+  else if (bn == 256)
+    hipLaunchKernelGGL((conv_halo_kernel<256>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<128>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
   return true;
 }
 
@@ -314,7 +324,7 @@ bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b
   if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
   if (a.N != 128 || !a.bias || a.act != MAPA_ACT_RELU || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
   const int hw = a.cv_OH * a.cv_OW;
-  const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + HB - 1) / HB) * ((a.cv_OW + HB - 1) / HB);
+  const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + 15) / 16) * ((a.cv_OW + BW - 1) / BW);
   if (tiles >= (int64_t(1) << 31)) return false;
   HeadOut h;
   h.w6 = w6; h.b6 = b6; h.pose = pose; h.scale = scale;

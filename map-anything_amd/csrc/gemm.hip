@@ -297,7 +297,9 @@ int pick_variant(int dtype, bool conv, int M, int N, int K) {
 // blocks fill the CUs (the 148^2 .. 518^2 DPT head convs); the small-image convs keep the implicit GEMM / stream-K.
 // Measured (kbench, 8 views): the 128-wide tile at 2 workgroups / CU beats the 256-wide one on every head conv
 // (reg2@518 1794 vs 2567 us, rn1@148 652 vs 781) and the implicit GEMM from 148^2 up (2207 / 734 us); at 74^2 and
-// below (<= 400 tiles) the implicit GEMM / stream-K stay ahead.
+// below (<= 400 tiles) the implicit GEMM / stream-K stay ahead.  N = 256 (the 148^2 DPT convs) runs 8x16-pixel
+// blocks with 256-wide tiles, 2 / CU (rn1@148 643 -> 613 us, l1rn@148 284 -> 260: fewer idle rows at 148, 2.97
+// instead of 3.1 rounds); N = 128 keeps 16x16 blocks.
 static int g_halo = 1;     // mapa_gemm_tune(MAPA_TUNE_CONV_HALO, .)
 static int g_tail_sk = 0;  // mapa_gemm_tune(MAPA_TUNE_TAIL_STREAMK, .)
 static bool pick_halo(int M, int N, int OH, int OW, int kb) {
@@ -418,10 +420,14 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int variant = forced ? forced : pick_variant(d->dtype, conv, d->M, d->N, d->K);
   const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
   const bool halo = conv && d->dtype == MAPA_BF16 &&
-                    (forced ? (forced >= 2584 && forced <= 2586) : pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb));
+                    (forced ? (forced >= 2584 && forced <= 2586) || forced == 2588
+                            : pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb));
   if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
-  } else if (halo && launch_conv_halo(a, forced == 2585 ? 256 : 128, stream)) {
+  } else if (halo && (forced ? launch_conv_halo(a, forced == 2585 || forced == 2588 ? 256 : 128, stream,
+                                                forced == 2588 ? 8 : 16)
+                              : launch_conv_halo(a, a.N % 256 == 0 && g_halo == 1 ? 256 : 128, stream,
+                                                 a.N % 256 == 0 && g_halo == 1 ? 8 : 16))) {
     // launched (LDS halo-window conv)
   } else if (d->dtype == MAPA_BF16 && ((variant >= 2575 && variant <= 2579) || variant == 2583) &&
              launch_gemm_8p(a, conv, variant == 2583 ? 5 : variant - 2575, stream)) {
@@ -466,14 +472,14 @@ extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6,
 
 extern "C" int mapa_gemm_tune(int key, int value) {
   MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK, "mapa_gemm_tune: unknown key %d", key);
-  if (key == MAPA_TUNE_CONV_HALO) g_halo = value ? 1 : 0;
+  if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 ? 2 : value ? 1 : 0;
   else g_tail_sk = value ? 1 : 0;
   return 0;
 }
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2587) ||
+                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2588) ||
                      variant == 2590 || variant == 2591 || variant == 2592 || variant == 2593,
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;

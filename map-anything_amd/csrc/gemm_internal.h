@@ -205,7 +205,7 @@ bool launch_gemm_8p(const GemmArgs& a, bool conv, int diag, hipStream_t stream);
 
 // Stride-1 3x3 conv with its A operand read from an LDS halo window (conv_halo.hip); bn = 256 / 128 / 0 (auto).
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).
-bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream);
+bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh = 16);
 
 // The halo conv with the regressor tail fused into its epilogue (conv_halo.hip): conv3x3 128->128 + ReLU, 1x1 128->6,
 // adaptors and output assembly.  false unless the conv qualifies (bf16, stride 1, conv_kblock 32, N 128, ReLU, bias).

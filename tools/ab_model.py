@@ -34,6 +34,9 @@ def main():
     elif what == "halo":  # the kernel choice is baked into each model's captured graph at its first infer
         arms = [("halo", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 1)),
                 ("implicit", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 0))]
+    elif what == "halo8":  # N = 256 halo convs: 8x16-pixel blocks / 256-wide tiles vs 16x16 / 128-wide
+        arms = [("rows8", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 1)),
+                ("rows16", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 2))]
     elif what == "tailsk":
         arms = [("tailsk", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 1)),
                 ("dataparallel", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 0))]
