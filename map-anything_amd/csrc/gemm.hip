@@ -331,7 +331,9 @@ int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   if (f) return f >= 2580 && f <= 2582 ? f : 0;
   if (dtype != MAPA_BF16) return 0;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
-  if (big_tiles < 256 && K >= 4096) return 2580;
+  // 256x256 stream-K tiles from N = 512 up at a few thousand rows (the stride-2 768-channel DPT conv at 37 -> 19,
+  // M = views * 361: 244 -> 152 us); the 224^2 geometric encoders (M = views * 256) keep 256x128
+  if (big_tiles < 256 && K >= 4096) return N >= 512 && M >= 2048 ? 2581 : 2580;
   // tail-only stream-K where the 256x128 data-parallel schedule leaves a nearly empty last wave (enc.qkv / aat.fc1
   // at 8 views: 1032 tiles on 512 slots -> a third wave of 8 tiles)
   if (g_tail_sk && !conv) {

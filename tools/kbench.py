@@ -36,7 +36,7 @@ if os.environ.get("KB_HEADS"):  # the split-precision (3C-wide operand) head con
     CONVS = [("l1rn@148", V, 148, 148, 288, 256), ("l2rn@74", V, 74, 74, 576, 256), ("l3rn@37", V, 37, 37, 1152, 256),
              ("l4rn@19", V, 19, 19, 2304, 256), ("rn4@19", V, 19, 19, 768, 256), ("rn3@37", V, 37, 37, 768, 256),
              ("rn2@74", V, 74, 74, 768, 256), ("rn1@148", V, 148, 148, 768, 256), ("reg1@296", V, 296, 296, 768, 128),
-             ("reg2@518", V, 518, 518, 384, 128)]
+             ("reg2@518", V, 518, 518, 384, 128), ("ip3s2@37", V, 37, 37, 2304, 768, 2)]
 if ONLY:
     CONVS = [c for c in CONVS if c[0] in ONLY.split(",")]
 
@@ -103,12 +103,14 @@ def main():
                       flush=True)
             nat.gemm_set_variant(0)
     if what in ("conv", "all"):
-        for name, n, H, W_, C, Co in CONVS:
+        for name, n, H, W_, C, Co, *st in CONVS:  # optional 7th field: stride
+            stride = st[0] if st else 1
+            OH, OW = (H - 1) // stride + 1, (W_ - 1) // stride + 1
             x = (torch.randn(n, H, W_, C, device="cuda") * 0.5).to(dt)
             w0 = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(dt)
             b = torch.randn(Co, device="cuda")
-            o = torch.empty(n * H * W_, Co, device="cuda", dtype=dt)
-            M = n * H * W_
+            o = torch.empty(n * OH * OW, Co, device="cuda", dtype=dt)
+            M = n * OH * OW
             combos = []
             for kb in KBLOCKS:  # channel-block-major K order (mapa_gemm_desc.conv_kblock)
                 w = w0
@@ -120,7 +122,7 @@ def main():
             def runc(var, w):
                 def f():
                     nat.gemm_set_variant(var)
-                    nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, H, W_, 1))
+                    nat.gemm(x, w, M, Co, 9 * C, bias=b, out_lp=o, conv=(C, H, W_, OH, OW, stride))
                 return f
             for (var, kb, _), ms in zip(combos, interleaved([runc(v, w) for v, _, w in combos], reps)):
                 print(f"conv {name:10s} v{var:<4d} kb{kb:<3d} M={M} N={Co} K={9*C}: {ms*1e3:8.1f} us  "
