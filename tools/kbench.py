@@ -82,12 +82,15 @@ def main():
             resid = name.endswith(("proj", "fc2")) and not os.environ.get("KB_NO_RESID")
             x = torch.randn(M, N, device="cuda") if resid else None
             gam = torch.randn(N, device="cuda") * 0.1 if resid else None
+            gelu = name.endswith("fc1") and not os.environ.get("KB_NO_RESID")  # the MLP's first linear: GELU epilogue
 
             def run(var):
                 def f():
                     nat.gemm_set_variant(var)
                     if resid:
                         nat.gemm(A, W, M, N, K, bias=b, gamma=gam, resid1=x, out_f32=x)
+                    elif gelu:
+                        nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=o)
                     else:
                         nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
                 return f
