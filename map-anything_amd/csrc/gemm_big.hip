@@ -209,11 +209,11 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   }
   __syncthreads();  // all waves done with the last stage: LDS becomes the epilogue staging area
 
-  // ---- epilogue: 32 rows x 64 fp32 per wave per pass through LDS, 16-B stores --------------------------------
+  // ---- epilogue: 32 rows x 64 fp32 per wave per pass through LDS; 8 columns per lane (16-B bf16 stores) -------
   float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
-  const int c4 = (lane & 15) * 4;
-  const int n0 = bn + wn * C::TN + c4;
-  const EpiCol ec = epi_col_setup(p, n0);
+  const int c8 = (lane & 7) * 8;
+  const int n0 = bn + wn * C::TN + c8;
+  const EpiCol8 ec = epi_col_setup8(p, n0);
 #pragma unroll
   for (int part = 0; part < C::FM / 2; ++part) {
 #pragma unroll
@@ -225,13 +225,14 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (n0 < p.N && c4 < C::TN) {
+    if (n0 < p.N && c8 < C::TN) {
 #pragma unroll 2
-      for (int pass = 0; pass < 8; ++pass) {
-        const int rloc = pass * 4 + g;
+      for (int pass = 0; pass < 4; ++pass) {
+        const int rloc = pass * 8 + (lane >> 3);
         const int m = bm + wm * C::TM + part * 32 + rloc;
         if (m >= p.M) break;
-        epi_store_row<bf16_t>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c4));
+        epi_store_row8<bf16_t>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8),
+                               *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8 + 4));
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -196,6 +196,91 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
   }
 }
 
+// 8 consecutive columns n0..n0+7 of row m: one 16-B store per bf16 output row segment (the 4-column form stores 8 B)
+// for row-major outputs with n0 % 8 == 0 and ldo % 8 == 0; otherwise two 4-column calls.
+struct EpiCol8 {
+  EpiCol a, b;
+  bool vec8;
+};
+
+__device__ __forceinline__ EpiCol8 epi_col_setup8(const GemmArgs& p, int n0) {
+  EpiCol8 c;
+  c.a = epi_col_setup(p, n0);
+  c.b = epi_col_setup(p, n0 + 4);
+  c.vec8 = p.out_mode == 0 && p.vec_ok && p.ldo % 8 == 0 && n0 + 7 < p.N;
+  return c;
+}
+
+template <typename T>
+__device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8& c, int m, f32x4 lo, f32x4 hi) {
+  if (!c.vec8) {
+    epi_store_row<T>(p, c.a, m, lo);
+    if (c.b.n0 < p.N) epi_store_row<T>(p, c.b, m, hi);
+    return;
+  }
+  const int64_t ld = p.ldo;
+  const int64_t off = (int64_t)m * ld + c.a.n0;
+  const int64_t off3 = (int64_t)m * 2 * ld + c.a.n0;
+  f32x4 v0, v1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v0[e] = epi_act(lo[e] + c.a.bv[e], p.act) * c.a.gv[e];
+    v1[e] = epi_act(hi[e] + c.b.bv[e], p.act) * c.b.gv[e];
+  }
+  if (p.resid1) {
+    v0 += *reinterpret_cast<const f32x4*>(p.resid1 + off);
+    v1 += *reinterpret_cast<const f32x4*>(p.resid1 + off + 4);
+  }
+  if (p.resid2) {
+    v0 += *reinterpret_cast<const f32x4*>(p.resid2 + off);
+    v1 += *reinterpret_cast<const f32x4*>(p.resid2 + off + 4);
+  }
+  if (p.act == MAPA_ACT_GELU_POST) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = gelu_erf(v0[e]);
+      v1[e] = gelu_erf(v1[e]);
+    }
+  }
+  if (p.out_f32) {
+    *reinterpret_cast<f32x4*>(p.out_f32 + off) = v0;
+    *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = v1;
+  }
+  if constexpr (sizeof(T) == 2) {
+    if (p.out_lp) {
+      const uint4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                       pack_bf16x2(v1[2], v1[3])};
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
+    }
+    if (p.out_lp_relu) {
+      const uint4 u = {pack_bf16x2(fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f)), pack_bf16x2(fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)),
+                       pack_bf16x2(fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f)), pack_bf16x2(fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
+      *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
+    }
+    if (p.out_s3) {
+      store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0);
+      store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + 4, ld, v1);
+    }
+    if (p.out_s3_relu) {
+      const f32x4 r0 = {fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f), fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)};
+      const f32x4 r1 = {fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f), fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f)};
+      store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, r0);
+      store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + 4, ld, r1);
+    }
+  } else {
+    if (p.out_lp) {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v0;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off + 4) = v1;
+    }
+    if (p.out_lp_relu) {
+      const f32x4 r0 = {fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f), fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)};
+      const f32x4 r1 = {fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f), fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f)};
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off) = r0;
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp_relu) + off + 4) = r1;
+    }
+  }
+}
+
 // 256-row bf16 kernel (gemm_big.hip): variant 0 = 256x256 tile, 1 = 256x128 tile.  Returns false if it does not
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
