@@ -264,11 +264,11 @@ __global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(Gem
       }
     }
   } else {
-  // ---- epilogue: 32 rows (two block rows) x 64 fp32 per wave per pass through LDS, 16-B stores
+  // ---- epilogue: 32 rows (two block rows) x 64 fp32 per wave per pass through LDS, 8 columns per lane
   float* ep = reinterpret_cast<float*>(lds) + wave * 32 * H_ELD;
-  const int c4 = (lane & 15) * 4;
-  const int n0 = bn + wn * C::TN + c4;
-  const EpiCol ec = epi_col_setup(p, n0);
+  const int c8 = (lane & 7) * 8;
+  const int n0 = bn + wn * C::TN + c8;
+  const EpiCol8 ec = epi_col_setup8(p, n0);
 #pragma unroll
   for (int part = 0; part < C::FM / 2; ++part) {
 #pragma unroll
@@ -281,12 +281,13 @@ __global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(Gem
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll 2
-    for (int pass = 0; pass < 8; ++pass) {
-      const int rloc = pass * 4 + g;  // row of the 32-row pass: block row wm*FM + part*2 + rloc/16, px rloc%16
+    for (int pass = 0; pass < 4; ++pass) {
+      const int rloc = pass * 8 + (lane >> 3);  // row of the 32-row pass: block row wm*FM + part*2 + rloc/16, px rloc%16
       const int oy = by * BH + wm * C::FM + part * 2 + (rloc >> 4), ox = bx * BW + (rloc & 15);
       if (oy < p.cv_OH && ox < p.cv_OW)
-        epi_store_row<bf16_t>(p, ec, (img * p.cv_OH + oy) * p.cv_OW + ox,
-                              *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c4));
+        epi_store_row8<bf16_t>(p, ec, (img * p.cv_OH + oy) * p.cv_OW + ox,
+                               *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c8),
+                               *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c8 + 4));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

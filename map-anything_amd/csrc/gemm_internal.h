@@ -257,15 +257,11 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
                        pack_bf16x2(fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f)), pack_bf16x2(fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
     }
-    if (p.out_s3) {
-      store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0);
-      store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + 4, ld, v1);
-    }
+    if (p.out_s3) store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0, v1);
     if (p.out_s3_relu) {
       const f32x4 r0 = {fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f), fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)};
       const f32x4 r1 = {fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f), fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f)};
-      store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, r0);
-      store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + 4, ld, r1);
+      store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, r0, r1);
     }
   } else {
     if (p.out_lp) {

@@ -62,6 +62,21 @@ __device__ __forceinline__ void store_split3(bf16_t* p, int64_t ld, f32x4 v) {
   *reinterpret_cast<uint2*>(p) = h;
   *reinterpret_cast<uint2*>(p + ld) = l;
 }
+// 8 consecutive values (16-B aligned): one 16-B store of hi, one of lo
+__device__ __forceinline__ void store_split3x8(bf16_t* p, int64_t ld, f32x4 a, f32x4 b) {
+  uint4 h, l;
+  uint32_t* hp = &h.x;
+  uint32_t* lp = &l.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float x0 = k < 2 ? a[2 * k] : b[2 * k - 4], x1 = k < 2 ? a[2 * k + 1] : b[2 * k - 3];
+    const bf16_t h0 = f32_to_bf16(x0), h1 = f32_to_bf16(x1);
+    hp[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+    lp[k] = pack_bf16x2(x0 - bf16_to_f32(h0), x1 - bf16_to_f32(h1));
+  }
+  *reinterpret_cast<uint4*>(p) = h;
+  *reinterpret_cast<uint4*>(p + ld) = l;
+}
 __device__ __forceinline__ void store_split1(bf16_t* p, int64_t ld, float x) {
   const bf16_t h = f32_to_bf16(x);
   p[0] = h;
