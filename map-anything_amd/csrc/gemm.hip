@@ -225,9 +225,9 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
 
   // ---- epilogue: accumulators -> LDS (per-wave 32 x 64 fp32 half tile) -> 16-B row segments ------------
   float* ep = reinterpret_cast<float*>(lds) + wave * 32 * EPI_LD;
-  const int c4 = (lane & 15) * 4;
-  const int n0 = bn + wn * 64 + c4;
-  const EpiCol ec = epi_col_setup(p, n0);
+  const int c8 = (lane & 7) * 8;  // 8 columns per lane (16-B bf16 stores, epi_store_row8)
+  const int n0 = bn + wn * 64 + c8;
+  const EpiCol8 ec = epi_col_setup8(p, n0);
   const int g = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -242,11 +242,12 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (n0 < p.N) {
 #pragma unroll 2
-      for (int pass = 0; pass < 8; ++pass) {
-        const int rloc = pass * 4 + (lane >> 4);
+      for (int pass = 0; pass < 4; ++pass) {
+        const int rloc = pass * 8 + (lane >> 3);
         const int m = bm + wm * 64 + half * 32 + rloc;
         if (m >= p.M) break;
-        epi_store_row<T>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c4));
+        epi_store_row8<T>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c8),
+                          *reinterpret_cast<const f32x4*>(ep + rloc * EPI_LD + c8 + 4));
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
