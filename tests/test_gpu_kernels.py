@@ -62,6 +62,23 @@ def test_gemm_epilogues(nat):
     assert rel_l2(x.cpu(), (r1 + g * acc).cpu()) < 1e-4
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_gemm_gelu_epilogue_fp32_exactness(nat, dtype):
+    """The GELU epilogue's erf (mapa_common.h erf_as, Abramowitz-Stegun 7.1.26) against torch's exact-erf GELU on
+    fp32 outputs: |error| <= 5e-7 absolute, including the negative tail and |x| > 4 (the 8-column epilogue path
+    and its 4-column tail: N = 200 is not a multiple of 8)."""
+    M, N, K = 513, 200, 64
+    A = (_rand(M, K, seed=70) * 1.5).to(dtype)
+    W = _rand(N, K, scale=K ** -0.5, seed=71).to(dtype)
+    b = _rand(N, seed=72)
+    out = torch.empty(M, N, device="cuda")
+    nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_f32=out)
+    pre = (A.double() @ W.double().t() + b.double()).float()
+    ref = F.gelu(pre.double()).float()
+    assert float(pre.abs().max()) > 4.0  # the tails are exercised
+    assert float((out - ref).abs().max()) < (5e-6 if dtype == torch.float32 else 5e-5)
+
+
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2575, 2576, 2577, 2578, 2590, 2591,
                                      2592, 2593, 2587])
 @pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72)])
