@@ -289,6 +289,9 @@ int pick_variant(int dtype, bool conv, int M, int N, int K) {
   if (!conv && N % 192 == 0 && t192sq <= 256 && t192sq > t192) return 2587;
   if (t192 <= 256 && t256 <= 192 && N >= 256) return 2574;
   if (conv) return N >= 256 ? 2568 : 2571;
+  // 256x128 tiles at 2 / CU leaving a nearly empty last round (enc.qkv at 8 views: 1032 tiles on 512 slots) with
+  // K >= 1024: 192x256 tiles at 1 / CU (696 tiles, 2.7 rounds) measured 97.2 -> 93.0 us (K = 768: equal)
+  if (K >= 1024 && K < 4096 && big_tiles > 512 && big_tiles % 512 != 0 && (big_tiles % 512) * 8 < 512) return 2574;
   if (K >= 4096) return 2568;
   if (N >= 3072 && K <= 1024) return 2570;
   return 2571;
