@@ -82,12 +82,6 @@ __device__ __forceinline__ void conv_kmap(const GemmArgs& p, int kc, int& tap, i
   ci = split_col(p, c);
 }
 
-__device__ __forceinline__ float epi_act(float v, int act) {
-  if (act == MAPA_ACT_GELU) return gelu_erf(v);
-  if (act == MAPA_ACT_RELU) return fmaxf(v, 0.f);
-  return v;  // NONE, GELU_POST (applied after the residuals)
-}
-
 // Per-thread column state of the epilogue: 4 consecutive output columns n0..n0+3.
 struct EpiCol {
   int n0;
@@ -138,7 +132,19 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
   const int64_t off3 = orow * 2 * ld + c.col_off;  // split-operand rows are stored [hi | lo], 2*ld wide
   f32x4 v;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = epi_act(a[e] + c.bv[e], p.act) * c.gv[e];
+  for (int e = 0; e < 4; ++e) v[e] = a[e] + c.bv[e];
+  // activation and gamma once per call (uniform branches), not per element
+  if (p.act == MAPA_ACT_GELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = gelu_erf(v[e]);
+  } else if (p.act == MAPA_ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  }
+  if (p.gamma) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= c.gv[e];
+  }
   if (c.vec) {
     if (p.resid1) v += *reinterpret_cast<const f32x4*>(p.resid1 + off);
     if (p.resid2) v += *reinterpret_cast<const f32x4*>(p.resid2 + off);
@@ -224,8 +230,29 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
   f32x4 v0, v1;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    v0[e] = epi_act(lo[e] + c.a.bv[e], p.act) * c.a.gv[e];
-    v1[e] = epi_act(hi[e] + c.b.bv[e], p.act) * c.b.gv[e];
+    v0[e] = lo[e] + c.a.bv[e];
+    v1[e] = hi[e] + c.b.bv[e];
+  }
+  // activation and gamma once per call (uniform branches), not per element
+  if (p.act == MAPA_ACT_GELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = gelu_erf(v0[e]);
+      v1[e] = gelu_erf(v1[e]);
+    }
+  } else if (p.act == MAPA_ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] = fmaxf(v0[e], 0.f);
+      v1[e] = fmaxf(v1[e], 0.f);
+    }
+  }
+  if (p.gamma) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v0[e] *= c.a.gv[e];
+      v1[e] *= c.b.gv[e];
+    }
   }
   if (p.resid1) {
     v0 += *reinterpret_cast<const f32x4*>(p.resid1 + off);
