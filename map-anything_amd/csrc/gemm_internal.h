@@ -304,6 +304,56 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
   }
 }
 
+// Epilogue patterns of the transformer blocks, fixed once per tile so the per-row calls carry no output-set checks:
+// 1 = act(acc + bias) -> bf16 out_lp only (qkv, fc1 + GELU); 2 = resid1 + gamma * (acc + bias) -> out_f32 only, in
+// place (attn proj, fc2); 0 = anything else (epi_store_row8).
+__device__ __forceinline__ int epi_mode(const GemmArgs& p) {
+  const bool lp_outs = p.out_lp_relu || p.out_s3 || p.out_s3_relu;
+  if (p.out_mode != 0 || p.resid2 || lp_outs || p.ldo % 8 != 0 || !p.vec_ok) return 0;
+  if (p.out_lp && !p.out_f32 && !p.resid1 && !p.gamma && (p.act == MAPA_ACT_NONE || p.act == MAPA_ACT_GELU)) return 1;
+  if (p.out_f32 && !p.out_lp && p.resid1 && p.act == MAPA_ACT_NONE) return 2;
+  return 0;
+}
+
+template <int MODE>
+__device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const EpiCol8& c, int m, f32x4 lo, f32x4 hi) {
+  if (MODE == 0 || !c.vec8) {
+    epi_store_row8<bf16_t>(p, c, m, lo, hi);
+    return;
+  }
+  const int64_t off = (int64_t)m * p.ldo + c.a.n0;
+  f32x4 v0, v1;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v0[e] = lo[e] + c.a.bv[e];
+    v1[e] = hi[e] + c.b.bv[e];
+  }
+  if constexpr (MODE == 1) {
+    if (p.act == MAPA_ACT_GELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] = gelu_erf(v0[e]);
+        v1[e] = gelu_erf(v1[e]);
+      }
+    }
+    const uint4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                     pack_bf16x2(v1[2], v1[3])};
+    *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
+  } else {
+    if (p.gamma) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v0[e] *= c.a.gv[e];
+        v1[e] *= c.b.gv[e];
+      }
+    }
+    v0 += *reinterpret_cast<const f32x4*>(p.resid1 + off);
+    v1 += *reinterpret_cast<const f32x4*>(p.resid1 + off + 4);
+    *reinterpret_cast<f32x4*>(p.out_f32 + off) = v0;
+    *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = v1;
+  }
+}
+
 // 256-row bf16 kernel (gemm_big.hip): variant 0 = 256x256 tile, 1 = 256x128 tile.  Returns false if it does not
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
