@@ -5,6 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/shape
 mkdir -p $O
+export KB_NO_RESID=1  # plain bias + bf16-out epilogues, as hipBLASLt's linear (like-for-like columns)
 timeout -k 10 300 python -u tools/kbench.py gemm 20 torch > $O/kb_gemm.log 2>&1 || { tail -5 $O/kb_gemm.log; exit 1; }
 KB_KBLOCK=32 KB_HEADS=1 timeout -k 10 300 python -u tools/kbench.py conv 10 > $O/kb_conv.log 2>&1 || { tail -5 $O/kb_conv.log; exit 1; }
 for what in gemm conv; do
