@@ -27,6 +27,8 @@ typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
 enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2 };
 enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
 enum { MAPA_OUT_ROWMAJOR = 0, MAPA_OUT_PIXSHUF = 1 };
+/* GELU is the exact-erf form (nn.GELU()), erf evaluated branch-free to within 5e-7 absolute (Abramowitz & Stegun
+ * 7.1.26 in fp32; the GELU output within 3.5e-7 absolute). */
 enum { MAPA_ACT_NONE = 0, MAPA_ACT_GELU = 1, MAPA_ACT_RELU = 2, MAPA_ACT_GELU_POST = 3 };
 
 const char* mapa_last_error(void);
