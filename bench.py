@@ -3,7 +3,11 @@
   python bench.py                        # N=1: configs[1] = 8 views 518x518 bf16 image-only infer on 1 GPU
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
       bench.py --gpus N                  # 8 views per GPU (weak scaling), global-attention K/V all-gathered
+  python bench.py --gpus N               # the same: without WORLD_SIZE in the environment and N > 1 this process
+                                         # (which never touches the GPU) starts that torch.distributed.run itself
+                                         # and exits with its status; rank 0's JSON line is the output
   ... bench.py --gpus N --total-views 100  # configs[2]: a fixed 100-view job split over the N ranks (strong)
+  python bench.py --gpus 2 --dry-run     # launcher rehearsal on CPU: gloo ranks, no GPU, a placeholder step
 
 One step = one full `MapAnything.infer(views)` (validation, forward, post-processing with edge masks) over
 synthetic images with inputs already resident in HBM, in the reference's own precision recipe (bf16 encoder and
@@ -68,20 +72,34 @@ def main():
                     help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh); default: "
                          "profiles/r2/attn_global_pmc.json (8 views) or attn_global_v100_pmc.json (>= 100 views)")
     ap.add_argument("--lib", default=None, help="A/B only: load this libmapa.so build (tools/ab_build.sh)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher rehearsal without a GPU: gloo process group, placeholder CPU step (tests only)")
+    ap.add_argument("--fail-rank", type=int, default=-1, help="dry-run only: this rank exits with an error")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    if args.dry_run:
+        return dry_run(args, world, rank)
     if args.lib:
         from mapanything import _native
 
         _native.load_library(args.lib)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    observed_world = 1
     if world > 1:
         import torch.distributed as dist
 
+        from mapanything.parallel import init_distributed
+
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        _, observed_world = init_distributed("nccl", torch.device("cuda", local_rank))
+        assert observed_world == args.gpus, (observed_world, args.gpus)
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -234,7 +252,8 @@ def main():
             if H == 518 else None
         line = {
             "metric": "views/sec + ms/infer, N-view 518x518 bf16 at 1/2/4/8 MI355X",
-            "value": value, "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "value": value, "unit": "views/s", "n_gpus": world, "world_size_observed": observed_world,
+            "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "strong" if args.total_views else "weak",
             "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
@@ -263,6 +282,78 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
+        dist.destroy_process_group()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run (one process per GPU, env://
+    rendezvous on 127.0.0.1) as CHILD processes — this process never initialises the GPU — relay their output, and
+    return a non-zero status if any rank fails (torch.distributed.run stops the others then)."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", env.get("OMP_NUM_THREADS", "16"))
+    rc = subprocess.call(cmd, env=env)
+    if rc != 0:
+        print(f"bench.py: {n}-rank job failed with status {rc}", file=sys.stderr, flush=True)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """The multi-rank control path of the bench (launcher, rendezvous, timed barrier + max-over-ranks, rank-0 JSON
+    line) over gloo with a placeholder CPU step, for the CPU test-suite (tests/test_bench_launcher.py)."""
+    import torch.distributed as dist
+
+    from mapanything.parallel import CommError, DistComm, init_distributed
+
+    observed = 1
+    if world > 1:
+        _, observed = init_distributed("gloo")
+    if rank == args.fail_rank:
+        raise SystemExit(f"rank {rank}: injected failure (--fail-rank)")
+    comm = DistComm() if world > 1 else None
+    x = torch.ones(64, 64)
+
+    def step():
+        y = x @ x
+        if comm is not None:
+            t = torch.zeros(world * 4, 4)
+            t[rank * 4:(rank + 1) * 4] = y[:4, :4]
+            comm.allgather_slots(t, 4)
+        return y
+
+    try:
+        for _ in range(args.warmup):
+            step()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        if world > 1:
+            dist.barrier()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+    except CommError as e:
+        raise SystemExit(f"rank {rank}: {e}")
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher rehearsal, no GPU)", "value": args.steps / dt, "unit": "steps/s",
+                          "n_gpus": world, "world_size_observed": observed, "steps": args.steps,
+                          "warmup": args.warmup, "dry_run": True}), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 

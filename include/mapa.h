@@ -35,6 +35,10 @@ const char* mapa_last_error(void);
 int mapa_version(void);
 /* 1 if a gfx950 device is visible and the code object loads on it, else 0 (message in mapa_last_error). */
 int mapa_device_check(int device);
+/* Debug / serialize mode: synchronise `stream` and report any device error as the failure of `what` (0 = ok).
+ * The Python binding calls it after every launch when MAPA_SERIALIZE=1 (or AMD_SERIALIZE_KERNEL /
+ * HIP_LAUNCH_BLOCKING is set) — SURVEY.md §5's race-detection / serialize row; no reference counterpart. */
+int mapa_stream_check(mapa_stream_t stream, const char* what);
 
 /* ---------------------------------------------------------------------------------------------------------
  * GEMM / implicit-GEMM convolution: C[M,N] = A[M,K] * W[N,K]^T, fused epilogue
@@ -97,10 +101,10 @@ int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
 int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
 /* Tuning / test hook: force one kernel variant for every later mapa_gemm call (0 = automatic per-shape choice,
  * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
- * 2560..2574 = 256-row tiles, 2575..2578 = phase-interleaved 256x256 tiles (2579 / 2583 timing diagnostics),
- * 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one the automatic choice runs),
- * 2584..2586 = LDS halo-window conv, 2587 = 192x192 tiles, 2590/2591 = four-wave 256x256 / 192x256 tiles,
- * 2592/2593 = four-wave inline-asm MFMA tiles. */
+ * 2560..2574 = 256-row tiles, 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one
+ * the automatic choice runs), 2584..2586 / 2588 = LDS halo-window conv, 2587 = 192x192 tiles.  (The round-2 opt-in
+ * main-loop experiments — phase-interleaved and four-wave tiles — measured slower on every path shape and were
+ * removed from the library) */
 int mapa_gemm_set_variant(int variant);
 /* The regressor tail in one launch (DPTRegressionProcessor conv2 + the dense head, dpt.py:285-311 and model.py:
  * 1865-2150): d describes the 3x3 conv 128 -> 128 (bf16, stride 1, conv_kblock 32, act MAPA_ACT_RELU, bias; no

@@ -37,3 +37,14 @@ extern "C" int mapa_device_check(int device) {
   }
   return 1;
 }
+
+// Debug / serialize mode (MAPA_SERIALIZE=1, or AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING set): the binding calls
+// this after every launch, so a faulting or failing kernel is reported by the launch that caused it instead of by
+// whatever synchronises next.
+extern "C" int mapa_stream_check(hipStream_t stream, const char* what) {
+  hipError_t e = hipStreamSynchronize(stream);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) return mapa_set_error("%s: device error after launch: %s", what ? what : "launch",
+                                             hipGetErrorString(e));
+  return 0;
+}

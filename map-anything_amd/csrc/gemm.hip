@@ -435,15 +435,6 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
                               : launch_conv_halo(a, a.N % 256 == 0 && g_halo == 1 ? 256 : 128, stream,
                                                  a.N % 256 == 0 && g_halo == 1 ? 8 : 16))) {
     // launched (LDS halo-window conv)
-  } else if (d->dtype == MAPA_BF16 && ((variant >= 2575 && variant <= 2579) || variant == 2583) &&
-             launch_gemm_8p(a, conv, variant == 2583 ? 5 : variant - 2575, stream)) {
-    // launched
-  } else if (d->dtype == MAPA_BF16 && (variant == 2592 || variant == 2593) &&
-             launch_gemm_w4a(a, conv, variant - 2592, stream)) {
-    // launched
-  } else if (d->dtype == MAPA_BF16 && (variant == 2590 || variant == 2591) &&
-             launch_gemm_w4(a, conv, variant - 2590, stream)) {
-    // launched
   } else if (d->dtype == MAPA_BF16 && ((variant >= 2560 && variant <= 2574) || variant == 2587) &&
              launch_gemm_big(a, conv, variant == 2587 ? 15 : variant - 2560, stream)) {
     // launched
@@ -485,8 +476,8 @@ extern "C" int mapa_gemm_tune(int key, int value) {
 
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
-                     (variant >= 2560 && variant <= 2579) || (variant >= 2580 && variant <= 2588) ||
-                     variant == 2590 || variant == 2591 || variant == 2592 || variant == 2593,
+                     (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582) ||
+                     (variant >= 2584 && variant <= 2588),
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;

@@ -358,9 +358,6 @@ __device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const Epi
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
 
-// 256x256 bf16 kernel with the phase-interleaved (ping-pong, half-tile ring) main loop (gemm_8p.hip).
-bool launch_gemm_8p(const GemmArgs& a, bool conv, int diag, hipStream_t stream);
-
 // Stride-1 3x3 conv with its A operand read from an LDS halo window (conv_halo.hip); bn = 256 / 128 / 0 (auto).
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).
 bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh = 16);
@@ -370,14 +367,6 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh = 16
 bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b6, const float* pose,
                               const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
                               float* conf, float* logits, uint8_t* mask, hipStream_t stream);
-
-// Four-wave bf16 kernel with inline-asm MFMAs on AGPR accumulators and an explicitly ordered main loop
-// (gemm_w4a.hip): variant 0 = 256x256, 1 = 192x256; dense A with K % 32 == 0.  false if it does not take the shape.
-bool launch_gemm_w4a(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
-
-// Four-wave 256-column bf16 kernel (gemm_w4.hip): variant 0 = 256x256 tile, 1 = 192x256 tile; 1 workgroup/CU.
-bool launch_gemm_w4(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
-
 // Stream-K bf16 kernel (gemm_big.hip): variant 0 = 256x128 tiles, 2 workgroups per CU; 1 = 256x256, 1 per CU.
 // streamk_workspace_bytes: bytes the launch needs (ticket words + partial-sum slabs); launch returns false if
 // the workspace is missing or too small.

@@ -83,23 +83,38 @@ __device__ __forceinline__ void store_split1(bf16_t* p, int64_t ld, float x) {
   p[ld] = f32_to_bf16(x - bf16_to_f32(h));
 }
 
-// erf for the GELU epilogues: Abramowitz & Stegun 7.1.26 (|error| <= 5e-7 absolute evaluated in fp32; GELU output
-// within 3.5e-7 absolute, far below its bf16 rounding) — 11 instructions, one rcp and one
-// exp2, branch-free; the device libm erff costs ~36 with a divergent two-path branch, and the fc1 GEMMs evaluate
-// it on every one of their 1.9 G outputs per 8-view step.
-__device__ __forceinline__ float erf_as(float x) {
-  const float a = fabsf(x);
-  const float t = __builtin_amdgcn_rcpf(__builtin_fmaf(0.3275911f, a, 1.0f));
-  float p = __builtin_fmaf(1.061405429f, t, -1.453152027f);
-  p = __builtin_fmaf(p, t, 1.421413741f);
-  p = __builtin_fmaf(p, t, -0.284496736f);
-  p = __builtin_fmaf(p, t, 0.254829592f);
-  p *= t;
-  const float e = __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
-  return copysignf(__builtin_fmaf(-p, e, 1.0f), x);
+// erf for the GELU epilogues, faithful to fp32 erff (≤ 1.2 ulp over the whole range, tools/erf_check.py; the
+// reference's GELU is exact-erf, dinov2 layers/mlp.py:29-39 / nn.GELU): two minimax pieces evaluated branch-free
+// and selected per lane —
+//   |x| ≤ 0.9277:  erf = x + x·s·P(s), s = x²  (odd polynomial, degree 13)
+//   |x| > 0.9277:  erf = sign(x)·(1 − exp(R(|x|))), R a degree-9 polynomial fit of log(erfc)
+// (coefficients: the well-known single-precision erff minimax pair).  One exp2 and 14 FMAs; the device libm erff is
+// ~36 instructions with a divergent two-path branch, and the fc1 GEMMs evaluate it on 1.9 G outputs per 8-view step.
+// Round 2 used Abramowitz & Stegun 7.1.26 (5e-7 absolute, large relative error in GELU's negative tail); that moved a
+// scalar bf16 output measurably, so the epilogue is held to erff accuracy.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float t = fabsf(x);
+  const float s = x * x;
+  // large |x|: 1 - exp(R(t))
+  float r = __builtin_fmaf(-1.72853470e-5f, t, 3.83197126e-4f);
+  const float u = __builtin_fmaf(-3.88396438e-3f, t, 2.42546219e-2f);
+  r = __builtin_fmaf(r, s, u);
+  r = __builtin_fmaf(r, t, -1.06777877e-1f);
+  r = __builtin_fmaf(r, t, -6.34846687e-1f);
+  r = __builtin_fmaf(r, t, -1.28717512e-1f);
+  r = __builtin_fmaf(r, t, -t);
+  const float big = copysignf(1.0f - __builtin_amdgcn_exp2f(r * 1.4426950408889634f), x);
+  // small |x|: x + x * P(s)
+  float q = __builtin_fmaf(-5.96761703e-4f, s, 4.99119423e-3f);
+  q = __builtin_fmaf(q, s, -2.67681349e-2f);
+  q = __builtin_fmaf(q, s, 1.12819925e-1f);
+  q = __builtin_fmaf(q, s, -3.76125336e-1f);
+  q = __builtin_fmaf(q, s, 1.28379166e-1f);
+  q = __builtin_fmaf(q, x, x);
+  return t > 0.927734375f ? big : q;
 }
 __device__ __forceinline__ float gelu_erf(float x) {
-  return 0.5f * x * (1.0f + erf_as(x * 0.70710678118654752f));
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
 
 template <typename T>

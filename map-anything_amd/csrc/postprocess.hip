@@ -42,10 +42,17 @@ __device__ __forceinline__ float norm3(const float a[3]) {
 // K1: points_to_normals(point, mask) -> normal (H,W,3) and normal_mask (H,W).  Stored already renormalised
 // (n / (|n| + 1e-12), normals_edge's first step, geometry.py:2216): K2 reads every normal 9 times, and the same
 // float operations applied once per pixel give the same bits.  32-bit pixel indices (the host checks n*H*W).
+// Grid-stride step in 64-bit, clamped to `total`: a 32-bit `e += stride` overflows when total is within one grid of
+// 2^31; the index stays 32-bit inside the loop bodies.
+__device__ __forceinline__ int grid_next(int e, int total) {
+  const int64_t n = (int64_t)e + (int64_t)gridDim.x * blockDim.x;
+  return n < total ? (int)n : total;
+}
+
 __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __restrict__ mask, int n, int H, int W,
                                float* __restrict__ nrm, uint8_t* __restrict__ nmask) {
   const int total = n * H * W, HW = H * W;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e = grid_next(e, total)) {
     const int im = e / HW;
     const int rem = e - im * HW;
     const int y = rem / W, x = rem - y * W;
@@ -100,7 +107,7 @@ __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __r
 __global__ void normal_state_kernel(const float* __restrict__ nrm, const uint8_t* __restrict__ nmask, int n, int H,
                                     int W, float cos_thr, uint8_t* __restrict__ state) {
   const int total = n * H * W, HW = H * W;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e = grid_next(e, total)) {
     const int im = e / HW;
     const int rem = e - im * HW;
     const int y = rem / W, x = rem - y * W;
@@ -134,7 +141,7 @@ __global__ void mask_combine_kernel(const uint8_t* __restrict__ state, const flo
                                     int64_t dz_stride, const uint8_t* __restrict__ m_in, int n, int H, int W,
                                     float rtol, int use_edges, uint8_t* __restrict__ m_out) {
   const int total = n * H * W, HW = H * W;
-  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e = grid_next(e, total)) {
     const bool mc = m_in[e] != 0;
     bool keep = mc;
     if (use_edges && mc) {

@@ -81,6 +81,9 @@ extern "C" int mapa_rope2d(void* tokens, int dtype, int B, int H, int N, int D, 
   MAPA_CHECK_ARG(D > 0 && D % 16 == 0 && D <= 256, "mapa_rope2d: head dim %d must be a multiple of 16, <= 256", D);
   MAPA_CHECK_ARG(dtype == MAPA_F32 || dtype == MAPA_BF16, "mapa_rope2d: dtype must be f32 or bf16");
   MAPA_CHECK_ARG(sb % 4 == 0 && sh % 4 == 0 && sn % 4 == 0, "mapa_rope2d: strides must keep 4-element alignment");
+  // the kernel moves 4 elements per vector access (16 B fp32 / 8 B bf16): the base must be aligned to that too
+  MAPA_CHECK_ARG(((uintptr_t)tokens % (dtype == MAPA_BF16 ? 8 : 16)) == 0,
+                 "mapa_rope2d: tokens base pointer must be %d-byte aligned", dtype == MAPA_BF16 ? 8 : 16);
   const int64_t total = (int64_t)B * N * H * 2 * (D / 16);
   const dim3 g(grid_for(total)), b(TPB);
   if (dtype == MAPA_BF16)

@@ -30,7 +30,7 @@ EXPORTED = (
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
     "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_tune",
-    "mapa_regressor_head_out",
+    "mapa_regressor_head_out", "mapa_stream_check",
 )
 
 
@@ -123,6 +123,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_dense_adaptor.argtypes = [vp, i, i64, vp, vp, vp, vp, vp]
     L.mapa_normalize_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
     L.mapa_rope2d.argtypes = [vp, i, i, i, i, i, i64, i64, i64, vp, f, f, vp]
+    L.mapa_stream_check.argtypes = [vp, ctypes.c_char_p]
     _lib = L
     return L
 
@@ -140,9 +141,30 @@ def lib():
     return L
 
 
+def _serialize_from_env() -> bool:
+    """Debug / serialize mode: MAPA_SERIALIZE=1, or the HIP runtime's own switches (AMD_SERIALIZE_KERNEL >= 1,
+    HIP_LAUNCH_BLOCKING=1) — every launch is followed by a stream synchronise + device-error check."""
+    if os.environ.get("MAPA_SERIALIZE", "0") not in ("", "0"):
+        return True
+    if os.environ.get("AMD_SERIALIZE_KERNEL", "0") not in ("", "0"):
+        return True
+    return os.environ.get("HIP_LAUNCH_BLOCKING", "0") not in ("", "0")
+
+
+SERIALIZE = _serialize_from_env()
+
+
+def set_serialize(on: bool):
+    global SERIALIZE
+    SERIALIZE = bool(on)
+
+
 def check(rc: int, what: str):
     if rc != 0:
         raise NativeError(f"{what}: {_lib.mapa_last_error().decode()}")
+    if SERIALIZE and not torch.cuda.is_current_stream_capturing():
+        if _lib.mapa_stream_check(stream(), what.encode()) != 0:
+            raise NativeError(_lib.mapa_last_error().decode())
 
 
 def ptr(t: Optional[torch.Tensor]):

@@ -912,13 +912,23 @@ class MapaEngine:
                 raise AssertionError("shard plan does not match the local views")
             if self.info.nonref_pe and pe_idx is None:
                 raise ValueError("this info-sharing variant encodes every view's index: pass pe_idx")
+            # DPT inputs (model.py:1724-1768): [encoder, tap0, tap1, final] or, with three taps, [tap0..2, final].
+            # The fused encoder features enter the heads as a head operand (fp32 in the reference's heads); they are
+            # split BEFORE the transformer when it has no input projection, because aat() then runs its residual
+            # stream in place in fused_f32
+            first = None
+            if len(self.info.indices) != 3:
+                if not self.hsplit:
+                    first = fused_lp
+                elif self.w.pe_proj is None:
+                    first = self.head_rows(fused_f32[:VB * T])
             inter, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx,
                                           fused_f32=fused_f32)
-            # DPT inputs (model.py:1724-1768): [encoder, tap0, tap1, final] or, with three taps, [tap0..2, final]
             if len(inter) == 3:
                 first, l11, l17 = inter
-            else:  # the fused encoder features, as a head operand (fp32 in the reference's heads)
-                first = self.head_rows(fused_f32[:VB * T]) if self.hsplit else fused_lp
+            else:
+                if first is None:
+                    first = self.head_rows(fused_f32[:VB * T])
                 l11, l17 = inter
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)

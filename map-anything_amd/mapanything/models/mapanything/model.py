@@ -12,7 +12,10 @@ Differences that are by design:
     geometric encoders and the downstream heads fp32-exact as the reference runs them with autocast disabled
     (model.py:1377, 1774; split-precision bf16 GEMMs on MI355X); `use_amp=False` (or precision="fp32") runs the
     exact-fp32 MFMA path; `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
-  * multi-view batches are processed B = 1 per view (the reference's configs all use B = 1).
+  * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687) run scene by scene through the engine
+    (every stage of the path is per scene: global attention, the scale token and scale head, the camera
+    normalisation across views), and the per-view outputs are concatenated on the batch dimension as the reference
+    returns them.
 """
 
 from __future__ import annotations
@@ -305,8 +308,42 @@ class MapAnything:
             if "img" not in v:
                 # the reference's _encode_n_views (model.py:700) indexes views[i]["img"] for every view
                 raise KeyError(f"view {i}: 'img'")
-            if v["img"].shape[0] != 1:
-                raise NotImplementedError("batch size per view must be 1")
+        B = views[0]["img"].shape[0]
+        if any(v["img"].shape[0] != B for v in views):
+            raise ValueError("every view must carry the same batch size (batch_size_per_view, model.py:687)")
+        return B
+
+    @staticmethod
+    def _scene_views(views, b: int, B: int):
+        """Scene b of a batch of B scenes: every per-sample entry of every view sliced to [b:b+1] (tensors and
+        tuples of tensors with a leading B, lists of B entries); other entries are shared."""
+        out = []
+        for v in views:
+            d = {}
+            for k, x in v.items():
+                if isinstance(x, torch.Tensor) and x.dim() >= 1 and x.shape[0] == B:
+                    d[k] = x[b:b + 1]
+                elif (isinstance(x, tuple) and x and all(isinstance(t, torch.Tensor) and t.dim() >= 1
+                                                         and t.shape[0] == B for t in x)):
+                    d[k] = tuple(t[b:b + 1] for t in x)
+                elif isinstance(x, list) and len(x) == B:
+                    d[k] = x[b:b + 1]
+                else:
+                    d[k] = x
+            out.append(d)
+        return out
+
+    @staticmethod
+    def _merge_scenes(per_scene):
+        """[scene][view] output dicts -> [view] dicts with every entry concatenated over the scenes (dim 0), the
+        reference's (B, ...) per-view outputs (model.py:1865-1923, 2266-2282)."""
+        merged = []
+        for i in range(len(per_scene[0])):
+            if per_scene[0][i] is None:  # a view owned by another rank (view sharding)
+                merged.append(None)
+                continue
+            merged.append({k: torch.cat([sc[i][k] for sc in per_scene], 0) for k in per_scene[0][i]})
+        return merged
 
     @staticmethod
     def _metric_flags(views) -> List[bool]:
@@ -357,7 +394,10 @@ class MapAnything:
         cam_trans, cam_quats, metric_scaling_factor, conf, non_ambiguous_mask, non_ambiguous_mask_logits).
         Views are in the preprocessed form (ray_directions_cam, depth_along_ray, camera_pose_quats/trans,
         is_metric_scale); every provided geometric input is used (infer()'s deterministic masks)."""
-        self._check_views(views)
+        B = self._check_views(views)
+        if B > 1:
+            return self._merge_scenes([self.forward(self._scene_views(views, b, B), memory_efficient_inference,
+                                                    precision) for b in range(B)])
         dnt = views[0].get("data_norm_type", ["dinov2"])
         if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
@@ -440,7 +480,16 @@ class MapAnything:
         else:
             precision = "fp32"
         validated = validate_input_views_for_inference(views)
-        self._check_views(validated)
+        B = self._check_views(validated)
+        if B > 1:  # scene by scene (module docstring), outputs concatenated per view as the reference returns them
+            kw = dict(memory_efficient_inference=memory_efficient_inference, use_amp=use_amp, amp_dtype=amp_dtype,
+                      apply_mask=apply_mask, mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
+                      edge_depth_threshold=edge_depth_threshold, apply_confidence_mask=apply_confidence_mask,
+                      confidence_percentile=confidence_percentile, ignore_calibration_inputs=ignore_calibration_inputs,
+                      ignore_depth_inputs=ignore_depth_inputs, ignore_pose_inputs=ignore_pose_inputs,
+                      ignore_depth_scale_inputs=ignore_depth_scale_inputs,
+                      ignore_pose_scale_inputs=ignore_pose_scale_inputs)
+            return self._merge_scenes([self.infer(self._scene_views(validated, b, B), **kw) for b in range(B)])
         metric = self._metric_flags(validated)   # host-side flags read before the H2D copies
         for v in validated:
             for k in list(v.keys()):

@@ -17,11 +17,51 @@ the attention kernel reads the valid rows through its K/V segment table, so no c
 
 from __future__ import annotations
 
+import datetime
+import os
 import threading
 from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
 import torch
+
+
+class CommError(RuntimeError):
+    """A collective of the view-sharded path failed or timed out (dead peer, RCCL / gloo error).  Raised instead of
+    hanging; the process is expected to exit non-zero (bench.py does)."""
+
+
+def comm_timeout() -> datetime.timedelta:
+    """Timeout for communicator init and for every collective: MAPA_COMM_TIMEOUT_S seconds (default 300)."""
+    return datetime.timedelta(seconds=float(os.environ.get("MAPA_COMM_TIMEOUT_S", "300")))
+
+
+def init_distributed(backend: str = "nccl", device: Optional[torch.device] = None):
+    """One process per GPU, env:// rendezvous (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, as torchrun sets them;
+    the reference's own setup is mapanything/utils/train_tools.py:389-402).  Differences that matter for a serving
+    job: the process group gets an explicit timeout (comm_timeout()), RCCL's watchdog tears the process down when a
+    collective exceeds it (TORCH_NCCL_ASYNC_ERROR_HANDLING=1 unless set), and a first all-reduce proves that every
+    peer is up — a rank that cannot reach the others raises CommError within the timeout instead of hanging.
+    Returns (rank, world)."""
+    import torch.distributed as dist
+
+    timeout = comm_timeout()
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    try:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device, timeout=timeout)
+        else:
+            dist.init_process_group(backend, timeout=timeout)
+        probe = torch.ones(1, device=device if backend == "nccl" else "cpu")
+        dist.all_reduce(probe)
+        if backend == "nccl":
+            torch.cuda.synchronize(device)
+    except Exception as e:  # noqa: BLE001 — every init failure becomes one error type
+        raise CommError(f"communicator init ({backend}) failed: {e}") from e
+    world = dist.get_world_size()
+    if int(probe.item()) != world:
+        raise CommError(f"communicator init: probe all-reduce saw {int(probe.item())} of {world} ranks")
+    return dist.get_rank(), world
 
 
 @dataclass
@@ -76,20 +116,38 @@ class DistComm:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
 
+    def _call(self, what, fn, *a, **k):
+        """Run one collective; a backend error (gloo raises on a dead peer / timeout, RCCL's watchdog on a timed-out
+        collective) becomes CommError naming the collective and this rank."""
+        try:
+            return fn(*a, **k)
+        except CommError:
+            raise
+        except RuntimeError as e:
+            raise CommError(f"{what} failed on rank {self.rank} of {self.world}: {e}") from e
+
     def allgather_slots(self, full: torch.Tensor, rows_per_slot: int):
         """full: [world * rows_per_slot, C]; this rank's slot already written in place."""
         mine = full.narrow(0, self.rank * rows_per_slot, rows_per_slot)
-        self.dist.all_gather_into_tensor(full, mine, group=self.group)
+        self._call("K/V all-gather", self.dist.all_gather_into_tensor, full, mine, group=self.group)
 
     def allgather_slots_async(self, full: torch.Tensor, rows_per_slot: int):
         """Start the slot all-gather on the communicator's stream (it waits for the current stream's K/V
         projection); the returned handle's wait() makes the current stream wait for the gathered slots."""
         mine = full.narrow(0, self.rank * rows_per_slot, rows_per_slot)
-        return self.dist.all_gather_into_tensor(full, mine, group=self.group, async_op=True)
+        work = self._call("K/V all-gather", self.dist.all_gather_into_tensor, full, mine, group=self.group,
+                          async_op=True)
+        comm = self
+
+        class _Handle:
+            def wait(self_inner):
+                comm._call("K/V all-gather (wait)", work.wait)
+
+        return _Handle()
 
     def broadcast_(self, t: torch.Tensor, src: int = 0):
         """In place: every rank's t = rank src's t."""
-        self.dist.broadcast(t, src, group=self.group)
+        self._call("scale-token broadcast", self.dist.broadcast, t, src, group=self.group)
 
     def gather_views(self, local: torch.Tensor, counts: List[int], dst: Optional[int]) -> Optional[torch.Tensor]:
         """View-major local rows [counts[rank], ...] -> [sum(counts), ...] in rank order on rank dst (None: on
@@ -102,10 +160,10 @@ class DistComm:
         slot[:local.shape[0]].copy_(local)
         if dst is None:
             full = torch.empty((self.world * mx,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-            self.dist.all_gather_into_tensor(full, slot, group=self.group)
+            self._call("output all-gather", self.dist.all_gather_into_tensor, full, slot, group=self.group)
         else:
             lst = [torch.empty_like(slot) for _ in range(self.world)] if self.rank == dst else None
-            self.dist.gather(slot, lst, dst=dst, group=self.group)
+            self._call("output gather", self.dist.gather, slot, lst, dst=dst, group=self.group)
             if self.rank != dst:
                 return None
             full = torch.cat(lst, 0)

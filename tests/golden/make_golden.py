@@ -13,8 +13,10 @@ Cases:
   v2_518     2 views 518x518 image-only, fp32 (outputs subsampled [::7, ::7] + taps subsampled)
   mm_224     2 views 224x224 + intrinsics + 90 %-sparse depth_z + is_metric_scale (full outputs + taps)
   cfg2_518   configs[1] itself: 8 views 518x518 image-only, the bench's input seed (outputs [::7, ::7], taps strided)
-  cfg4_518   configs[3] itself: 32 views 518x518 + intrinsics + 90 %-sparse depth_z + is_metric_scale (fp32 only:
-             the CPU bf16 emulation at this size is too slow; the GPU test uses cfg2's bf16 yardstick)
+  cfg4_518   configs[3] itself: 32 views 518x518 + intrinsics + 90 %-sparse depth_z + is_metric_scale (its bf16
+             yardstick and spread come from make_yardstick_spread.py)
+  b2_224     3 views 224x224 with TWO scenes per view (batch_size_per_view = 2, model.py:687): intrinsics, depth on
+             views 0/2, poses on views 0/1, per-scene metric flags
   cfg1_224 under the reference's own bf16 autocast recipe, emulated on CPU (device "cuda" -> "cpu"):
              rel-L2 of bf16 vs fp32 per output key = the bf16 yardstick (golden_bf16_yardstick.json)
 Info-sharing variants (the reference built with a modified info_sharing_config):
@@ -96,26 +98,26 @@ VARIANTS = {
 
 def make_views(case):
     n, h, w, seed = case["views"], case["h"], case["w"], case["seed"]
-    imgs = synthetic.synthetic_images(n, h, w, seed)
+    B = case.get("batch", 1)  # scenes per view (batch_size_per_view, reference model.py:687)
+    imgs = synthetic.synthetic_images(n, h, w, seed, batch=B)
     views = []
     for v in range(n):
         view = {"img": torch.from_numpy(imgs[v]), "data_norm_type": ["dinov2"]}
         if case.get("multimodal"):
-            K = synthetic.synthetic_intrinsics(n, h, w, seed)[v]
-            d = synthetic.synthetic_sparse_depth(n, h, w, seed)[v]
-            view["intrinsics"] = torch.from_numpy(K)
-            view["depth_z"] = torch.from_numpy(d)
-            view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed, batch=B)[v])
+            view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed, batch=B)[v])
+            view["is_metric_scale"] = torch.ones(B, dtype=torch.bool)
         if case.get("rays_only"):
-            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed, batch=B)[v])
         if case.get("mixed"):
-            # 3 views: intrinsics everywhere, depth on views 0 and 2, poses on views 0 and 1, view 2 not metric
-            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
+            # 3 views: intrinsics everywhere, depth on views 0 and 2, poses on views 0 and 1; scene 0: view 2 not
+            # metric, further scenes: only view 0 metric
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed, batch=B)[v])
             if v in (0, 2):
-                view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
+                view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed, batch=B)[v])
             if v in (0, 1):
-                view["camera_poses"] = torch.from_numpy(synthetic.synthetic_poses(n, seed)[v])
-            view["is_metric_scale"] = torch.tensor([v != 2])
+                view["camera_poses"] = torch.from_numpy(synthetic.synthetic_poses(n, seed, batch=B)[v])
+            view["is_metric_scale"] = torch.tensor([(v != 2) if b == 0 else (v == 0) for b in range(B)])
         views.append(view)
     return views
 
@@ -229,7 +231,7 @@ def shrink(d, out_step, tap_step, dpt_step):
 
 
 STEPS = {"cfg1_224": (1, 2, 8), "v2_518": (7, 6, 24), "cfg2_518": (7, 6, 24), "cfg4_518": (14, 12, 48), "mm_224": (2, 4, 8), "mixed_224": (2, 4, 8),
-         "ns_280x392": (4, 2, 8), "one_224": (2, 2, 8), "gat_224": (4, 2, 8), "aatpe_224": (4, 2, 8),
+         "ns_280x392": (4, 2, 8), "one_224": (2, 2, 8), "b2_224": (2, 4, 8), "gat_224": (4, 2, 8), "aatpe_224": (4, 2, 8),
          "aatnoref_224": (4, 2, 8), "aat48_224": (4, 2, 8)}
 
 
@@ -260,6 +262,7 @@ def main():
         "one_224": dict(views=1, h=224, w=224, seed=7, rays_only=True),
         "cfg2_518": dict(views=8, h=518, w=518, seed=2),
         "cfg4_518": dict(views=32, h=518, w=518, seed=4, multimodal=True),
+        "b2_224": dict(views=3, h=224, w=224, seed=12, mixed=True, batch=2),
     }
     no_bf16 = ("cfg4_518",)
     only = os.environ.get("GOLDEN_ONLY")

@@ -79,8 +79,7 @@ def test_gemm_gelu_epilogue_fp32_exactness(nat, dtype):
     assert float((out - ref).abs().max()) < (5e-6 if dtype == torch.float32 else 5e-5)
 
 
-@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2575, 2576, 2577, 2578, 2590, 2591,
-                                     2592, 2593, 2587])
+@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2587])
 @pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72)])
 def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
     """Every 256-row schedule, incl. the stream-K ones (split tiles summed by the last arriver), on the path's
@@ -107,7 +106,7 @@ def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
         assert ws.numel() > 0 and int(ws[: 4 * 65536].count_nonzero()) == 0
 
 
-@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574, 2575, 2576, 2577, 2578, 2590, 2591])
+@pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574])
 def test_conv3x3_big_variants(nat, variant):
     n, H, W, C, Co = 2, 37, 37, 256, 256
     x = _rand(n, C, H, W, seed=26).to(torch.bfloat16)
@@ -124,7 +123,7 @@ def test_conv3x3_big_variants(nat, variant):
 
 
 @pytest.mark.parametrize("variant,dtype", [(0, torch.bfloat16), (0, torch.float32), (2568, torch.bfloat16),
-                                           (2571, torch.bfloat16), (2575, torch.bfloat16), (2580, torch.bfloat16)])
+                                           (2571, torch.bfloat16), (2580, torch.bfloat16)])
 @pytest.mark.parametrize("n,H,W,C,Co,stride", [(2, 37, 37, 96, 256, 1), (1, 19, 19, 768, 128, 2)])
 def test_conv3x3_channel_block_k_order(nat, variant, dtype, n, H, W, C, Co, stride):
     """conv_kblock = 32: the K index walks the 9 taps of each 32-channel slice (weights packed [out][C/32][tap][32])
@@ -608,7 +607,7 @@ def test_split_bf16x3_is_bit_exact(nat, rows, cols, cp):
     assert torch.equal(y.view(torch.int16), ref.reshape(rows, -1).view(torch.int16))
 
 
-@pytest.mark.parametrize("variant", [0, 2568, 2575, 2576])
+@pytest.mark.parametrize("variant", [0, 2568])
 def test_split_precision_conv_matches_fp32(nat, variant):
     """A 3x3 conv run as one bf16 implicit-GEMM over split activations (stored [hi | lo], read [hi | hi | lo]) and
     [hi | lo | hi] weights (the geometric encoders' bf16-mode path) stays within ~1e-5 of the fp32 conv (plain

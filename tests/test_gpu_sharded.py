@@ -53,7 +53,10 @@ def _views(n, h, w, seed):
     return [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]} for i in synthetic.synthetic_images(n, h, w, seed)]
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 2.4e-2)])  # bf16: 3x reference bf16 yardstick
+# bf16: the same computation as the single-GPU run up to summation order (attention chunking, merge order) — held
+# below the reference's OWN bf16-vs-fp32 deviation on a case of this size (cfg1's pts3d yardstick, 8.0e-3), i.e. far
+# tighter than any recipe difference; fp32 at 2e-5 is the structural check
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 8e-3)])
 @pytest.mark.parametrize("world,V", [(1, 2), (2, 3), (3, 3)])
 def test_sharded_equals_single(precision, tol, world, V):
     from mapanything.models import MapAnything
@@ -69,13 +72,16 @@ def test_sharded_equals_single(precision, tol, world, V):
     model.enable_view_sharding(comm=comm)
     model.engine()  # build weights once, before the threads start
     outs = _run_ranks(comm, world, lambda rank: model.forward(views))
+    worst = 0.0
     for r in range(world):
         for v, o in enumerate(outs[r]):
             if o is None:
                 continue
             for k in ("pts3d", "conf", "cam_quats", "cam_trans", "metric_scaling_factor"):
                 e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
+                worst = max(worst, e)
                 assert e < tol, (r, v, k, e)
+    print(f"\n[{precision} world {world}] worst rel-L2 sharded vs single: {worst:.2e}")
     # every view produced exactly once; one metric scale for the whole job
     owners = [sum(outs[r][v] is not None for r in range(world)) for v in range(V)]
     assert owners == [1] * V
@@ -110,10 +116,13 @@ def test_sharded_gather_outputs_to_rank0():
     assert outs["rank0"][1][0] is None and outs["rank0"][1][2] is not None
 
 
-def test_cfg3_layout_100_views_on_8_ranks():
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 1.4e-2)])
+def test_cfg3_layout_100_views_on_8_ranks(precision, tol):
     """configs[2]'s shard layout: 100 views at 518x518 over 8 ranks (13,13,13,13,12,12,12,12; per global layer
     each rank's 13*1369+1-row K/V slot all-gathered, 136 901 keys) equals the single-GPU run of the same job, and
-    every rank derives the same metric scale.  bf16 (the bench recipe); the ranks are 8 threads on one GPU."""
+    every rank derives the same metric scale.  fp32 (exact-fp32 MFMA) at 2e-5: the structural check that every
+    slot, segment and split is indexed right at this size; bf16 (the bench recipe) below the reference's own
+    bf16-vs-fp32 spread at 8 views (cfg2 pts3d max 1.39e-2).  The ranks are 8 threads on one GPU."""
     from mapanything.models import MapAnything
     from mapanything.parallel import ShardPlan, ThreadComm
     from tests_helpers import released_config
@@ -121,13 +130,13 @@ def test_cfg3_layout_100_views_on_8_ranks():
     world, V = 8, 100
     assert ShardPlan(V, world, 0, 1369).counts == [13, 13, 13, 13, 12, 12, 12, 12]
     views = _views(V, 518, 518, seed=21)
-    ref_model = MapAnything(**released_config()).load_synthetic_weights().to("cuda")
+    ref_model = MapAnything(**released_config(), precision=precision).load_synthetic_weights().to("cuda")
     ref = ref_model.forward(views)
     ref = [{k: ref[v][k].float().cpu() for k in ("pts3d", "conf", "cam_quats", "cam_trans",
                                                  "metric_scaling_factor")} for v in range(V)]
     torch.cuda.empty_cache()
     comm = ThreadComm(world)
-    model = MapAnything(**released_config()).to("cuda")
+    model = MapAnything(**released_config(), precision=precision).to("cuda")
     model._sd = ref_model._sd
     del ref_model
     model.enable_view_sharding(comm=comm)
@@ -140,8 +149,8 @@ def test_cfg3_layout_100_views_on_8_ranks():
                 continue
             for k in ref[v]:
                 worst[k] = max(worst.get(k, 0.0), rel_l2(o[k].float().cpu(), ref[v][k]))
-    print("\n[cfg3 layout] worst per-view rel-L2 sharded vs single:", worst)
-    assert all(e < 2.4e-2 for e in worst.values()), worst
+    print(f"\n[cfg3 layout, {precision}] worst per-view rel-L2 sharded vs single:", worst)
+    assert all(e < tol for e in worst.values()), worst
     _scale_equal_across_ranks(outs)
 
 

@@ -23,6 +23,8 @@ CASES = {
     "cfg2_518": dict(views=8, h=518, w=518, seed=2),   # configs[1] at its real size (the bench's input seed)
     # configs[3] at its real size: 32 views + intrinsics + 90 %-sparse depth + metric flag
     "cfg4_518": dict(views=32, h=518, w=518, seed=4, multimodal=True),
+    # two scenes per view (batch_size_per_view = 2, reference model.py:687), mixed geometric inputs
+    "b2_224": dict(views=3, h=224, w=224, seed=12, mixed=True, batch=2),
 }
 
 
@@ -47,23 +49,26 @@ def make_views(case):
     from mapanything.utils import synthetic
 
     n, h, w, seed = case["views"], case["h"], case["w"], case["seed"]
-    imgs = synthetic.synthetic_images(n, h, w, seed)
+    B = case.get("batch", 1)  # scenes per view (batch_size_per_view, reference model.py:687)
+    imgs = synthetic.synthetic_images(n, h, w, seed, batch=B)
     views = []
     for v in range(n):
         view = {"img": torch.from_numpy(imgs[v]), "data_norm_type": ["dinov2"]}
         if case.get("multimodal"):
-            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
-            view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
-            view["is_metric_scale"] = torch.ones(1, dtype=torch.bool)
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed, batch=B)[v])
+            view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed, batch=B)[v])
+            view["is_metric_scale"] = torch.ones(B, dtype=torch.bool)
         if case.get("rays_only"):
-            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed, batch=B)[v])
         if case.get("mixed"):
-            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed)[v])
+            # 3 views: intrinsics everywhere, depth on views 0 and 2, poses on views 0 and 1; scene 0: view 2 not
+            # metric, further scenes: only view 0 metric
+            view["intrinsics"] = torch.from_numpy(synthetic.synthetic_intrinsics(n, h, w, seed, batch=B)[v])
             if v in (0, 2):
-                view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed)[v])
+                view["depth_z"] = torch.from_numpy(synthetic.synthetic_sparse_depth(n, h, w, seed, batch=B)[v])
             if v in (0, 1):
-                view["camera_poses"] = torch.from_numpy(synthetic.synthetic_poses(n, seed)[v])
-            view["is_metric_scale"] = torch.tensor([v != 2])
+                view["camera_poses"] = torch.from_numpy(synthetic.synthetic_poses(n, seed, batch=B)[v])
+            view["is_metric_scale"] = torch.tensor([(v != 2) if b == 0 else (v == 0) for b in range(B)])
         views.append(view)
     return views
 

@@ -40,7 +40,7 @@ def group(name: str) -> str:
 
 def _is_gemm(name):
     return "gemm_big_kernel" in name or "gemm_kernel<" in name or "gemm_sk_kernel" in name or \
-        "gemm_pp_kernel" in name or "gemm_w4" in name or "gemm_8p_kernel" in name or "conv_halo_kernel" in name
+        "gemm_pp_kernel" in name or "conv_halo_kernel" in name
 
 
 def dispatch_kinds(names, log_path):
