@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "mapa_common.h"
+#include "index_math.h"
 
 namespace {
 
@@ -58,10 +59,7 @@ __device__ __forceinline__ int kv_row(const AttnArgs& p, int key) {
   return key + off;
 }
 
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
-  const int q = nblk / 8, r = nblk % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
+using mapa_idx::xcd_remap;
 
 typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
@@ -114,18 +112,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
   const int nkt = (p.seq_kv + KT - 1) / KT;
   const bool has_tail = (p.seq_kv % KT) != 0;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
-  int task, k0, k1, slot = -1;
-  if ((int)blockIdx.x < sp.n_dp) {  // whole task; consecutive tasks (same batch/head: shared K/V) on one XCD
-    task = xcd_remap(blockIdx.x, sp.n_dp);
-    k0 = 0;
-    k1 = nkt;
-  } else {
-    slot = blockIdx.x - sp.n_dp;
-    task = sp.n_dp + slot / sp.chunks;
-    const int ch = slot % sp.chunks;
-    k0 = (int)((int64_t)ch * nkt / sp.chunks);
-    k1 = (int)((int64_t)(ch + 1) * nkt / sp.chunks);
-  }
+  int task, k0, k1, slot;
+  mapa_idx::attn_block_work(blockIdx.x, sp.n_dp, sp.chunks, nkt, task, k0, k1, slot);
 
   // Staging: piece = i*NW + wave is 8 rows x 128 B of K (piece < 8) or V; this lane's 16 B sit at tile row
   // srow[i] (XOR-swizzled 16-B column on the source so the LDS image stays lane-linear).  The byte offset inside
@@ -717,11 +705,11 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
     // the remainder after the full waves of resident slots is cut into K/V chunks of >= 4 tiles (or not at all
     // without a workspace)
     const int slots = sk_slots();
-    const int rem = ntask % slots;
-    const int chunks = rem ? std::min(slots / rem, std::max(1, nkt / 4)) : 1;
+    int n_dp, chunks;
+    mapa_idx::attn_split_plan(ntask, nkt, slots, n_dp, chunks);
     if (chunks > 1 && d->workspace && d->workspace_bytes >= sk_workspace_bytes(slots) &&
         getenv("MAPA_ATTN_NO_SPLIT") == nullptr) {
-      sp.n_dp = ntask - rem;
+      sp.n_dp = n_dp;
       sp.chunks = chunks;
       sp.part_o = reinterpret_cast<float*>(d->workspace);
       sp.part_lse = sp.part_o + (int64_t)slots * SK_QBLK * 64;

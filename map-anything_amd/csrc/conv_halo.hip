@@ -123,12 +123,8 @@ __global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(Gem
   // ---- tile: (img, block row, block col, column tile), XCD-contiguous ranges of neighbouring blocks
   const int nbx = (p.cv_OW + BW - 1) / BW, nby = (p.cv_OH + BH - 1) / BH, ntn = p.N / BN;
   const int imgs = p.M / (p.cv_OH * p.cv_OW);
-  int t = xcd_remap(blockIdx.x, imgs * nby * nbx * ntn);
-  const int tn = t % ntn;
-  t /= ntn;
-  const int bx = t % nbx;
-  t /= nbx;
-  const int by = t % nby, img = t / nby;
+  int img, by, bx, tn;
+  mapa_idx::halo_block(blockIdx.x, imgs, nby, nbx, ntn, img, by, bx, tn);
   const int bn = tn * BN;
   const int nk = p.K / 32;  // 9 taps x (logical channels / 32)
 

@@ -478,31 +478,13 @@ __global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
 // relaxed agent fetch_add on the tile's ticket; no release fence needed for sc1 payloads); the block drawing ticket
 // nseg-1 reads every slab with sc1 loads (no acquire: no plain load of slab bytes anywhere), sums them in range
 // order (bit-reproducible whatever the arrival order), resets the ticket and runs the fused epilogue.  No block ever waits on another, so the grid drains whatever the residency.
-struct SkArgs {
+struct SkArgs : mapa_idx::SkPlan {  // dp_tiles / base / total / per / nk: the iteration plan (index_math.h)
   int* tickets;   // [tiles], zero at launch (zeroed once at workspace creation; the last arriver re-zeroes)
   float* slabs;   // [G][2][BBM * BN] fp32 accumulator images in fragment order
-  int dp_tiles;   // tiles 0 .. dp_tiles-1: whole tiles, tile t on block t % G (data-parallel part)
-  int base;       // dp_tiles * nk: first stream-K iteration
-  int total;      // tiles * nk
-  int per;        // stream-K iterations per workgroup: ceil((total - base) / G)
-  int nk;
 };
 
-// block b owns stream-K iterations [base + b * per, min(base + (b + 1) * per, total)); its slab slot 0 holds the
-// segment its range starts with, slot 1 the one it ends with (a range touches at most two split tiles).
-__device__ __forceinline__ int64_t sk_slab(int b, int tb, const SkArgs& s) {
-  return (int64_t)b * 2 + (s.base + b * s.per >= tb ? 0 : 1);
-}
+using mapa_idx::sk_slab;
 
-template <int GM>
-__device__ __forceinline__ void group_coords(int t, int ntm, int ntn, int& tm, int& tn) {
-  const int group = t / (GM * ntn);
-  const int first = group * GM;
-  const int rows = min(GM, ntm - first);
-  const int in = t - group * GM * ntn;
-  tm = first + in % rows;
-  tn = in / rows;
-}
 
 template <int AMODE, int BN, int RB, int STAGES, int PRIO, int MINB>
 __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkArgs s) {
@@ -521,29 +503,17 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
   const int wm = wave / C::WN, wn = wave % C::WN;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BBM - 1) / BBM;
   const int vb = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ranges (shared tiles) on one XCD
-  const int r0 = s.base + vb * s.per, r1 = min(r0 + s.per, s.total);
   const bool k_exact = (p.K % C::BK) == 0;
   const int lds_wave = wave * 1024;
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
   const int g = lane >> 4, r16 = lane & 15;
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 
-  int dp_t = vb;
-  for (int it = r0;;) {
+  // data-parallel whole tiles first, then this block's stream-K iteration range (mapa_idx::sk_next)
+  mapa_idx::SkCursor cur = mapa_idx::sk_begin(s, vb);
+  for (;;) {
     int t, k0, k1;
-    if (dp_t < s.dp_tiles) {  // data-parallel whole tiles first
-      t = dp_t;
-      k0 = 0;
-      k1 = s.nk;
-      dp_t += gridDim.x;
-    } else if (it < r1) {
-      t = it / s.nk;
-      k0 = it - t * s.nk;
-      k1 = min(s.nk, r1 - t * s.nk);
-      it = t * s.nk + k1;
-    } else {
-      break;
-    }
+    if (!mapa_idx::sk_next(s, gridDim.x, cur, t, k0, k1)) break;
     const int tb = t * s.nk;
     int tm, tn;
     group_coords<4>(t, ntm, ntn, tm, tn);
@@ -641,8 +611,8 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
     }
     __syncthreads();  // LDS free for the epilogue
 
-    const int lo = t < s.dp_tiles ? 0 : (tb - s.base) / s.per;
-    const int hi = t < s.dp_tiles ? 0 : (tb + s.nk - 1 - s.base) / s.per;
+    int lo, hi;
+    mapa_idx::sk_contributors(s, t, lo, hi);
     if (lo != hi) {
       // split tile: publish this segment's partial sums.  Buffer stores/loads: the per-fragment offset is an
       // SGPR (soffset), the only VGPR is the lane's 16-B column -> no hoisted 64-bit addresses across the
@@ -827,34 +797,11 @@ bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, in
   const int64_t nk = (a.K + bk - 1) / bk;
   if (tiles * nk >= (int64_t(1) << 31)) return false;
   SkArgs s;
-  s.nk = (int)nk;
-  s.total = (int)(tiles * nk);
   const int g = sk_cus() * per_cu;
-  // Data-parallel whole tiles for all but the last one-to-two waves; stream-K spreads the rest evenly, so at most
-  // ~one tile per block is split (each split costs a 128-256 KB slab write + read).
-  int G;
-  if (variant == 2) {
-    // tail-only stream-K: every full wave of resident tiles runs data-parallel; only the iterations of the last,
-    // partial wave are spread (in chunks of >= nk/4 K-steps, so a split tile has at most 4 contributors)
-    s.dp_tiles = (int)((tiles / g) * g);
-    s.base = s.dp_tiles * s.nk;
-    const int rem = s.total - s.base;
-    s.per = std::max((rem + g - 1) / g, std::max(1, s.nk / 4));
-    G = g;  // blocks past the stream-K ranges only take data-parallel tiles
-  } else {
-    // Data-parallel whole tiles for all but the last one-to-two waves; stream-K spreads the rest evenly, so at most
-    // ~one tile per block is split (each split costs a 128-256 KB slab write + read).
-    static const int dp_env = getenv("MAPA_SK_DP") ? atoi(getenv("MAPA_SK_DP")) : 1;  // tuning: 0 = pure stream-K
-    s.dp_tiles = (dp_env && tiles >= 2 * g) ? (int)((tiles / g - 1) * g) : 0;
-    s.base = s.dp_tiles * s.nk;
-    s.per = (s.total - s.base + g - 1) / g;
-    // at least a tenth of a tile's K per block: past ~10 contributors per tile the last arriver's serial slab sum
-    // dominates (kbench, 8 views: rn4@19 80 -> 55 us, layer4_rn 119 -> 87; the 37^2 convs already split coarser)
-    s.per = std::max(s.per, s.nk / 10);
-    static const int per_env = getenv("MAPA_SK_PER") ? atoi(getenv("MAPA_SK_PER")) : 0;  // tuning: iterations/block
-    if (per_env > s.per) s.per = per_env;  // only coarser: G stays within the workspace's slab count
-    G = (s.total - s.base + s.per - 1) / s.per;
-  }
+  static const int dp_env = getenv("MAPA_SK_DP") ? atoi(getenv("MAPA_SK_DP")) : 1;   // tuning: 0 = pure stream-K
+  static const int per_env = getenv("MAPA_SK_PER") ? atoi(getenv("MAPA_SK_PER")) : 0;  // tuning: iterations/block
+  // kbench, 8 views: the tenth-of-a-tile floor took rn4@19 80 -> 55 us, layer4_rn 119 -> 87 (mapa_idx::sk_make_plan)
+  const int G = mapa_idx::sk_make_plan(tiles, (int)nk, g, variant == 2, dp_env != 0, per_env, s);
   s.tickets = reinterpret_cast<int*>(ws);
   s.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + SK_TICKET_BYTES);
   void (*k)(GemmArgs, SkArgs);

@@ -2,6 +2,7 @@
 // tiles): launch arguments and the shared fused epilogue.
 #pragma once
 #include "mapa_common.h"
+#include "index_math.h"
 
 namespace mapa_gemm_impl {
 
@@ -34,25 +35,9 @@ struct GemmArgs {
   int vec_ok;    // N % 4 == 0, ldo % 4 == 0, ps_cout % 4 == 0: 4-wide epilogue
 };
 
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
-  // blocks b, b+8, ... share an XCD (round-robin dispatch); give each XCD a contiguous tile range.
-  const int q = nblk / 8, r = nblk % 8, x = b % 8;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-}
-
-// Output tile of this workgroup: XCD-contiguous tile ranges (xcd_remap), walked in groups of GM tile-rows so the
-// ~32 tiles an XCD runs at once form a GM x (32/GM) patch: its A row-blocks and W column-blocks are re-read
-// from that XCD's L2 instead of the Infinity Cache.
-template <int GM>
-__device__ __forceinline__ void tile_coords(int b, int ntm, int ntn, int& tm, int& tn) {
-  const int t = xcd_remap(b, ntm * ntn);
-  const int group = t / (GM * ntn);
-  const int first = group * GM;
-  const int rows = min(GM, ntm - first);
-  const int in = t - group * GM * ntn;
-  tm = first + in % rows;
-  tn = in / rows;
-}
+using mapa_idx::group_coords;
+using mapa_idx::tile_coords;
+using mapa_idx::xcd_remap;
 
 // Logical A column (within a row, or within a conv tap) -> physical column of a compact split operand: the
 // logical blocks [hi | hi | lo] map onto the stored [hi | lo] (the second hi block re-reads the first).
@@ -66,19 +51,7 @@ __device__ __forceinline__ int64_t split_koff(const GemmArgs& p, int kc, int esz
 // mapa_gemm_desc.conv_kblock.
 __device__ __forceinline__ void conv_kmap(const GemmArgs& p, int kc, int& tap, int& ci) {
   int c;
-  if (p.cv_kb == 32) {  // the head convs' block: divisions by constants
-    const int blk = kc / 288, r = kc - blk * 288;
-    tap = r >> 5;
-    c = blk * 32 + (r & 31);
-  } else if (p.cv_kb > 0) {
-    const int span = 9 * p.cv_kb;
-    const int blk = kc / span, r = kc - blk * span;
-    tap = r / p.cv_kb;
-    c = blk * p.cv_kb + (r - tap * p.cv_kb);
-  } else {
-    tap = kc / p.cv_C;
-    c = kc - tap * p.cv_C;
-  }
+  mapa_idx::conv_kmap_logical(kc, p.cv_kb, p.cv_C, tap, c);
   ci = split_col(p, c);
 }
 

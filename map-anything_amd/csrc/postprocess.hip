@@ -10,6 +10,7 @@
 //   final combine.  Float operations follow numpy's order (no fma contraction, -ffp-contract=off) so equal
 //   inputs give equal bits; the angle threshold is applied on the dot product (arccos is monotone).
 #include "mapa_common.h"
+#include "index_math.h"
 
 #include <math.h>
 #include <string.h>
@@ -42,11 +43,10 @@ __device__ __forceinline__ float norm3(const float a[3]) {
 // K1: points_to_normals(point, mask) -> normal (H,W,3) and normal_mask (H,W).  Stored already renormalised
 // (n / (|n| + 1e-12), normals_edge's first step, geometry.py:2216): K2 reads every normal 9 times, and the same
 // float operations applied once per pixel give the same bits.  32-bit pixel indices (the host checks n*H*W).
-// Grid-stride step in 64-bit, clamped to `total`: a 32-bit `e += stride` overflows when total is within one grid of
-// 2^31; the index stays 32-bit inside the loop bodies.
+// Grid-stride step in 64-bit, clamped to `total` (mapa_idx::grid_step): a 32-bit `e += stride` overflows when total
+// is within one grid of 2^31; the index stays 32-bit inside the loop bodies.
 __device__ __forceinline__ int grid_next(int e, int total) {
-  const int64_t n = (int64_t)e + (int64_t)gridDim.x * blockDim.x;
-  return n < total ? (int)n : total;
+  return mapa_idx::grid_step(e, total, (int64_t)gridDim.x * blockDim.x);
 }
 
 __global__ void normals_kernel(const float* __restrict__ pts, const uint8_t* __restrict__ mask, int n, int H, int W,
