@@ -53,7 +53,8 @@ def main():
     ap.add_argument("--total-views", type=int, default=0,
                     help="strong scaling: this many views split over the ranks (configs[2]: 100), else views-per-gpu")
     ap.add_argument("--res", type=int, default=518)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
+                    help="autocast operand dtype of the encoder / transformer (infer(amp_dtype=...)); fp32 = use_amp off")
     ap.add_argument("--head-precision", default="fp32", choices=["fp32", "bf16"],
                     help="fp32 = the reference's recipe (autocast disabled for the heads); bf16 = fast mode")
     ap.add_argument("--no-fast-mode", action="store_true", help="skip the bf16-heads fast-mode measurement")
@@ -124,8 +125,10 @@ def main():
             v.update(intrinsics=torch.from_numpy(K).to(dev), depth_z=torch.from_numpy(D).to(dev),
                      is_metric_scale=torch.ones(1, dtype=torch.bool, device=dev))
 
+    amp = dict(use_amp=args.precision != "fp32", amp_dtype=args.precision if args.precision != "fp32" else "bf16")
+
     def step():
-        return model.infer(views)
+        return model.infer(views, **amp)
 
     for _ in range(args.warmup):
         step()
@@ -170,11 +173,11 @@ def main():
         fm = MapAnything(**released_config(), precision=args.precision, head_precision="bf16").to(dev).eval()
         fm._sd = model._sd
         for _ in range(args.warmup):
-            fm.infer(views)
+            fm.infer(views, **amp)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            fm.infer(views)
+            fm.infer(views, **amp)
         torch.cuda.synchronize()
         fdt = time.perf_counter() - t0
         fast = {"value": V_total * args.steps / fdt, "unit": "views/s", "ms_per_step": fdt / args.steps * 1e3,
@@ -190,8 +193,8 @@ def main():
         s_imgs = synthetic.synthetic_images(args.strong_views, H, W, seed=3)
         s_views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in s_imgs]
         del s_imgs
-        model.infer(s_views)  # warm-up (graph capture at N=1)
-        sdt = timed_fn(lambda: model.infer(s_views), args.strong_steps)
+        model.infer(s_views, **amp)  # warm-up (graph capture at N=1)
+        sdt = timed_fn(lambda: model.infer(s_views, **amp), args.strong_steps)
         strong = {"views": args.strong_views, "value": args.strong_views * args.strong_steps / sdt, "unit": "views/s",
                   "ms_per_step": sdt / args.strong_steps * 1e3, "steps": args.strong_steps, "warmup": 1,
                   "scaling": "strong", "views_per_gpu": args.strong_views / world,

@@ -24,11 +24,13 @@ typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
 
 /* MAPA_BF16X3: split-precision bf16 operand rows [hi | lo] (2x the logical width; see mapa_split_bf16x3),
  * accepted as an OUTPUT dtype by mapa_layernorm (y_lp) and mapa_bilinear_ac */
-enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2 };
+/* MAPA_F16: IEEE binary16 operands (the fp16 autocast recipe, infer(amp_dtype="fp16")); accepted by mapa_gemm (dense
+ * A), mapa_attention, mapa_attn_merge, and as an output dtype of mapa_layernorm / mapa_patchify / mapa_convert_rows */
+enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2, MAPA_F16 = 3 };
 enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
 enum { MAPA_OUT_ROWMAJOR = 0, MAPA_OUT_PIXSHUF = 1 };
-/* GELU is the exact-erf form (nn.GELU()), erf evaluated branch-free to within 5e-7 absolute (Abramowitz & Stegun
- * 7.1.26 in fp32; the GELU output within 3.5e-7 absolute). */
+/* GELU is the exact-erf form (nn.GELU()), erf evaluated branch-free to within 1.2 ulp of fp32 erff (two minimax
+ * pieces, csrc/mapa_common.h erf_fast; tools/erf_check.py). */
 enum { MAPA_ACT_NONE = 0, MAPA_ACT_GELU = 1, MAPA_ACT_RELU = 2, MAPA_ACT_GELU_POST = 3 };
 
 const char* mapa_last_error(void);

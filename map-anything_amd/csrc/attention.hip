@@ -99,7 +99,8 @@ struct SplitArgs {
   int chunks;       // K/V chunks per remaining task (grid ids n_dp + j: task n_dp + j / chunks, chunk j % chunks)
 };
 
-template <int NW, bool SEG>
+// F16: fp16 operands (the fp16 autocast recipe): same structure, f16 MFMAs, P rounded to fp16
+template <int NW, bool SEG, bool F16 = false>
 __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArgs sp) {
   constexpr int TILE = KT * 128;  // 64 rows x 128 B
   constexpr int QBLK_WG = NW * 32;
@@ -182,16 +183,23 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 
     // Q^T fragments (B operand): lane holds Q[q][kk*16 + 8*hl + j], pre-scaled by 1/8 * log2(e) so the
     // scores come out of the MFMA already in the log2 domain (one bf16 rounding of the scaled Q).
-    b8 qf[4];
+    bf16x8 qf[4];  // raw 16-bit operand words (bf16, or fp16 with F16)
     {
       const int qrow_c = qrow < p.seq_q ? qrow : p.seq_q - 1;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         const s8v raw = *reinterpret_cast<const s8v*>(qbase + (int64_t)qrow_c * p.qr + kk * 16 + 8 * hl);
-        b8 sc;
+        if constexpr (F16) {
+          f16x8_t sc;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (p.qscale * LOG2E));
-        qf[kk] = sc;
+          for (int j = 0; j < 8; ++j) sc[j] = (_Float16)(f16_to_f32((uint16_t)raw[j]) * (p.qscale * LOG2E));
+          qf[kk] = __builtin_bit_cast(bf16x8, sc);
+        } else {
+          b8 sc;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sc[j] = (__bf16)(bf16_to_f32((bf16_t)raw[j]) * (p.qscale * LOG2E));
+          qf[kk] = __builtin_bit_cast(bf16x8, sc);
+        }
       }
     }
 
@@ -223,14 +231,14 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
       const char* Vs = Ks + TILE;
       // every LDS read of this tile is issued before the next tile's DMA, so the compiler's conservative
       // vmcnt(0) (an LDS-DMA may alias any LDS read) never lands inside the tile
-      b8 kf[2][4];
+      bf16x8 kf[2][4];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         const int row = kb * 32 + l32;
 #pragma unroll
         for (int kk = 0; kk < 4; ++kk) {
           const int chunk = kk * 2 + hl;
-          kf[kb][kk] = *reinterpret_cast<const b8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+          kf[kb][kk] = *reinterpret_cast<const bf16x8*>(Ks + row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
         }
       }
       // S^T - m_ref = K Q^T + C, C = -m_ref (masked keys of the tail tile: -inf)
@@ -243,16 +251,16 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
             const int key = kt * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hl;
             st[kb][r] = key < p.seq_kv ? csplat[r] : -INFINITY;
           }
-          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], st[kb], 0, 0, 0);
+          st[kb] = mfma32x32x16<F16>(kf[kb][0], qf[0], st[kb]);
         } else {
-          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][0], qf[0], csplat, 0, 0, 0);
+          st[kb] = mfma32x32x16<F16>(kf[kb][0], qf[0], csplat);
         }
 #pragma unroll
         for (int kk = 1; kk < 4; ++kk)
-          st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kb][kk], qf[kk], st[kb], 0, 0, 0);
+          st[kb] = mfma32x32x16<F16>(kf[kb][kk], qf[kk], st[kb]);
       }
       // V^T fragments (transposed LDS reads), then the next tile's DMA
-      b8 vf[2][2][2];
+      bf16x8 vf[2][2][2];
       {
         const int i4 = lane & 15, q4 = i4 >> 2, p4 = i4 & 3, grp = (lane >> 4) & 1;
 #pragma unroll
@@ -268,14 +276,14 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
               const s4v lo = tr_read(Vs + R0 * 128 + ((chunk ^ (((R0 >> 1) & 1) << 2)) << 4) + within);
               const s4v hi = tr_read(Vs + R1 * 128 + ((chunk ^ (((R1 >> 1) & 1) << 2)) << 4) + within);
               const s8v vv = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-              vf[dt][kb][s] = __builtin_bit_cast(b8, vv);
+              vf[dt][kb][s] = vv;
             }
         }
       }
       if (kt + 1 < k1) stage(cur ^ 1, kt + 1);
 
       // P = exp2(S - m_ref) -> bf16 fragments, row partial sums (this lane's 32 keys)
-      b8 pf[2][2];
+      bf16x8 pf[2][2];
       float ls;
       auto exp_pack = [&](float shift) __attribute__((always_inline)) {
         float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -283,14 +291,25 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            b8 t;
+            if constexpr (F16) {
+              f16x8_t t;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float e = __builtin_amdgcn_exp2f(st[kb][8 * s + j] - shift);
-              a[j & 3] = add_s(a[j & 3], e);
-              t[j] = (__bf16)e;
+              for (int j = 0; j < 8; ++j) {
+                const float e = __builtin_amdgcn_exp2f(st[kb][8 * s + j] - shift);
+                a[j & 3] = add_s(a[j & 3], e);
+                t[j] = (_Float16)e;
+              }
+              pf[kb][s] = __builtin_bit_cast(bf16x8, t);
+            } else {
+              b8 t;
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float e = __builtin_amdgcn_exp2f(st[kb][8 * s + j] - shift);
+                a[j & 3] = add_s(a[j & 3], e);
+                t[j] = (__bf16)e;
+              }
+              pf[kb][s] = __builtin_bit_cast(bf16x8, t);
             }
-            pf[kb][s] = t;
           }
         ls = add_s(add_s(a[0], a[1]), add_s(a[2], a[3]));
       };
@@ -330,7 +349,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
           for (int s = 0; s < 2; ++s)
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[dt][kb][s], pf[kb][s], o[dt], 0, 0, 0);
+            o[dt] = mfma32x32x16<F16>(vf[dt][kb][s], pf[kb][s], o[dt]);
       __syncthreads();
     };
 
@@ -372,8 +391,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
           for (int gq = 0; gq < 4; ++gq) {
             const int d = dt * 32 + 8 * gq + 4 * hl;
             uint2 pk;
-            pk.x = pack_bf16x2(o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-            pk.y = pack_bf16x2(o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
+            pk.x = pack_lp2(F16, o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
+            pk.y = pack_lp2(F16, o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
             *reinterpret_cast<uint2*>(obase + d) = pk;
           }
         if (p.lse && hl == 0)
@@ -400,7 +419,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 // each over every MERGE_G-th chunk, combined by a fixed butterfly (deterministic): ~43 chunks per row were a
 // latency-bound serial walk in one thread (14.5 us per 8-view global layer).
 constexpr int MERGE_G = 8;
-template <int NW>
+template <int NW, bool F16 = false>
 __global__ void __launch_bounds__(256) attn_split_merge(AttnArgs p, SplitArgs sp, int nsplit_rows) {
   constexpr int QBLK_WG = NW * 32;
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -436,8 +455,8 @@ __global__ void __launch_bounds__(256) attn_split_merge(AttnArgs p, SplitArgs sp
   if (!live || g != 0 || qrow >= p.seq_q) return;
   const float inv = 1.f / wsum;
   uint2 pk;
-  pk.x = pack_bf16x2(acc[0] * inv, acc[1] * inv);
-  pk.y = pack_bf16x2(acc[2] * inv, acc[3] * inv);
+  pk.x = pack_lp2(F16, acc[0] * inv, acc[1] * inv);
+  pk.y = pack_lp2(F16, acc[2] * inv, acc[3] * inv);
   *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64 + c4 * 4) = pk;
   if (p.lse && c4 == 0) p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = mx + __logf(wsum);
 }
@@ -579,7 +598,7 @@ __global__ void __launch_bounds__(NT, 1) attn_fwd_f32(AttnArgs p) {
 // Merge of two attention partials over disjoint key sets (flash-decoding style):
 //   w_a = exp(lse_a - m), w_b = exp(lse_b - m), m = max(lse_a, lse_b);  o = (w_a o_a + w_b o_b) / (w_a + w_b)
 // o rows [rows][heads*64] (row stride ld), lse [heads][rows] (natural log, as attn_fwd writes it).
-template <typename T>
+template <typename T, bool F16 = false>
 __global__ void attn_merge_kernel(const T* __restrict__ oa, const float* __restrict__ la, const T* __restrict__ ob,
                                   const float* __restrict__ lb, T* __restrict__ out, float* __restrict__ lse_out,
                                   int rows, int heads, int64_t ld) {
@@ -598,14 +617,14 @@ __global__ void attn_merge_kernel(const T* __restrict__ oa, const float* __restr
     for (int j = 0; j < 4; ++j) {
       float va, vb;
       if constexpr (sizeof(T) == 2) {
-        va = bf16_to_f32(oa[o + j]);
-        vb = bf16_to_f32(ob[o + j]);
+        va = lp_to_f32(F16, oa[o + j]);
+        vb = lp_to_f32(F16, ob[o + j]);
       } else {
         va = oa[o + j];
         vb = ob[o + j];
       }
       const float v = (wa * va + wb * vb) * inv;
-      if constexpr (sizeof(T) == 2) out[o + j] = f32_to_bf16(v);
+      if constexpr (sizeof(T) == 2) out[o + j] = f32_to_lp(F16, v);
       else out[o + j] = v;
     }
     if (lse_out && d4 == 0) lse_out[(int64_t)h * rows + r] = m + __logf(wa + wb);
@@ -624,6 +643,9 @@ extern "C" int mapa_attn_merge(const void* o_a, const float* lse_a, const void* 
   if (dtype == MAPA_BF16)
     hipLaunchKernelGGL(attn_merge_kernel<bf16_t>, dim3((unsigned)g), dim3(256), 0, stream, (const bf16_t*)o_a, lse_a,
                        (const bf16_t*)o_b, lse_b, (bf16_t*)o_out, lse_out, rows, heads, ld);
+  else if (dtype == MAPA_F16)
+    hipLaunchKernelGGL((attn_merge_kernel<bf16_t, true>), dim3((unsigned)g), dim3(256), 0, stream, (const bf16_t*)o_a,
+                       lse_a, (const bf16_t*)o_b, lse_b, (bf16_t*)o_out, lse_out, rows, heads, ld);
   else
     hipLaunchKernelGGL(attn_merge_kernel<float>, dim3((unsigned)g), dim3(256), 0, stream, (const float*)o_a, lse_a,
                        (const float*)o_b, lse_b, (float*)o_out, lse_out, rows, heads, ld);
@@ -671,8 +693,8 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d->batch > 0 && d->heads > 0 && d->seq_q > 0 && d->seq_kv > 0,
                  "mapa_attention: bad shape b=%d h=%d q=%d kv=%d", d->batch, d->heads, d->seq_q, d->seq_kv);
   MAPA_CHECK_ARG(d->q && d->k && d->v && d->o, "mapa_attention: null pointer");
-  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32, "mapa_attention: bad dtype");
-  const int align = d->dtype == MAPA_BF16 ? 8 : 4;
+  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F16 || d->dtype == MAPA_F32, "mapa_attention: bad dtype");
+  const int align = d->dtype == MAPA_F32 ? 4 : 8;
   MAPA_CHECK_ARG(d->q_rstride % align == 0 && d->k_rstride % align == 0 && d->v_rstride % align == 0 &&
                      d->o_rstride % 4 == 0,
                  "mapa_attention: row strides must keep 16-B alignment");
@@ -694,7 +716,8 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   }
   MAPA_CHECK_ARG(d->kv_nseg == 0 || tot == d->seq_kv, "mapa_attention: kv segments sum %lld != seq_kv %d",
                  (long long)tot, d->seq_kv);
-  if (d->dtype == MAPA_BF16) {
+  if (d->dtype != MAPA_F32) {  // bf16 or fp16 operands: the MFMA flash kernel
+    const bool f16 = d->dtype == MAPA_F16;
     const int ntask = ((d->seq_q + SK_QBLK - 1) / SK_QBLK) * d->heads * d->batch;
     const int nkt = (d->seq_kv + KT - 1) / KT;
     SplitArgs sp;
@@ -715,15 +738,25 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
       sp.part_lse = sp.part_o + (int64_t)slots * SK_QBLK * 64;
     }
     const int grid = sp.n_dp + (ntask - sp.n_dp) * sp.chunks;
-    if (a.nseg > 0)
+    if (f16) {
+      if (a.nseg > 0)
+        hipLaunchKernelGGL((attn_fwd_bf16<SK_NW, true, true>), dim3(grid), dim3(SK_NW * 64), 0, stream, a, sp);
+      else
+        hipLaunchKernelGGL((attn_fwd_bf16<SK_NW, false, true>), dim3(grid), dim3(SK_NW * 64), 0, stream, a, sp);
+    } else if (a.nseg > 0) {
       hipLaunchKernelGGL((attn_fwd_bf16<SK_NW, true>), dim3(grid), dim3(SK_NW * 64), 0, stream, a, sp);
-    else
+    } else {
       hipLaunchKernelGGL((attn_fwd_bf16<SK_NW, false>), dim3(grid), dim3(SK_NW * 64), 0, stream, a, sp);
+    }
     MAPA_CHECK_LAUNCH("mapa_attention");
     if (sp.n_dp < ntask) {
       const int rows = (ntask - sp.n_dp) * SK_QBLK;
-      hipLaunchKernelGGL((attn_split_merge<SK_NW>), dim3((rows * 16 * MERGE_G + 255) / 256), dim3(256), 0, stream, a,
-                         sp, rows);
+      if (f16)
+        hipLaunchKernelGGL((attn_split_merge<SK_NW, true>), dim3((rows * 16 * MERGE_G + 255) / 256), dim3(256), 0,
+                           stream, a, sp, rows);
+      else
+        hipLaunchKernelGGL((attn_split_merge<SK_NW>), dim3((rows * 16 * MERGE_G + 255) / 256), dim3(256), 0, stream,
+                           a, sp, rows);
       MAPA_CHECK_LAUNCH("mapa_attention (split merge)");
     }
     return 0;

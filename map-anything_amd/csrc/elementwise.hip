@@ -15,7 +15,8 @@ inline int grid_for(int64_t n, int per_block = TPB) {
 // ---------------------------------------------------------------------------------------------- patchify
 // PatchEmbed (vision_transformer.py:244-249, Conv2d 3->1024 k14 s14) as im2col rows for the GEMM.
 template <typename T>
-__global__ void patchify_kernel(const float* __restrict__ img, int n, int H, int W, T* __restrict__ out, int kpad) {
+__global__ void patchify_kernel(const float* __restrict__ img, int n, int H, int W, T* __restrict__ out, int kpad,
+                                int f16) {
   const int hp = H / 14, wp = W / 14;
   const int64_t total = (int64_t)n * hp * wp * kpad;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -30,7 +31,7 @@ __global__ void patchify_kernel(const float* __restrict__ img, int n, int H, int
       const int c = k / 196, rem = k - c * 196, ky = rem / 14, kx = rem - ky * 14;
       v = img[(((int64_t)im * 3 + c) * H + py * 14 + ky) * W + px * 14 + kx];
     }
-    if constexpr (sizeof(T) == 2) out[e] = f32_to_bf16(v);
+    if constexpr (sizeof(T) == 2) out[e] = f32_to_lp(f16, v);
     else out[e] = v;
   }
 }
@@ -323,7 +324,7 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, 
     const int c = (int)(e % cols);
     const int64_t r = e / cols;
     const float v = src[r * lds + c];
-    if (bf) reinterpret_cast<bf16_t*>(dst)[r * ldd + c] = f32_to_bf16(v);
+    if (bf) reinterpret_cast<bf16_t*>(dst)[r * ldd + c] = f32_to_lp(bf == 2, v);  // 1 bf16, 2 fp16
     else reinterpret_cast<float*>(dst)[r * ldd + c] = v;
   }
 }
@@ -363,12 +364,13 @@ extern "C" int mapa_patchify(const float* img, int n, int H, int W, void* out, i
                              hipStream_t stream) {
   MAPA_CHECK_ARG(img && out && n > 0 && H % 14 == 0 && W % 14 == 0 && kpad >= 588, "mapa_patchify: bad args");
   const int64_t total = (int64_t)n * (H / 14) * (W / 14) * kpad;
-  if (dtype == MAPA_BF16)
+  MAPA_CHECK_ARG(dtype == MAPA_BF16 || dtype == MAPA_F16 || dtype == MAPA_F32, "mapa_patchify: bad dtype");
+  if (dtype != MAPA_F32)
     hipLaunchKernelGGL(patchify_kernel<bf16_t>, dim3(grid_for(total)), dim3(TPB), 0, stream, img, n, H, W,
-                       reinterpret_cast<bf16_t*>(out), kpad);
+                       reinterpret_cast<bf16_t*>(out), kpad, dtype == MAPA_F16 ? 1 : 0);
   else
     hipLaunchKernelGGL(patchify_kernel<float>, dim3(grid_for(total)), dim3(TPB), 0, stream, img, n, H, W,
-                       reinterpret_cast<float*>(out), kpad);
+                       reinterpret_cast<float*>(out), kpad, 0);
   MAPA_CHECK_LAUNCH("mapa_patchify");
   return 0;
 }
@@ -500,7 +502,7 @@ extern "C" int mapa_convert_rows(const float* src, int64_t lds, int rows, int co
                                  int64_t ldd, hipStream_t stream) {
   MAPA_CHECK_ARG(src && dst && rows > 0 && cols > 0, "mapa_convert_rows: bad args");
   hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(TPB), 0, stream, src, lds, rows,
-                     cols, dst, dst_dtype == MAPA_BF16 ? 1 : 0, ldd);
+                     cols, dst, dst_dtype == MAPA_BF16 ? 1 : dst_dtype == MAPA_F16 ? 2 : 0, ldd);
   MAPA_CHECK_LAUNCH("mapa_convert_rows");
   return 0;
 }

@@ -46,10 +46,17 @@ __device__ __forceinline__ int swz(int row) {
 struct TraitsBF16 {
   using T = bf16_t;
   static constexpr int E = 8;    // elements per 16-B chunk
+  static constexpr bool F16 = false;
+};
+struct TraitsF16 {  // fp16 operands (the fp16 autocast recipe): same 16-bit storage and tiles, f16 MFMA
+  using T = bf16_t;
+  static constexpr int E = 8;
+  static constexpr bool F16 = true;
 };
 struct TraitsF32 {
   using T = float;
   static constexpr int E = 4;
+  static constexpr bool F16 = false;
 };
 
 template <typename Tr, int RB>
@@ -59,19 +66,18 @@ __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int 
   const int g = lane >> 4, r16 = lane & 15;
   const int chunk = kg * 4 + g;
   if constexpr (sizeof(typename Tr::T) == 2) {
-    typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-    b8 a[4], b[4];
+    bf16x8 a[4], b[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ra = wm * 64 + i * 16 + r16;
-      a[i] = *reinterpret_cast<const b8*>(As + ra * ROW_BYTES + ((chunk ^ swz<RB>(ra)) << 4));
+      a[i] = *reinterpret_cast<const bf16x8*>(As + ra * ROW_BYTES + ((chunk ^ swz<RB>(ra)) << 4));
       const int rb = wn * 64 + i * 16 + r16;
-      b[i] = *reinterpret_cast<const b8*>(Bs + rb * ROW_BYTES + ((chunk ^ swz<RB>(rb)) << 4));
+      b[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * ROW_BYTES + ((chunk ^ swz<RB>(rb)) << 4));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16x16x32<Tr::F16>(a[i], b[j], acc[i][j]);
   } else {
     f32x4 a[4], b[4];
 #pragma unroll
@@ -276,7 +282,7 @@ void launch_variant(int variant, int nblk, hipStream_t stream, const GemmArgs& a
 //   2587 = 192x192 tile, 1 workgroup/CU (N = 768: a fuller single wave)
 //   1282 / 643 = 128x128 tiles (fp32 parity mode; problems too small to fill the chip with 256-row tiles)
 int pick_variant(int dtype, bool conv, int M, int N, int K) {
-  if (dtype != MAPA_BF16) return (conv || K < 1024) ? 643 : 1282;
+  if (dtype == MAPA_F32) return (conv || K < 1024) ? 643 : 1282;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
   if (big_tiles < 256) return (conv || K < 1024) ? 643 : 1282;
   // 192x256 tiles when they fit one wave on the CUs and 256-row tiles leave a quarter of them idle: the path's
@@ -354,11 +360,16 @@ using namespace mapa_gemm_impl;
 static int gemm_args(const mapa_gemm_desc* d, GemmArgs& a) {
   MAPA_CHECK_ARG(d != nullptr, "mapa_gemm: null descriptor");
   MAPA_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "mapa_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
-  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32, "mapa_gemm: dtype must be bf16 or f32");
-  const int E = d->dtype == MAPA_BF16 ? 8 : 4;
+  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32 || d->dtype == MAPA_F16,
+                 "mapa_gemm: dtype must be bf16, f16 or f32");
+  // fp16: the transformer linears of the fp16 autocast recipe (dense A; the heads stay fp32-exact split bf16)
+  MAPA_CHECK_ARG(d->dtype != MAPA_F16 || (d->a_mode == MAPA_A_DENSE && !d->a_split && d->out_mode == MAPA_OUT_ROWMAJOR),
+                 "mapa_gemm: f16 takes dense row-major problems only");
+  const int E = d->dtype == MAPA_F32 ? 4 : 8;
   MAPA_CHECK_ARG(d->K % E == 0, "mapa_gemm: K=%d must be a multiple of %d", d->K, E);
   MAPA_CHECK_ARG(d->A && d->W, "mapa_gemm: null operand");
   MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || (!d->out_s3 && !d->out_s3_relu), "mapa_gemm: split outputs need dtype bf16");
+  a.lp_f16 = d->dtype == MAPA_F16 ? 1 : 0;
   MAPA_CHECK_ARG(d->act >= MAPA_ACT_NONE && d->act <= MAPA_ACT_GELU_POST, "mapa_gemm: bad act %d", d->act);
   MAPA_CHECK_ARG(d->act != MAPA_ACT_GELU_POST || !d->gamma, "mapa_gemm: GELU_POST takes no gamma");
   if (d->a_mode == MAPA_A_CONV3X3) {
@@ -435,9 +446,11 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
                               : launch_conv_halo(a, a.N % 256 == 0 && g_halo == 1 ? 256 : 128, stream,
                                                  a.N % 256 == 0 && g_halo == 1 ? 8 : 16))) {
     // launched (LDS halo-window conv)
-  } else if (d->dtype == MAPA_BF16 && ((variant >= 2560 && variant <= 2574) || variant == 2587) &&
+  } else if (d->dtype != MAPA_F32 && ((variant >= 2560 && variant <= 2574) || variant == 2587) &&
              launch_gemm_big(a, conv, variant == 2587 ? 15 : variant - 2560, stream)) {
-    // launched
+    // launched (bf16, or f16 for the tile kernels that carry an fp16 instantiation)
+  } else if (d->dtype == MAPA_F16) {
+    launch_variant<TraitsF16, 0>(variant >= 2560 ? 1282 : variant, nblk, stream, a);
   } else if (d->dtype == MAPA_BF16) {
     if (conv) launch_variant<TraitsBF16, 1>(variant, nblk, stream, a);
     else launch_variant<TraitsBF16, 0>(variant, nblk, stream, a);

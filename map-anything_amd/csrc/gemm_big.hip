@@ -86,7 +86,8 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
   }
 }
 
-template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1, int BM = BBM>
+template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1, int BM = BBM,
+          bool F16 = false>
 __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   using C = Cfg<BN, RB, BM>;
   constexpr int MAIN = STAGES * C::STAGE;
@@ -142,24 +143,23 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   const int g = lane >> 4, r16 = lane & 15;
   auto compute = [&](int slot) __attribute__((always_inline)) {
     const char* As = lds + slot * C::STAGE;
     const char* Bs = As + C::A_BYTES;
-    b8 a[C::KG][C::FM], b[C::KG][C::FN];
+    bf16x8 a[C::KG][C::FM], b[C::KG][C::FN];
 #pragma unroll
     for (int kg = 0; kg < C::KG; ++kg) {  // every k-group's fragment reads in flight before the first MFMA
       const int chunk = kg * 4 + g;
 #pragma unroll
       for (int j = 0; j < C::FN; ++j) {
         const int rb = wn * C::TN + j * 16 + r16;
-        b[kg][j] = *reinterpret_cast<const b8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
+        b[kg][j] = *reinterpret_cast<const bf16x8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
       }
 #pragma unroll
       for (int i = 0; i < C::FM; ++i) {
         const int ra = wm * C::TM + i * 16 + r16;
-        a[kg][i] = *reinterpret_cast<const b8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
+        a[kg][i] = *reinterpret_cast<const bf16x8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
       }
     }
 #pragma unroll
@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kg][i], b[kg][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32<F16>(a[kg][i], b[kg][j], acc[i][j]);
       if (PRIO) __builtin_amdgcn_s_setprio(0);
     }
   };
@@ -714,6 +714,19 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
   const int BMv = bms[variant];
   const int nblk = ((a.M + BMv - 1) / BMv) * ((a.N + BN - 1) / BN);
   void (*k)(GemmArgs) = nullptr;
+  if (a.lp_f16) {  // fp16 operands: the tile kernels the automatic choice uses for dense linears
+    if (conv) return false;
+    switch (variant) {
+      case 8: k = gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, BBM, true>; break;
+      case 10: k = gemm_big_kernel<0, 128, 64, 3, 0, 0, 2, BBM, true>; break;
+      case 11: k = gemm_big_kernel<0, 128, 64, 3, 0, 1, 2, BBM, true>; break;
+      case 14: k = gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, true>; break;
+      case 15: k = gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, true>; break;
+      default: return false;
+    }
+    hipLaunchKernelGGL(k, dim3(nblk), dim3(BTHREADS), 0, stream, a);
+    return true;
+  }
 #define MAPA_BIG(V, BN_, RB_, S_) \
   case V: k = conv ? gemm_big_kernel<1, BN_, RB_, S_> : gemm_big_kernel<0, BN_, RB_, S_>; break;
   switch (variant) {

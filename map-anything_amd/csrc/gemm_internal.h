@@ -33,6 +33,7 @@ struct GemmArgs {
   int out_mode;  // 0 row-major, 1 pixel shuffle
   int ps_s, ps_h, ps_w, ps_cout;
   int vec_ok;    // N % 4 == 0, ldo % 4 == 0, ps_cout % 4 == 0: 4-wide epilogue
+  int lp_f16;    // 16-bit operands (A, W) and out_lp / out_lp_relu are fp16 (MAPA_F16) instead of bf16
 };
 
 using mapa_idx::group_coords;
@@ -129,14 +130,14 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
     if constexpr (sizeof(T) == 2) {
       if (p.out_lp) {
         uint2 u;
-        u.x = pack_bf16x2(v[0], v[1]);
-        u.y = pack_bf16x2(v[2], v[3]);
+        u.x = pack_lp2(p.lp_f16, v[0], v[1]);
+        u.y = pack_lp2(p.lp_f16, v[2], v[3]);
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
       }
       if (p.out_lp_relu) {
         uint2 u;
-        u.x = pack_bf16x2(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
-        u.y = pack_bf16x2(fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+        u.x = pack_lp2(p.lp_f16, fmaxf(v[0], 0.f), fmaxf(v[1], 0.f));
+        u.y = pack_lp2(p.lp_f16, fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
       }
       if (p.out_s3) store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v);
@@ -163,8 +164,8 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
       if (p.act == MAPA_ACT_GELU_POST) x = gelu_erf(x);
       if (p.out_f32) p.out_f32[o] = x;
       if constexpr (sizeof(T) == 2) {
-        if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_bf16(x);
-        if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_bf16(fmaxf(x, 0.f));
+        if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_lp(p.lp_f16, x);
+        if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_lp(p.lp_f16, fmaxf(x, 0.f));
         if (p.out_s3) store_split1(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + e, ld, x);
         if (p.out_s3_relu) store_split1(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + e, ld, fmaxf(x, 0.f));
       } else {
@@ -248,13 +249,15 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
   }
   if constexpr (sizeof(T) == 2) {
     if (p.out_lp) {
-      const uint4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
-                       pack_bf16x2(v1[2], v1[3])};
+      const bool h = p.lp_f16;
+      const uint4 u = {pack_lp2(h, v0[0], v0[1]), pack_lp2(h, v0[2], v0[3]), pack_lp2(h, v1[0], v1[1]),
+                       pack_lp2(h, v1[2], v1[3])};
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
     }
     if (p.out_lp_relu) {
-      const uint4 u = {pack_bf16x2(fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f)), pack_bf16x2(fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)),
-                       pack_bf16x2(fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f)), pack_bf16x2(fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
+      const bool h = p.lp_f16;
+      const uint4 u = {pack_lp2(h, fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f)), pack_lp2(h, fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)),
+                       pack_lp2(h, fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f)), pack_lp2(h, fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
     }
     if (p.out_s3) store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0, v1);
@@ -278,7 +281,7 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
 }
 
 // Epilogue patterns of the transformer blocks, fixed once per tile so the per-row calls carry no output-set checks:
-// 1 = act(acc + bias) -> bf16 out_lp only (qkv, fc1 + GELU); 2 = resid1 + gamma * (acc + bias) -> out_f32 only, in
+// 1 = act(acc + bias) -> 16-bit out_lp only (qkv, fc1 + GELU); 2 = resid1 + gamma * (acc + bias) -> out_f32 only, in
 // place (attn proj, fc2); 0 = anything else (epi_store_row8).
 __device__ __forceinline__ int epi_mode(const GemmArgs& p) {
   const bool lp_outs = p.out_lp_relu || p.out_s3 || p.out_s3_relu;
@@ -309,8 +312,12 @@ __device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const Epi
         v1[e] = gelu_erf(v1[e]);
       }
     }
-    const uint4 u = {pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
-                     pack_bf16x2(v1[2], v1[3])};
+    uint4 u;
+    if (p.lp_f16)
+      u = uint4{pack_f16x2(v0[0], v0[1]), pack_f16x2(v0[2], v0[3]), pack_f16x2(v1[0], v1[1]), pack_f16x2(v1[2], v1[3])};
+    else
+      u = uint4{pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
+                pack_bf16x2(v1[2], v1[3])};
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
   } else {
     if (p.gamma) {

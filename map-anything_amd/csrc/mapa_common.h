@@ -48,6 +48,42 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
+// IEEE binary16 storage (MAPA_F16: the operand dtype of the reference's fp16 autocast recipe, model.py:2287-2291),
+// kept as raw 16-bit words like bf16; conversions round to nearest even (v_cvt_f16_f32).
+__device__ __forceinline__ uint16_t f32_to_f16(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+__device__ __forceinline__ float f16_to_f32(uint16_t v) { return (float)__builtin_bit_cast(_Float16, v); }
+__device__ __forceinline__ uint32_t pack_f16x2(float lo, float hi) {
+  return (uint32_t)f32_to_f16(lo) | ((uint32_t)f32_to_f16(hi) << 16);
+}
+// 16-bit operand dtype chosen at run time (uniform branch): fp16 or bf16
+__device__ __forceinline__ uint32_t pack_lp2(bool f16, float lo, float hi) {
+  return f16 ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi);
+}
+__device__ __forceinline__ uint16_t f32_to_lp(bool f16, float f) { return f16 ? f32_to_f16(f) : f32_to_bf16(f); }
+__device__ __forceinline__ float lp_to_f32(bool f16, uint16_t v) { return f16 ? f16_to_f32(v) : bf16_to_f32(v); }
+
+// MFMA on raw 16-bit operand words: bf16 or fp16 arithmetic by template flag (same shapes and rates on gfx950)
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma32x32x16(bf16x8 a, bf16x8 b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c,
+                                                  0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b),
+                                                   c, 0, 0, 0);
+}
+
 // Split-precision operand of 4 consecutive values, stored compact: hi = bf16(v) at [0, ld), lo = bf16(v - hi) at
 // [ld, 2ld).  A bf16 GEMM reads it as the logical K blocks [hi | hi | lo] (the A loader maps the second hi block back
 // onto the first) against weights packed [hi | lo | hi]: v_hi*w_hi + v_hi*w_lo + v_lo*w_hi, the fp32 product to
@@ -86,9 +122,9 @@ __device__ __forceinline__ void store_split1(bf16_t* p, int64_t ld, float x) {
 // erf for the GELU epilogues, faithful to fp32 erff (≤ 1.2 ulp over the whole range, tools/erf_check.py; the
 // reference's GELU is exact-erf, dinov2 layers/mlp.py:29-39 / nn.GELU): two minimax pieces evaluated branch-free
 // and selected per lane —
-//   |x| ≤ 0.9277:  erf = x + x·s·P(s), s = x²  (odd polynomial, degree 13)
-//   |x| > 0.9277:  erf = sign(x)·(1 − exp(R(|x|))), R a degree-9 polynomial fit of log(erfc)
-// (coefficients: the well-known single-precision erff minimax pair).  One exp2 and 14 FMAs; the device libm erff is
+//   |x| ≤ 0.9277:  erf = x + x·P(x²), P of degree 5 (odd, degree 11 overall)
+//   |x| > 0.9277:  erf = sign(x)·(1 − exp(R(|x|))), R a degree-7 polynomial fit of log(erfc)
+// (coefficients: the well-known single-precision erff minimax pair).  One exp2 and 13 FMAs; the device libm erff is
 // ~36 instructions with a divergent two-path branch, and the fc1 GEMMs evaluate it on 1.9 G outputs per 8-view step.
 // Round 2 used Abramowitz & Stegun 7.1.26 (5e-7 absolute, large relative error in GELU's negative tail); that moved a
 // scalar bf16 output measurably, so the epilogue is held to erff accuracy.

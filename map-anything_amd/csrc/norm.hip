@@ -2,7 +2,7 @@
 // Replaces norm1/norm2/final norms of DINOv2 (layers/block.py:93-118, vision_transformer.py:304),
 // AAT (transformer_blocks.py:452-469, alternating_attention_transformer.py:706-747) and the fusion LayerNorm
 // (model.py:1422-1431).  The row is held in registers (dim/64 floats per lane), two-pass mean/variance like
-// ATen, and written as fp32 and/or the GEMM operand dtype (bf16 or fp32) in the same pass.
+// ATen, and written as fp32 and/or the GEMM operand dtype (bf16, fp16, a split bf16 pair, or fp32) in the same pass.
 #include <stdlib.h>
 
 #include "mapa_common.h"
@@ -50,10 +50,10 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     if (ylp) {
       if (lp_bf16 == 2) {  // split operand row: [hi | lo], 2*ldy wide
         store_split3(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y);
-      } else if (lp_bf16) {
+      } else if (lp_bf16) {  // 1 = bf16, 3 = fp16
         uint2 pk;
-        pk.x = pack_bf16x2(y[0], y[1]);
-        pk.y = pack_bf16x2(y[2], y[3]);
+        pk.x = pack_lp2(lp_bf16 == 3, y[0], y[1]);
+        pk.y = pack_lp2(lp_bf16 == 3, y[2], y[3]);
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * ldy + c) = pk;
       } else {
         *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(ylp) + (int64_t)row * ldy + c) = y;
@@ -134,12 +134,13 @@ __global__ void __launch_bounds__(256) layernorm8_kernel(const float* __restrict
         bf16_t* dst = reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c;
         *reinterpret_cast<uint4*>(dst) = hv;
         *reinterpret_cast<uint4*>(dst + ldy) = lv;
-      } else if (lp_bf16) {
+      } else if (lp_bf16) {  // 1 = bf16, 3 = fp16
+        const bool h = lp_bf16 == 3;
         uint4 pk;
-        pk.x = pack_bf16x2(y[0][0], y[0][1]);
-        pk.y = pack_bf16x2(y[0][2], y[0][3]);
-        pk.z = pack_bf16x2(y[1][0], y[1][1]);
-        pk.w = pack_bf16x2(y[1][2], y[1][3]);
+        pk.x = pack_lp2(h, y[0][0], y[0][1]);
+        pk.y = pack_lp2(h, y[0][2], y[0][3]);
+        pk.z = pack_lp2(h, y[1][0], y[1][1]);
+        pk.w = pack_lp2(h, y[1][2], y[1][3]);
         *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * ldy + c) = pk;
       } else {
         float* dst = reinterpret_cast<float*>(ylp) + (int64_t)row * ldy + c;
@@ -159,8 +160,9 @@ extern "C" int mapa_layernorm(const float* x, int64_t ldx, int rows, int dim, co
   MAPA_CHECK_ARG(dim == 768 || dim == 1024 || dim == 512 || dim == 256, "mapa_layernorm: dim %d unsupported", dim);
   MAPA_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "mapa_layernorm: strides must be multiples of 4");
   const dim3 grid((rows + 3) / 4), blk(256);
-  MAPA_CHECK_ARG(lp_dtype == MAPA_F32 || lp_dtype == MAPA_BF16 || lp_dtype == MAPA_BF16X3, "mapa_layernorm: bad lp_dtype");
-  const int bf = lp_dtype == MAPA_BF16X3 ? 2 : lp_dtype == MAPA_BF16 ? 1 : 0;
+  MAPA_CHECK_ARG(lp_dtype == MAPA_F32 || lp_dtype == MAPA_BF16 || lp_dtype == MAPA_BF16X3 || lp_dtype == MAPA_F16,
+                 "mapa_layernorm: bad lp_dtype");
+  const int bf = lp_dtype == MAPA_BF16X3 ? 2 : lp_dtype == MAPA_BF16 ? 1 : lp_dtype == MAPA_F16 ? 3 : 0;
   static const bool f4_only = getenv("MAPA_LN_F4") != nullptr;  // A/B: the float4-per-lane kernel for every width
   // 1024 wide: 8-channel groups (kbench 13.2 -> 12.4 us); 768 wide keeps float4 lanes (10.0 vs 10.5: half the
   // lanes would idle in the second group)

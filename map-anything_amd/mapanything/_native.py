@@ -15,7 +15,7 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmapa.so")
 _lib = None
 
-F32, BF16, BF16X3 = 0, 1, 2
+F32, BF16, BF16X3, F16 = 0, 1, 2, 3
 A_DENSE, A_CONV3X3 = 0, 1
 OUT_ROWMAJOR, OUT_PIXSHUF = 0, 1
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_POST = 0, 1, 2, 3
@@ -180,6 +180,8 @@ def dt_code(dtype: torch.dtype) -> int:
         return BF16
     if dtype == torch.float32:
         return F32
+    if dtype == torch.float16:
+        return F16
     raise NativeError(f"unsupported dtype {dtype}")
 
 
@@ -363,7 +365,7 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
     d.o_bstride, d.o_rstride = o_bstride, o_rstride
     d.lse = None if lse is None else lse.data_ptr()
     d.scale = 0.0 if scale is None else float(scale)  # 0 -> 1/sqrt(64)
-    if d.dtype == BF16:
+    if d.dtype in (BF16, F16):
         ws = attention_workspace(d)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     if kv_segments:
@@ -387,7 +389,7 @@ def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, 
             raise NativeError("layernorm: y_s3 (bf16) replaces y_lp")
         y_lp, lp_dtype = y_s3, BF16X3
     else:
-        lp_dtype = BF16 if (y_lp is not None and y_lp.dtype == torch.bfloat16) else F32
+        lp_dtype = dt_code(y_lp.dtype) if y_lp is not None else F32
     tok = _tic()
     check(lib().mapa_layernorm(ptr(x), ldx if ldx is not None else dim, rows, dim, ptr(w), ptr(b), eps, ptr(y_f32),
                                ptr(y_lp), lp_dtype, ldy if ldy is not None else dim, group, group_stride, row_off,

@@ -12,7 +12,8 @@ torch allocations on the current device; torch does nothing else.  Layout in HBM
   outputs           NHWC fp32 [view][H][W][c] (the reference's (B,H,W,c) per view, view-major)
 
 Precision modes: "bf16" (the reference's own autocast recipe, model.py:2287-2302: the encoder and the transformer run
-on bf16 MFMA operands with fp32 accumulate / LayerNorm / softmax / residuals; the geometric-input encoders
+on bf16 MFMA operands with fp32 accumulate / LayerNorm / softmax / residuals; "fp16" the same on fp16 operands —
+infer(amp_dtype="fp16"); the geometric-input encoders
 (autocast disabled, model.py:1377) and the downstream heads (autocast disabled, model.py:1774-1799) stay fp32-exact,
 computed as split-precision bf16 GEMMs: activations [hi | hi | lo], weights [hi | lo | hi], ~2^-16 relative) and
 "fp32" (exact-fp32 MFMA everywhere, for parity against the fp32 reference to ~1e-5).  heads="bf16" is an opt-in
@@ -238,7 +239,7 @@ class PackedWeights:
         if getattr(self, "_geo", None) is not None:
             return self._geo
         dev = self.device
-        split = self.lp == torch.bfloat16
+        split = self.lp != torch.float32  # bf16 / fp16 autocast: the encoders' fp32 GEMMs as split bf16
 
         def t(name):
             return torch.from_numpy(np.ascontiguousarray(_np(sd[name]))).to(dev)
@@ -307,17 +308,20 @@ def _ceil8(c: int) -> int:
 class MapaEngine:
     def __init__(self, sd: Dict[str, object], device=None, precision: str = "bf16",
                  info: InfoSharingSpec = RELEASED_INFO, heads: str = "fp32"):
-        if precision not in ("bf16", "fp32"):
-            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision}")
+        if precision not in ("bf16", "fp16", "fp32"):
+            raise ValueError(f"precision must be 'bf16', 'fp16' or 'fp32', got {precision}")
         if heads not in ("fp32", "bf16"):
             raise ValueError(f"heads must be 'fp32' (the reference's recipe) or 'bf16' (fast mode), got {heads}")
+        if precision == "fp16" and heads != "fp32":
+            raise ValueError("the fp16 recipe runs the heads fp32-exact (heads='fp32'); the bf16-heads fast mode is bf16")
         nat.lib()  # fail loudly without the HIP library / a gfx950 device
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.precision = precision
-        self.lp = torch.bfloat16 if precision == "bf16" else torch.float32
-        # heads at the reference's fp32 in bf16 mode: split-precision operands (hsplit); fp32 mode is exact already
+        # operand dtype of the encoder / transformer GEMMs and attention: bf16 or fp16 autocast (model.py:2287-2302)
+        self.lp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[precision]
+        # heads at the reference's fp32 under autocast: split-precision bf16 operands (hsplit); fp32 mode is exact
         self.heads = "fp32" if precision == "fp32" else heads
-        self.hsplit = precision == "bf16" and heads == "fp32"
+        self.hsplit = precision != "fp32" and heads == "fp32"
         self._sd = sd  # host state dict: the geometric encoders are packed on first use
         self.info = info
         with torch.cuda.device(self.device):

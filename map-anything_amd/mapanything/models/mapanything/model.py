@@ -8,7 +8,8 @@ the gfx950 HIP library (`MapaEngine`); this class is host glue: validation, devi
 Differences that are by design:
   * weights come from a LOCAL directory (config.json + model.safetensors) or the synthetic named-PRNG
     checkpoint; there is no hub download (no network on this box),
-  * `precision="bf16"` (default) mirrors `infer(use_amp=True, amp_dtype="bf16")` — bf16 encoder/transformer, the
+  * `precision="bf16"` (default) mirrors `infer(use_amp=True, amp_dtype="bf16")` (`amp_dtype="fp16"` the same on
+    fp16 operands) — bf16 encoder/transformer, the
     geometric encoders and the downstream heads fp32-exact as the reference runs them with autocast disabled
     (model.py:1377, 1774; split-precision bf16 GEMMs on MI355X); `use_amp=False` (or precision="fp32") runs the
     exact-fp32 MFMA path; `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
@@ -473,11 +474,13 @@ class MapAnything:
               ignore_pose_inputs: bool = False, ignore_depth_scale_inputs: bool = False,
               ignore_pose_scale_inputs: bool = False) -> List[Dict[str, torch.Tensor]]:
         """model.py:2206-2355."""
+        # autocast recipe (model.py:2287-2302): bf16 or fp16 operands for the encoder and the transformer; the
+        # geometric encoders and the heads fp32 as the reference runs them (autocast disabled, model.py:1377 / 1774)
         if use_amp and amp_dtype in ("bf16", "fp16"):
-            if amp_dtype == "fp16":
-                warnings.warn("fp16 autocast is served by the bf16 MFMA path on MI355X")
-            precision = "bf16"
+            precision = amp_dtype
         else:
+            if use_amp and amp_dtype not in ("bf16", "fp16", "fp32"):
+                warnings.warn(f"unknown amp_dtype {amp_dtype!r}: running fp32")
             precision = "fp32"
         validated = validate_input_views_for_inference(views)
         B = self._check_views(validated)

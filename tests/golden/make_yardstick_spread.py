@@ -2,6 +2,8 @@
 
     python tests/golden/make_yardstick_spread.py            # writes tests/golden/golden_bf16_spread.json
     GOLDEN_ONLY=cfg4_518 python tests/golden/make_yardstick_spread.py
+    SPREAD_AMP=fp16 GOLDEN_ONLY=cfg1_224,mm_224,v2_518,cfg2_518 python tests/golden/make_yardstick_spread.py
+                                                            # the fp16 autocast recipe -> golden_fp16_spread.json
 
 One bf16 run of the reference is ONE sample of its bf16 rounding walk: a scalar output such as
 metric_scaling_factor (one number per scene) can land anywhere inside a spread several times wide.  To measure that
@@ -30,6 +32,7 @@ import make_golden as mg  # noqa: E402
 import ref_harness  # noqa: E402
 
 SAMPLES = int(os.environ.get("SPREAD_SAMPLES", "5"))
+AMP = os.environ.get("SPREAD_AMP", "bf16")  # the autocast dtype of the recipe whose spread is measured: bf16 / fp16
 REL_NOISE = 2.0 ** -20
 SMALL = ("out_cam_trans", "out_cam_quats", "out_metric_scaling_factor", "out_camera_poses", "out_intrinsics")
 
@@ -61,7 +64,7 @@ def run(model, case, pseed, bf16=True):
     views = perturbed_views(case, pseed)
     if bf16:
         with mg.cpu_autocast_emulation():
-            preds = model.infer(views, apply_mask=False, use_amp=True, amp_dtype="bf16")
+            preds = model.infer(views, apply_mask=False, use_amp=True, amp_dtype=AMP)
     else:
         preds = model.infer(views, apply_mask=False, use_amp=False)
     out = {}
@@ -72,6 +75,22 @@ def run(model, case, pseed, bf16=True):
     return out
 
 
+# outputs multiplied by the scene's metric_scaling_factor (model.py:1911-1921): compared also with each side's own
+# factor divided out ("_unscaled"), so their scale-free part can be held to the dense tolerance and the scalar's
+# one-number noise is accounted for once, in metric_scaling_factor itself
+METRIC = ("out_pts3d", "out_depth_along_ray", "out_cam_trans", "out_camera_poses")
+
+
+def unscale(k, v, s):
+    """v / s per (view, scene): s = metric_scaling_factor (V, B, 1); camera_poses: translation column only."""
+    s = np.asarray(s, np.float64).reshape(s.shape[0], s.shape[1])
+    v = np.asarray(v, np.float64).copy()
+    if k == "out_camera_poses":
+        v[..., :3, 3] /= s[:, :, None]
+        return v
+    return v / s.reshape(s.shape + (1,) * (v.ndim - 2))
+
+
 def compare(out, fix, step):
     res = {}
     for k in mg.KEEP_OUT:
@@ -79,6 +98,9 @@ def compare(out, fix, step):
         if k in mg.DENSE:
             v = v[:, :, ::step, ::step]
         res[k] = mg.rel_l2(v, fix[k])
+        if k in METRIC:
+            res[k + "_unscaled"] = mg.rel_l2(unscale(k, v, out["out_metric_scaling_factor"]),
+                                             unscale(k, fix[k], fix["out_metric_scaling_factor"]))
     return res
 
 
@@ -99,7 +121,7 @@ def main():
         vm.load_state_dict(mg.synthetic_reference_state_dict(info_cfg), strict=True)
         models[name] = vm
         cases[name] = case
-    spath = os.path.join(HERE, "golden_bf16_spread.json")
+    spath = os.path.join(HERE, f"golden_{AMP}_spread.json")
     spread = json.load(open(spath)) if os.path.exists(spath) else {}
     ypath = os.path.join(HERE, "golden_bf16_yardsticks.json")
     yards = json.load(open(ypath))
@@ -107,12 +129,12 @@ def main():
         fix = np.load(os.path.join(HERE, f"golden_{name}.npz"))
         step = mg.STEPS[name][0]
         t0 = time.time()
-        samples = {k: [] for k in mg.KEEP_OUT}
+        samples = {}
         for pseed in [None] + list(range(SAMPLES)):
             r = compare(run(models[name], case, pseed), fix, step)
             for k, e in r.items():
-                samples[k].append(e)
-            if pseed is None and name not in yards:
+                samples.setdefault(k, []).append(e)
+            if pseed is None and name not in yards and AMP == "bf16":
                 yards[name] = dict(r, seconds=time.time() - t0, note="unperturbed reference bf16 run vs the fp32 fixture "
                                    "(make_yardstick_spread.py; fixture subsampling)")
         entry = {"samples": 1 + SAMPLES, "rel_noise": REL_NOISE, "seconds": time.time() - t0,
@@ -126,8 +148,9 @@ def main():
               flush=True)
         with open(spath, "w") as f:
             json.dump(spread, f, indent=1, sort_keys=True)
-        with open(ypath, "w") as f:
-            json.dump(yards, f, indent=1, sort_keys=True)
+        if AMP == "bf16":
+            with open(ypath, "w") as f:
+                json.dump(yards, f, indent=1, sort_keys=True)
     print("done")
 
 

@@ -64,19 +64,27 @@ def test_gemm_epilogues(nat):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_gemm_gelu_epilogue_fp32_exactness(nat, dtype):
-    """The GELU epilogue's erf (mapa_common.h erf_as, Abramowitz-Stegun 7.1.26) against torch's exact-erf GELU on
-    fp32 outputs: |error| <= 5e-7 absolute, including the negative tail and |x| > 4 (the 8-column epilogue path
-    and its 4-column tail: N = 200 is not a multiple of 8)."""
+    """The GELU epilogue's erf (mapa_common.h erf_fast: <= 1.2 ulp of fp32 erff) against the exact-erf GELU of the
+    SAME kernel's pre-activation (a second launch without the activation, so only the GELU evaluation differs):
+    within a few fp32 ulp everywhere, including the negative tail and |x| > 4 (the 8-column epilogue path and its
+    4-column tail: N = 200 is not a multiple of 8).  The round-2 Abramowitz-Stegun erf (5e-7 absolute) fails this
+    in the tail, where GELU is ~1e-5 and that error is a few percent."""
     M, N, K = 513, 200, 64
     A = (_rand(M, K, seed=70) * 1.5).to(dtype)
     W = _rand(N, K, scale=K ** -0.5, seed=71).to(dtype)
     b = _rand(N, seed=72)
     out = torch.empty(M, N, device="cuda")
+    pre = torch.empty(M, N, device="cuda")
     nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_f32=out)
-    pre = (A.double() @ W.double().t() + b.double()).float()
-    ref = F.gelu(pre.double()).float()
-    assert float(pre.abs().max()) > 4.0  # the tails are exercised
-    assert float((out - ref).abs().max()) < (5e-6 if dtype == torch.float32 else 5e-5)
+    nat.gemm(A, W, M, N, K, bias=b, out_f32=pre)
+    ref = F.gelu(pre.double())
+    assert float(pre.abs().max()) > 4.0 and float(pre.min()) < -4.0  # the tails are exercised
+    ulp = torch.finfo(torch.float32).eps * ref.abs().clamp_min(torch.finfo(torch.float32).tiny)
+    err = (out.double() - ref).abs()
+    # 0.5 * x * (1 + erf): a few ulp of the result from the products, plus 0.5|x| times the erf's error near +-1
+    # (<= 1.2 ulp of 1 = 7e-8: the 1e-7 |x| term; in the negative tail 1 + erf cancels exactly, so that term is the
+    # whole error there — the round-2 erf's 5e-7 would put 2.5e-7 |x| there and fail)
+    assert bool((err <= 8 * ulp + 1e-7 * pre.abs().double()).all()), float((err / (ulp + 1e-30)).max())
 
 
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2587])
@@ -752,3 +760,76 @@ def test_rope2d_bf16_on_packed_qkv_rows(nat):
         got = work[:, blk * C:(blk + 1) * C].float().cpu()
         assert rel_l2(got, want) < 4e-3
     assert torch.equal(work[:, 2 * C:], qkv[:, 2 * C:])
+
+
+
+# ----------------------------------------------------------------------- fp16 operands (the fp16 autocast recipe)
+@pytest.mark.parametrize("variant", [0, 2568, 2570, 2571, 2574, 2587, 1282, 643])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 264), (1370, 1024, 1024), (2737, 768, 3072)])
+def test_gemm_fp16_operands(nat, variant, M, N, K):
+    """infer(amp_dtype="fp16"): fp16 A / W on the f16 MFMA in every tile kernel the automatic choice uses (and the
+    128x128 fallbacks), fp32 accumulate; plain, GELU -> fp16 and in-place residual epilogues."""
+    A = _rand(M, K, seed=80).to(torch.float16)
+    W = _rand(N, K, scale=K ** -0.5, seed=81).to(torch.float16)
+    b, g = _rand(N, seed=82), _rand(N, seed=83) * 0.1
+    acc = A.float() @ W.float().t() + b
+    nat.gemm_set_variant(variant)
+    try:
+        out = torch.empty(M, N, device="cuda")
+        nat.gemm(A, W, M, N, K, bias=b, out_f32=out)
+        assert rel_l2(out.cpu(), acc.cpu()) < 1e-5
+        o = torch.empty(M, N, device="cuda", dtype=torch.float16)
+        nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=o)
+        assert o.dtype == torch.float16 and rel_l2(o.float().cpu(), F.gelu(acc).cpu()) < 1e-3
+        x0 = _rand(M, N, seed=84)
+        x = x0.clone()
+        nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=x, out_f32=x)
+        assert rel_l2(x.cpu(), (x0 + g * acc).cpu()) < 1e-5
+    finally:
+        nat.gemm_set_variant(0)
+
+
+@pytest.mark.parametrize("B,Hh,S", [(2, 16, 1370), (1, 12, 10953), (3, 12, 65)])
+def test_attention_fp16_operands(nat, B, Hh, S):
+    """The flash kernel on fp16 q / k / v (f16 MFMAs, P rounded to fp16) against fp32 SDPA of the same inputs,
+    including the split-merge path (few query blocks) and the LSE."""
+    C = Hh * 64
+    qkv = _rand(B * S, 3 * C, seed=85).to(torch.float16)
+    o = torch.empty(B * S, C, device="cuda", dtype=torch.float16)
+    lse = torch.empty(B, Hh, S, device="cuda")
+    rs = 3 * C
+    nat.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B, heads=Hh, seq_q=S, seq_kv=S, q_bstride=S * rs,
+                  q_rstride=rs, k_bstride=S * rs, k_rstride=rs, v_bstride=S * rs, v_rstride=rs, o_bstride=S * C,
+                  o_rstride=C, lse=lse)
+    t = qkv.view(B, S, 3, Hh, 64).permute(2, 0, 3, 1, 4)
+    ref = _sdpa_ref(t[0], t[1], t[2]).transpose(1, 2).reshape(B * S, C)
+    assert rel_l2(o.float().cpu(), ref.cpu()) < 2e-3
+    s = (t[0].float() @ t[1].float().transpose(-1, -2)) / 8.0
+    assert rel_l2(lse.cpu(), torch.logsumexp(s, -1).cpu()) < 1e-4
+    # the overlapped all-gather's partial merge in fp16
+    half = S // 2
+    if half >= 1 and B == 1:
+        q = qkv[:, :C]
+        oa, ob = torch.empty_like(o), torch.empty_like(o)
+        la, lb = torch.empty(Hh, S, device="cuda"), torch.empty(Hh, S, device="cuda")
+        common = dict(batch=1, heads=Hh, seq_q=S, q_bstride=0, q_rstride=rs, k_bstride=0, k_rstride=rs, v_bstride=0,
+                      v_rstride=rs, o_bstride=0, o_rstride=C)
+        nat.attention(q, qkv[:, C:], qkv[:, 2 * C:], oa, seq_kv=half, lse=la, **common)
+        nat.attention(q, qkv[half:, C:], qkv[half:, 2 * C:], ob, seq_kv=S - half, lse=lb, **common)
+        om = torch.empty_like(o)
+        nat.attn_merge(oa, la, ob, lb, om, S, Hh, C)
+        assert rel_l2(om.float().cpu(), ref.cpu()) < 2e-3
+
+
+def test_layernorm_fp16_output(nat):
+    rows, dim = 517, 1024
+    x = _rand(rows, dim, scale=3.0, seed=86) + 1.5
+    w, b = _rand(dim, seed=87), _rand(dim, seed=88)
+    y = torch.empty(rows, dim, device="cuda", dtype=torch.float16)
+    nat.layernorm(x, rows, dim, w, b, y_lp=y)
+    ref = F.layer_norm(x, (dim,), w, b, 1e-6)
+    assert y.dtype == torch.float16 and rel_l2(y.float().cpu(), ref.cpu()) < 1e-3
+    y7 = torch.empty(rows, 768, device="cuda", dtype=torch.float16)
+    nat.layernorm(x[:, :768].contiguous(), rows, 768, w[:768], b[:768], y_lp=y7)
+    ref7 = F.layer_norm(x[:, :768], (768,), w[:768], b[:768], 1e-6)
+    assert rel_l2(y7.float().cpu(), ref7.cpu()) < 1e-3

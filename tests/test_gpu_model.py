@@ -6,10 +6,15 @@ Tolerances (rel-L2 per output):
   * precision "bf16" (the reference's own autocast recipe: bf16 encoder / transformer, fp32 geometric encoders and
     heads): bounded per case by the SPREAD of the reference's own bf16-vs-fp32 deviation on that case
     (tests/golden/golden_bf16_spread.json, make_yardstick_spread.py: the reference's bf16 recipe on the case's inputs
-    and on 5 copies perturbed by 2^-20 relative noise, each against the fp32 fixture) — BF16_FACTOR x its max for the
-    dense per-pixel outputs, SMALL_FACTOR x its max for the per-view vectors and the scalar scale (<= 16 numbers per
-    view: one rel-L2 is one sample of the rounding walk, the samples of one case spread ~2x), floor BF16_FLOOR; the
-    achieved rel-L2, its ratio to the case's unperturbed yardstick and to the spread max are printed (pytest -s);
+    and on 5 copies perturbed by 2^-20 relative noise, each against the fp32 fixture).  The metric scale s (ONE number
+    per scene) is a single draw of a wide distribution: over the 12 reference cases our deviation / the reference's
+    unperturbed one spans 0.04 - 2.2 (geometric mean ~0.9), and the reference's own perturbed draws of one case
+    spread up to 40x — so it gets SCALE_FACTOR x its spread max, and the outputs it multiplies (pts3d,
+    depth_along_ray, cam_trans, the pose translations: model.py:1911-1921) are checked twice: with each side's own s
+    divided out at the dense / small tolerance below, and raw at that bound plus the scale's.  Other dense per-pixel
+    outputs: BF16_FACTOR x the spread max; per-view vectors (<= 16 numbers per view): SMALL_FACTOR x; floor
+    BF16_FLOOR.  Every achieved rel-L2, its ratio to the case's unperturbed reference deviation and to the spread max
+    are printed (pytest -s);
   * head_precision "bf16" (opt-in fast mode, NOT the reference's recipe): 3x the yardstick, floor 2e-3.
 """
 
@@ -25,20 +30,40 @@ from conftest import GOLDEN, rel_l2
 pytestmark = pytest.mark.gpu
 
 from tests_helpers import CASES, make_views
-BF16_FACTOR, BF16_FLOOR, SMALL_FACTOR = 1.5, 1e-3, 2.0
+BF16_FACTOR, BF16_FLOOR, SMALL_FACTOR, SCALE_FACTOR = 1.5, 1e-3, 2.0, 3.0
 SMALL_KEYS = ("cam_trans", "cam_quats", "metric_scaling_factor", "camera_poses", "intrinsics")
+METRIC_KEYS = ("pts3d", "depth_along_ray", "cam_trans", "camera_poses")  # multiplied by metric_scaling_factor
 
 
 def _spread(name):
     return json.load(open(os.path.join(GOLDEN, "golden_bf16_spread.json")))[name]["max"]
 
 
-def _bf16_tol(name):
-    """Per-case bound from the case's own measured spread (no cross-case borrowing)."""
-    smax = _spread(name)
+def _unscale(k, v, s):
+    """v / s per (view, scene); camera_poses: the translation column only (make_yardstick_spread.unscale)."""
+    s = np.asarray(s, np.float64).reshape(s.shape[0], s.shape[1])
+    v = np.asarray(v, np.float64).copy()
+    if k == "camera_poses":
+        v[..., :3, 3] /= s[:, :, None]
+        return v
+    return v / s.reshape(s.shape + (1,) * (v.ndim - 2))
+
+
+def _bf16_tol(name, spread=None):
+    """Per-case bound from the case's own measured spread (no cross-case borrowing); keys '<k>_unscaled' are the
+    metric outputs with the scene scale divided out."""
+    smax = spread if spread is not None else _spread(name)
+
+    def base(k):
+        return max(BF16_FLOOR, (SMALL_FACTOR if k.split("_unscaled")[0] in SMALL_KEYS else BF16_FACTOR)
+                   * smax[f"out_{k}"])
 
     def tol(k):
-        return max(BF16_FLOOR, (SMALL_FACTOR if k in SMALL_KEYS else BF16_FACTOR) * smax[f"out_{k}"])
+        if k == "metric_scaling_factor":
+            return max(BF16_FLOOR, SCALE_FACTOR * smax["out_metric_scaling_factor"])
+        if k in METRIC_KEYS:
+            return base(k + "_unscaled") + tol("metric_scaling_factor")
+        return base(k)
     return tol
 
 
@@ -67,22 +92,41 @@ def _yard(name="cfg1_224"):
     return json.load(open(os.path.join(GOLDEN, "golden_bf16_yardsticks.json")))[name]
 
 
-def _compare(preds, g, step, tol_fn, yard=None, label="", spread=None):
-    errs = {}
+def _intrinsics_ill_conditioned(preds, min_z=1e-6):
+    """recover_pinhole_intrinsics_from_ray_directions (geometry.py:304-447) fits x = cx + fx * dx/dz on every
+    (H//50, W//50)-th pixel: a ray with |dz| ~ 0 on that grid (a true zero crossing, rounded to 0 or 1e-8 by any
+    implementation) makes the fit arbitrary for the reference and for us alike."""
+    for p in preds:
+        r = p["ray_directions"][0]
+        H, W = r.shape[:2]
+        if float(r[::max(1, H // 50), ::max(1, W // 50), 2].abs().min()) < min_z:
+            return True
+    return False
+
+
+def _compare(preds, g, step, tol_fn, yard=None, label="", spread=None, skip=()):
+    errs, mine_all = {}, {}
     for k in OUT_KEYS:
+        if k in skip:
+            continue
         ref = g[f"out_{k}"]
         mine = torch.stack([p[k].float() for p in preds], 0).cpu().numpy()
         if mine.ndim >= 4 and k not in ("intrinsics", "camera_poses"):
             mine = mine[:, :, ::step, ::step]
         assert mine.shape == ref.shape, (k, mine.shape, ref.shape)
         errs[k] = rel_l2(mine, ref)
+        mine_all[k] = mine
+    if spread is not None:  # the metric outputs with each side's own scene scale divided out
+        for k in METRIC_KEYS:
+            errs[f"{k}_unscaled"] = rel_l2(_unscale(k, mine_all[k], mine_all["metric_scaling_factor"]),
+                                           _unscale(k, g[f"out_{k}"], g["out_metric_scaling_factor"]))
     if yard is not None:
         print(f"\n[{label}] rel-L2 vs fp32 reference (ratio to the reference's own bf16 deviation; to its spread max):")
         for k, e in errs.items():
             y = yard.get(f"out_{k}")
             sm = spread.get(f"out_{k}") if spread else None
             print(f"  {k:28s} {e:.3e}" + (f"  yard {y:.3e}  ratio {e / y:.2f}" if y else "")
-                  + (f"  spread-max {sm:.3e}  ratio {e / sm:.2f}  tol {tol_fn(k):.3e}" if sm else ""))
+                  + (f"  spread-max {sm:.3e}  ratio {e / sm:.2f}" if sm else "") + f"  tol {tol_fn(k):.3e}")
     bad = {k: (e, tol_fn(k)) for k, e in errs.items() if not e < tol_fn(k)}
     assert not bad, f"rel-L2 over tolerance: {bad} (all: {errs})"
     return errs
@@ -321,10 +365,10 @@ def test_info_sharing_variants_match_reference(golden, name):
     preds = m.infer(_views(case), apply_mask=False)
     if name != "aatnoref_224":  # the variant's own measured spread, as for the released config
         _compare(preds, g, step, _bf16_tol(name), _yard(name), f"bf16 {name}", spread=_spread(name))
-    else:  # the reference's own bf16 path fails on this variant: cfg1's spread at 3x, floor 1e-2
+    else:  # the reference's own bf16 path fails on this variant: cfg1's spread-based bound at 2x, floor 1e-2
         sm = _spread("cfg1_224")
-        _compare(preds, g, step, lambda k: max(1e-2, 3.0 * sm[f"out_{k}"]), _yard("cfg1_224"), f"bf16 {name}",
-                 spread=sm)
+        t1 = _bf16_tol("cfg1_224", sm)
+        _compare(preds, g, step, lambda k: max(1e-2, 2.0 * t1(k)), _yard("cfg1_224"), f"bf16 {name}", spread=sm)
     # intermediate taps of the variant's transformer, fp32 engine
     eng = m.engine("fp32")
     imgs = torch.cat([v["img"] for v in _views(case)], 0).cuda()
@@ -410,3 +454,26 @@ def test_serialize_debug_mode_runs_and_matches(model):
         _native.set_serialize(False)
     for k in ("pts3d", "conf", "cam_quats", "metric_scaling_factor"):
         assert torch.equal(a[k], b[k]), k
+
+
+FP16_CASES = ["cfg1_224", "mm_224", "v2_518", "cfg2_518"]
+
+
+@pytest.mark.parametrize("name", FP16_CASES)
+def test_fp16_mode_within_reference_fp16_spread(model, golden, name):
+    """infer(amp_dtype="fp16"): the reference's fp16 autocast recipe (model.py:2287-2291) — fp16 operands for the
+    encoder and the transformer (f16 MFMAs), the geometric encoders and heads fp32 as in the reference — against the
+    fp32 fixture, bounded exactly like the bf16 mode but by the spread of the reference's OWN fp16 recipe on the case
+    (tests/golden/golden_fp16_spread.json, make_yardstick_spread.py SPREAD_AMP=fp16)."""
+    sp = json.load(open(os.path.join(GOLDEN, "golden_fp16_spread.json")))[name]
+    g = golden(name)
+    step = _meta(name)["steps_out_tap_dpt"][0]
+    preds = model.infer(_views(CASES[name]), apply_mask=False, amp_dtype="fp16")
+    assert model.engine("fp16").lp == torch.float16
+    yard = {k: v[0] for k, v in sp["rel_l2"].items()}  # the unperturbed reference fp16 run
+    # v2_518 in fp16: one view's ray at grid pixel (40, 390) crosses z = 0 (|z| 2e-8 .. 0 depending on summation
+    # order), which leaves the intrinsics fit undetermined — skipped only when that is detected
+    skip = ("intrinsics",) if _intrinsics_ill_conditioned(preds) else ()
+    if skip:
+        print(f"\n[fp16 {name}] intrinsics skipped: a ray on the recovery grid has |z| < 1e-6")
+    _compare(preds, g, step, _bf16_tol(name, sp["max"]), yard, f"fp16 {name}", spread=sp["max"], skip=skip)
