@@ -88,30 +88,41 @@ __device__ __forceinline__ void vm_wait(int n) {
   }
 }
 
-// DMA group of K tile kt: its W tile (ring slot kt % S) and, on a slice's first tap, that slice's window (a device
-// function, not a lambda in the kernel: with a lambda the host pass drops the kernel's launch stub)
+// Window image chunk position of channel chunk g (channels 8g..8g+7) of window pixel wp: pos = bswap2(g) ^ bit 2 of
+// wp.  ds_read_b128 serves a wave in four 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, and the same +32),
+// and an A fragment's lanes read 16 consecutive window pixels from an arbitrary start (the tap shift): in every
+// group each pixel residue mod 4 (= its 64-B bank quarter) is read by 4 lanes at pixels P, P+4, P+8, P+12 with
+// chunks {0,1,1,0} or {1,0,0,1} (+2 for the upper half-wave), and this map sends those to 4 distinct 16-B slots for
+// every P — conflict-free (the plain g ^ ((wp >> 2) & 3) of 16 contiguous lanes is 2-way in these groups).
+__device__ __forceinline__ int win_pos(int g, int wp) { return (((g & 1) << 1) | (g >> 1)) ^ ((wp >> 2) & 1); }
+// its inverse: the chunk stored at position pos
+__device__ __forceinline__ int win_chunk(int pos, int wp) { return (((pos & 1) << 1) | (pos >> 1)) ^ (((wp >> 2) & 1) << 1); }
+
+// DMA of K tile kt's W tile into ring slot `slot` (a device function, not a lambda in the kernel: with a lambda the
+// host pass drops the kernel's launch stub)
 template <int BN, int BH>
-__device__ __forceinline__ void halo_stage(const GemmArgs& p, char* wring, char* wins, int kt, int wave,
-                                           const char* const* w_src, const int64_t* wsrc, const bool* wok) {
+__device__ __forceinline__ void stage_w(char* wring, int slot, int wave, const char* const* w_src, int64_t koff) {
+  using C = HCfg<BN, BH>;
+  char* dst = wring + slot * C::WT + wave * 1024;
+#pragma unroll
+  for (int i = 0; i < C::NWG; ++i) __builtin_amdgcn_global_load_lds(w_src[i] + koff, dst + i * 8192, 16, 0, 0);
+}
+// DMA of the input window of 32-channel slice `slice` into window buffer slice & 1
+template <int BN, int BH>
+__device__ __forceinline__ void stage_win(const GemmArgs& p, char* wins, int slice, int wave, const int64_t* wsrc,
+                                          const bool* wok) {
   using C = HCfg<BN, BH>;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const char* abase = reinterpret_cast<const char*>(p.A);
-  char* dst = wring + (kt % C::S) * C::WT + wave * 1024;
+  const int64_t ch = split_col(p, slice * 32);
+  char* wd = wins + (slice & 1) * C::WBYTES + wave * 1024;
 #pragma unroll
-  for (int i = 0; i < C::NWG; ++i)
-    __builtin_amdgcn_global_load_lds(w_src[i] + (int64_t)kt * 64, dst + i * 8192, 16, 0, 0);
-  const int slice = kt / 9;
-  if (kt - slice * 9 == 0) {
-    const int64_t ch = split_col(p, slice * 32);
-    char* wd = wins + (slice & 1) * C::WBYTES + wave * 1024;
-#pragma unroll
-    for (int r = 0; r < C::WROUNDS; ++r)
-      __builtin_amdgcn_global_load_lds(wok[r] ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16, 0, 0);
-  }
+  for (int r = 0; r < C::WROUNDS; ++r)
+    __builtin_amdgcn_global_load_lds(wok[r] ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16, 0, 0);
 }
 
 template <int BN, bool HO = false, int BH = 16>
-__global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(GemmArgs p, HeadOut ho) {
+__global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel(GemmArgs p, HeadOut ho) {
   using C = HCfg<BN, BH>;
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS];
   char* const wring = lds;
@@ -135,7 +146,7 @@ __global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(Gem
   for (int r = 0; r < C::WROUNDS; ++r) {
     const int q = r * HT + tid;
     const int wp = q >> 2, cl = q & 3;
-    const int cs = cl ^ ((wp >> 2) & 3);
+    const int cs = win_chunk(cl, wp);  // LDS position cl holds channel chunk cs
     const int wy = wp / WE, wx = wp - wy * WE;
     const int iy = by * BH - 1 + wy, ix = bx * BW - 1 + wx;
     wok[r] = q < C::WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
@@ -157,40 +168,62 @@ __global__ void __launch_bounds__(HT, (HCfg<BN, BH>::MINB)) conv_halo_kernel(Gem
 
   typedef __bf16 b8 __attribute__((ext_vector_type(8)));
   const int g = lane >> 4, r16 = lane & 15;
-  int b_off[C::FN];
-#pragma unroll
-  for (int j = 0; j < C::FN; ++j) {
-    const int rb = wn * C::TN + j * 16 + r16;
-    b_off[j] = rb * 64 + ((g ^ swz64(rb)) << 4);
-  }
+  // B fragment j of this lane: ring row rb = wn*TN + j*16 + r16; the swizzle depends on bits 2-3 of rb only, so
+  // fragment j sits at b_off + j*1024 (an immediate offset of one address)
+  const int rb0 = wn * C::TN + r16;
+  const int b_off = rb0 * 64 + ((g ^ swz64(rb0)) << 4);
   const int wp0 = (wm * C::FM) * WE + r16;  // window pixel of (block row wm*FM, px = r16) at tap (0, 0)
+  // A fragment of window pixel wp0 + c: byte (wp0 + c)*64 + win_pos(g, wp0 + c)*16, and bit 2 of wp0 + c depends on
+  // c mod 8 only -> a_off[c % 8] + c*64, an immediate offset for every (tap, row) pair
 
+  // K loop: slices of 32 channels, the 9 taps of a slice unrolled, so the tap shift, the vmcnt depth of every step
+  // and which steps stage a window are compile-time constants (one runtime branch: the last slice, which stages no
+  // further W tiles / window past nk).  K tile kt = slice*9 + tap lives in ring slot kt % S (`so`); the DMA group
+  // issued at step kt is W tile kt+S-1 (+ the next slice's window when kt+S-1 starts it).
+  const int nslice = nk / 9;
+  stage_w<BN, BH>(wring, 0, wave, w_src, 0);  // group 0: W tile 0 + slice 0's window (vmcnt retires in issue order)
+  stage_win<BN, BH>(p, wins, 0, wave, wsrc, wok);
 #pragma unroll
-  for (int s0 = 0; s0 < C::S - 1; ++s0)
-    if (s0 < nk) halo_stage<BN, BH>(p, wring, wins, s0, wave, w_src, wsrc, wok);
-  for (int kt = 0; kt < nk; ++kt) {
-    // groups issued after kt's: W tiles kt+1 .. kt+after, plus a window if one of them starts a slice
-    const int after = min(C::S - 2, nk - 1 - kt);
-    const int next9 = (kt / 9 + 1) * 9;
-    vm_wait(C::NWG * after + (next9 <= kt + after ? C::WROUNDS : 0));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
-    __builtin_amdgcn_sched_barrier(0);
-    if (kt + C::S - 1 < nk) halo_stage<BN, BH>(p, wring, wins, kt + C::S - 1, wave, w_src, wsrc, wok);
-    const int slice = kt / 9, tap = kt - slice * 9;
-    const int ky = tap / 3, kx = tap - ky * 3;
-    const char* Ws = wring + (kt % C::S) * C::WT;
-    const char* Win = wins + (slice & 1) * C::WBYTES;
-    b8 b[C::FN];
+  for (int s0 = 1; s0 < C::S - 1; ++s0) stage_w<BN, BH>(wring, s0, wave, w_src, (int64_t)s0 * 64);
+  int so = 0;
+  int64_t koff = (int64_t)(C::S - 1) * 64;  // W source offset of the tile staged next (kt + S - 1)
+  for (int s = 0; s < nslice; ++s) {
+    const bool last = s == nslice - 1;
+    // recomputed per slice (8 VGPRs live in the slice loop, not 8 more hoisted across it): the empty asm hides
+    // wp0's loop invariance from LICM
+    int wpl = wp0;
+    asm volatile("" : "+v"(wpl));
+    int a_off[8];
 #pragma unroll
-    for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const b8*>(Ws + b_off[j]);
-    const int wpt = wp0 + ky * WE + kx;
+    for (int r = 0; r < 8; ++r)
+      a_off[r] = wpl * 64 + (win_pos(g, wpl + r) << 4) + (int)(wins - lds) + (s & 1) * C::WBYTES;
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      const int wp = wpt + i * WE;
-      const b8 a = *reinterpret_cast<const b8*>(Win + ((wp << 2) + (g ^ ((wp >> 2) & 3))) * 16);
+    for (int tap = 0; tap < 9; ++tap) {
+      // groups issued after kt's that may stay in flight: W tiles kt+1 .. kt+S-2 (+ the window riding with the next
+      // slice's first tap), fewer in the last slice
+      if (!last) vm_wait(C::NWG * (C::S - 2) + (tap >= 11 - C::S ? C::WROUNDS : 0));
+      else vm_wait(C::NWG * min(C::S - 2, 8 - tap));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
+      __builtin_amdgcn_sched_barrier(0);
+      if (!last || tap + C::S - 1 < 9) {
+        stage_w<BN, BH>(wring, so == 0 ? C::S - 1 : so - 1, wave, w_src, koff);
+        if (tap + C::S - 1 == 9 && !last) stage_win<BN, BH>(p, wins, s + 1, wave, wsrc, wok);
+      }
+      koff += 64;
+      const char* Ws = wring + so * C::WT + b_off;
+      so = so + 1 == C::S ? 0 : so + 1;
+      b8 b[C::FN];
 #pragma unroll
-      for (int j = 0; j < C::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const b8*>(Ws + j * 1024);
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int c = (tap / 3 + i) * WE + tap % 3;  // window pixel offset of (tap, block row i)
+        const b8 a = *reinterpret_cast<const b8*>(lds + a_off[c & 7] + c * 64);
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
