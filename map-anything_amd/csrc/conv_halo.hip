@@ -13,10 +13,13 @@
 //    <= 128 VGPRs (2 workgroups / CU: one tile's epilogue overlaps the other's main loop).
 //  * A fragment (16x16x32 MFMA) for block row py and tap (ky, kx): lane (px, g) reads 16 B = channels 8g..8g+7 of
 //    window pixel wp = (py+ky)*18 + px+kx.  Window image: pixel-major, 64 B per pixel, 16-B chunk g stored at
-//    chunk g ^ ((wp >> 2) & 3): the 16 lanes of a row group hit 16 distinct 16-B bank slots (conflict-free).
+//    position win_pos(g, wp): conflict-free in ds_read_b128's lane groups for every tap shift (see win_pos; the
+//    earlier g ^ ((wp >> 2) & 3) was 2-way in those groups: 29 % of the LDS cycles were conflict cycles).
 //  * W tiles (BN x 64 B, 16-B chunks XOR-swizzled as gemm_big's 64-B rows) stream through a ring of S slots,
 //    each DMA'd S-1 K tiles ahead; the window of slice c+1 rides in the DMA group of K tile 9(c+1) (two window
 //    buffers).  Counted vmcnt over the groups still in flight + raw s_barrier (no drain in the loop).
+//  * The 9 taps of a slice are unrolled: vmcnt depths, tap shifts and window staging are compile-time, and every A
+//    fragment read is one of 8 per-slice base addresses + an immediate (no per-read VALU, few SALU per step).
 #include "gemm_internal.h"
 
 namespace mapa_gemm_impl {

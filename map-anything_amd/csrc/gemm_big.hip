@@ -86,6 +86,52 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
   }
 }
 
+// ---- epilogue: 32 rows x 64 fp32 per wave per pass through LDS; 8 columns per lane (16-B bf16 stores) -------
+// The output pattern (epi_mode) selects one of three copies of the whole epilogue, so each keeps its part loop
+// fully unrolled (a runtime part index would move the accumulators to scratch).  LDS must be free (every wave past
+// its last main-loop read) before the call.
+template <int FM, int FN, int TM, int TN>
+__device__ __forceinline__ void big_epilogue(const GemmArgs& p, f32x4 (&acc)[FM][FN], char* lds, int bm, int bn,
+                                             int wave, int wm, int wn, int lane) {
+  const int g = lane >> 4, r16 = lane & 15;
+  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
+  const int c8 = (lane & 7) * 8;
+  const int n0 = bn + wn * TN + c8;
+  const EpiCol8 ec = epi_col_setup8(p, n0);
+  auto epilogue = [&](auto mode_tag) __attribute__((always_inline)) {
+    constexpr int MODE = decltype(mode_tag)::value;
+#pragma unroll
+    for (int part = 0; part < FM / 2; ++part) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (n0 < p.N && c8 < TN) {
+#pragma unroll 2
+        for (int pass = 0; pass < 4; ++pass) {
+          const int rloc = pass * 8 + (lane >> 3);
+          const int m = bm + wm * TM + part * 32 + rloc;
+          if (m >= p.M) break;
+          epi_store_row8_mode<MODE>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8),
+                                    *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8 + 4));
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  };
+  const int emode = epi_mode(p);
+  if (emode == 1) epilogue(std::integral_constant<int, 1>());
+  else if (emode == 2) epilogue(std::integral_constant<int, 2>());
+  else epilogue(std::integral_constant<int, 0>());
+}
+
 template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1, int BM = BBM,
           bool F16 = false>
 __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
@@ -210,47 +256,8 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   }
   __syncthreads();  // all waves done with the last stage: LDS becomes the epilogue staging area
 
-  // ---- epilogue: 32 rows x 64 fp32 per wave per pass through LDS; 8 columns per lane (16-B bf16 stores) -------
-  // The output pattern (epi_mode) selects one of three copies of the whole epilogue, so each keeps its part loop
-  // fully unrolled (a runtime part index would move the accumulators to scratch).
-  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
-  const int c8 = (lane & 7) * 8;
-  const int n0 = bn + wn * C::TN + c8;
-  const EpiCol8 ec = epi_col_setup8(p, n0);
-  auto epilogue = [&](auto mode_tag) __attribute__((always_inline)) {
-    constexpr int MODE = decltype(mode_tag)::value;
-#pragma unroll
-    for (int part = 0; part < C::FM / 2; ++part) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < C::FN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (n0 < p.N && c8 < C::TN) {
-#pragma unroll 2
-        for (int pass = 0; pass < 4; ++pass) {
-          const int rloc = pass * 8 + (lane >> 3);
-          const int m = bm + wm * C::TM + part * 32 + rloc;
-          if (m >= p.M) break;
-          epi_store_row8_mode<MODE>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8),
-                                    *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8 + 4));
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-  };
-  const int emode = epi_mode(p);
-  if (emode == 1) epilogue(std::integral_constant<int, 1>());
-  else if (emode == 2) epilogue(std::integral_constant<int, 2>());
-  else epilogue(std::integral_constant<int, 0>());
+  big_epilogue<C::FM, C::FN, C::TM, C::TN>(p, acc, lds, bm, bn, wave, wm, wn, lane);
 }
-
 
 // ---- ping-pong schedule: two wave groups offset by one barrier ------------------------------------------------
 // 256x256 tile, 32-deep K tiles (64-B LDS rows), a ring of NBUF K-tile buffers (32 KiB each).  Waves 0-3 (group 0,

@@ -427,12 +427,13 @@ class MapAnything:
 
     def _run_engine(self, eng, imgs, plan, geo, dpt_chunk):
         """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: one device, no
-        geometric inputs, no chunked dense head, no per-launch kernel timing.  The graph is keyed on the image
+        geometric inputs, no chunked dense head, no per-launch kernel timing, not in the serialize debug mode (every
+        launch checked, nat.SERIALIZE).  The graph is keyed on the image
         batch shape and precision; inputs are copied into its static buffer and outputs cloned out of it, so
         results never alias a later call's."""
         pe_idx = self._view_pe_rows(plan.num_views if plan is not None else imgs.shape[0])
         if (not self.hip_graphs or plan is not None or geo is not None or dpt_chunk is not None
-                or nat._timing is not None or imgs.device.type != "cuda"):
+                or nat._timing is not None or nat.SERIALIZE or imgs.device.type != "cuda"):
             return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx)
         key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index)
         with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
