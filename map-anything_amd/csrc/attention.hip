@@ -286,7 +286,8 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
       bf16x8 pf[2][2];
       float ls;
       auto exp_pack = [&](float shift) __attribute__((always_inline)) {
-        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        // four partial sums, seeded with the first four values (0 + e is not foldable: it would cost 4 adds)
+        float a[4];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -296,7 +297,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 const float e = __builtin_amdgcn_exp2f(st[kb][8 * s + j] - shift);
-                a[j & 3] = add_s(a[j & 3], e);
+                a[j & 3] = (kb == 0 && s == 0 && j < 4) ? e : add_s(a[j & 3], e);
                 t[j] = (_Float16)e;
               }
               pf[kb][s] = __builtin_bit_cast(bf16x8, t);
@@ -305,7 +306,7 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 const float e = __builtin_amdgcn_exp2f(st[kb][8 * s + j] - shift);
-                a[j & 3] = add_s(a[j & 3], e);
+                a[j & 3] = (kb == 0 && s == 0 && j < 4) ? e : add_s(a[j & 3], e);
                 t[j] = (__bf16)e;
               }
               pf[kb][s] = __builtin_bit_cast(bf16x8, t);
@@ -385,15 +386,25 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
     if (k0 == 0 && k1 == nkt) {  // whole task in this workgroup: final output
       if (qrow < p.seq_q) {
         bf16_t* obase = reinterpret_cast<bf16_t*>(p.o) + b * p.ob + (int64_t)qrow * p.orr + h * 64;
+        // lanes l and l+32 hold the two 4-column halves of each 8-column chunk of the same row: one permlane32_swap
+        // per packed word hands lane l the chunk's second half of an even chunk pair and lane l+32 the first half of
+        // the odd one, so every lane stores whole 16-B row segments (4 stores instead of 8 of 8 B)
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            const int d = dt * 32 + 8 * gq + 4 * hl;
-            uint2 pk;
-            pk.x = pack_lp2(F16, o[dt][4 * gq + 0] * inv, o[dt][4 * gq + 1] * inv);
-            pk.y = pack_lp2(F16, o[dt][4 * gq + 2] * inv, o[dt][4 * gq + 3] * inv);
-            *reinterpret_cast<uint2*>(obase + d) = pk;
+          for (int gp = 0; gp < 2; ++gp) {
+            uint32_t y[2], x[2];  // y: chunk 2gp (columns +4*hl), x: chunk 2gp+1
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+              y[w] = pack_lp2(F16, o[dt][8 * gp + 2 * w] * inv, o[dt][8 * gp + 2 * w + 1] * inv);
+              x[w] = pack_lp2(F16, o[dt][8 * gp + 4 + 2 * w] * inv, o[dt][8 * gp + 4 + 2 * w + 1] * inv);
+              const auto sw = __builtin_amdgcn_permlane32_swap(y[w], x[w], false, false);
+              y[w] = sw[0];
+              x[w] = sw[1];
+            }
+            // lane hl = 0: columns 16gp .. +7 = (y, x); hl = 1: columns 16gp + 8 .. +15 = (y, x)
+            const int d = dt * 32 + 16 * gp + 8 * hl;
+            *reinterpret_cast<uint4*>(obase + d) = make_uint4(y[0], y[1], x[0], x[1]);
           }
         if (p.lse && hl == 0)
           p.lse[((int64_t)b * p.heads + h) * p.seq_q + qrow] = (m_ref + __log2f(l_tot)) * LN2;
@@ -696,8 +707,9 @@ extern "C" int mapa_attention(const mapa_attn_desc* d, hipStream_t stream) {
   MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F16 || d->dtype == MAPA_F32, "mapa_attention: bad dtype");
   const int align = d->dtype == MAPA_F32 ? 4 : 8;
   MAPA_CHECK_ARG(d->q_rstride % align == 0 && d->k_rstride % align == 0 && d->v_rstride % align == 0 &&
-                     d->o_rstride % 4 == 0,
-                 "mapa_attention: row strides must keep 16-B alignment");
+                     d->o_rstride % align == 0 && d->o_bstride % align == 0 &&
+                     (reinterpret_cast<uintptr_t>(d->o) & 15) == 0,
+                 "mapa_attention: output base and row / batch strides must keep 16-B alignment (16-B row stores)");
   AttnArgs a;
   a.q = d->q; a.k = d->k; a.v = d->v; a.o = d->o; a.lse = d->lse;
   a.qb = d->q_bstride; a.qr = d->q_rstride; a.kb = d->k_bstride; a.kr = d->k_rstride;

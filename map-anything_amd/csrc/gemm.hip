@@ -315,7 +315,15 @@ static int g_tail_sk = 0;  // mapa_gemm_tune(MAPA_TUNE_TAIL_STREAMK, .)
 static bool pick_halo(int M, int N, int OH, int OW, int kb) {
   if (kb != 32 || !g_halo || N % 128 != 0) return false;
   const int64_t blocks = (int64_t)(M / (OH * OW)) * ((OH + 15) / 16) * ((OW + 15) / 16);
-  return blocks * (N / 128) >= 512;
+  // >= 400 tiles of 128 columns: from the 74^2 DPT convs up (8 views: 400 tiles; kbench after the round-3 window
+  // swizzle: rn2@74 167.6 -> 149.9 us, l2rn@74 140.7 -> 121.1 vs the implicit GEMM)
+  return blocks * (N / 128) >= 400;
+}
+
+// 8-row blocks with 256-wide tiles only where they cover fewer idle rows than 16-row blocks (148^2: 152 vs 160
+// rows; 74^2: 80 either way, and there the 128-wide 16x16 tile is faster: rn2@74 149.9 vs 156.4 us)
+static bool halo_rows8(const GemmArgs& a) {
+  return a.N % 256 == 0 && g_halo == 1 && ((a.cv_OH + 7) / 8) * 8 < ((a.cv_OH + 15) / 16) * 16;
 }
 
 static int g_forced = -1;  // -1: not read yet; 0: automatic; else a kernel variant code (tuning / tests)
@@ -443,8 +451,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
     // launched (persistent stream-K grid)
   } else if (halo && (forced ? launch_conv_halo(a, forced == 2585 || forced == 2588 ? 256 : 128, stream,
                                                 forced == 2588 ? 8 : 16)
-                              : launch_conv_halo(a, a.N % 256 == 0 && g_halo == 1 ? 256 : 128, stream,
-                                                 a.N % 256 == 0 && g_halo == 1 ? 8 : 16))) {
+                              : launch_conv_halo(a, halo_rows8(a) ? 256 : 128, stream, halo_rows8(a) ? 8 : 16))) {
     // launched (LDS halo-window conv)
   } else if (d->dtype != MAPA_F32 && ((variant >= 2560 && variant <= 2574) || variant == 2587) &&
              launch_gemm_big(a, conv, variant == 2587 ? 15 : variant - 2560, stream)) {
