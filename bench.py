@@ -35,6 +35,7 @@ import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
+PROFILE_ROUND = "r3"          # profiles/<round>/: the rocprofv3 PMC summaries the roofline / attention objects cite
 
 
 def enc_linear_flops_per_view(T):
@@ -65,13 +66,13 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--geometric", action="store_true",
                     help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r2", "pmc_traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", PROFILE_ROUND, "pmc_traffic.json"),
                     help="HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_summary.py)")
-    ap.add_argument("--mfma-pmc-json", default=os.path.join(REPO, "profiles", "r2", "pmc_mfma.json"),
+    ap.add_argument("--mfma-pmc-json", default=os.path.join(REPO, "profiles", PROFILE_ROUND, "pmc_mfma.json"),
                     help="per-kernel-group MFMA busy fraction + clock from a rocprofv3 SQ pass (tools/gpu_pmc.sh)")
     ap.add_argument("--attn-pmc-json", default=None,
                     help="global-attention MFMA busy fraction from rocprofv3 PMC passes (tools/attn_pmc.sh); default: "
-                         "profiles/r2/attn_global_pmc.json (8 views) or attn_global_v100_pmc.json (>= 100 views)")
+                         f"profiles/{PROFILE_ROUND}/attn_global_pmc.json (8 views) or attn_global_v100_pmc.json (>= 100 views)")
     ap.add_argument("--lib", default=None, help="A/B only: load this libmapa.so build (tools/ab_build.sh)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: gloo process group, placeholder CPU step (tests only)")
@@ -222,7 +223,7 @@ def main():
             roofline = {"kernel": kind, "bound": "mfma", "achieved": achieved, "peak": PEAK_BF16_TFLOPS,
                         "unit": "TFLOP/s", "frac": (achieved / PEAK_BF16_TFLOPS) if achieved else None,
                         "traffic": traffic,
-                        "traffic_unit": "bytes/launch: L2 fabric fetch (FETCH_SIZE x2, Infinity-Cache hits included) + WRITE_SIZE, rocprofv3 PMC, profiles/r2/pmc_traffic.json",
+                        "traffic_unit": "bytes/launch: L2 fabric fetch (FETCH_SIZE x2, Infinity-Cache hits included) + WRITE_SIZE, rocprofv3 PMC, " + os.path.relpath(args.traffic_json, REPO),
                         "pmc": mfma_pmc,
                         "launches": kt["count"], "avg_launch_us": kt["ms"] * 1e3 / kt["count"],
                         "timing_pass": {"ms_per_step": instr_ms, "launch": "eager, event pair per native call",
@@ -239,7 +240,7 @@ def main():
                      "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": tf / PEAK_BF16_TFLOPS, "target_frac": 0.40,
                      "ms_per_step": v["ms"] / args.steps, "launches_per_step": v["count"] / args.steps}
             attn_pmc = args.attn_pmc_json or os.path.join(
-                REPO, "profiles", "r2", "attn_global_v100_pmc.json" if V_total >= 100 else "attn_global_pmc.json")
+                REPO, "profiles", PROFILE_ROUND, "attn_global_v100_pmc.json" if V_total >= 100 else "attn_global_pmc.json")
             if os.path.exists(attn_pmc):
                 # MFMA-pipe busy fraction at the clock the chip really ran (rocprofv3 PMC pass, tools/attn_pmc.sh)
                 pj = json.load(open(attn_pmc))
