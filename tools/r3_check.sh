@@ -2,7 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 1500 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > gpurun_out/r3_tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -s --timeout 600 --timeout-method thread > gpurun_out/r3_tests.log 2>&1; rc=$?
 grep -E "passed|failed" gpurun_out/r3_tests.log | tail -2
 grep -E "^FAILED|Error" gpurun_out/r3_tests.log | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
