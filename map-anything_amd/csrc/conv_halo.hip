@@ -110,18 +110,20 @@ __device__ __forceinline__ void stage_w(char* wring, int slot, int wave, const c
 #pragma unroll
   for (int i = 0; i < C::NWG; ++i) __builtin_amdgcn_global_load_lds(w_src[i] + koff, dst + i * 8192, 16, 0, 0);
 }
-// DMA of the input window of 32-channel slice `slice` into window buffer slice & 1
+// DMA of the input window of 32-channel slice `slice` into window buffer slice & 1 (dummy: the zero page into that
+// buffer — the uniform group past the last slice, which nothing reads)
 template <int BN, int BH>
 __device__ __forceinline__ void stage_win(const GemmArgs& p, char* wins, int slice, int wave, const int64_t* wsrc,
-                                          const bool* wok) {
+                                          const bool* wok, bool dummy = false) {
   using C = HCfg<BN, BH>;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const char* abase = reinterpret_cast<const char*>(p.A);
-  const int64_t ch = split_col(p, slice * 32);
+  const int64_t ch = dummy ? 0 : split_col(p, slice * 32);
   char* wd = wins + (slice & 1) * C::WBYTES + wave * 1024;
 #pragma unroll
   for (int r = 0; r < C::WROUNDS; ++r)
-    __builtin_amdgcn_global_load_lds(wok[r] ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(wok[r] && !dummy ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16,
+                                     0, 0);
 }
 
 template <int BN, bool HO = false, int BH = 16>
@@ -180,10 +182,14 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   // c mod 8 only -> a_off[c % 8] + c*64, an immediate offset for every (tap, row) pair
 
   // K loop: slices of 32 channels, the 9 taps of a slice unrolled, so the tap shift, the vmcnt depth of every step
-  // and which steps stage a window are compile-time constants (one runtime branch: the last slice, which stages no
-  // further W tiles / window past nk).  K tile kt = slice*9 + tap lives in ring slot kt % S (`so`); the DMA group
-  // issued at step kt is W tile kt+S-1 (+ the next slice's window when kt+S-1 starts it).
+  // and which steps stage a window are compile-time constants.  K tile kt = slice*9 + tap lives in ring slot kt % S
+  // (`so`); the DMA group issued at step kt is W tile kt+S-1 (+ the next slice's window when kt+S-1 starts it).
+  // Every step issues exactly one group, also past the end (the last slice re-stages the last W tile and its own
+  // window into slots / the buffer nobody reads any more), so the counted waits hold in every slice with no
+  // last-slice branch: a peeled last slice spilled VGPRs, and scratch traffic inside a counted-vmcnt region breaks
+  // the count (a spill store can retire before an older LDS-DMA).
   const int nslice = nk / 9;
+  const int64_t klast = (int64_t)(nk - 1) * 64;
   stage_w<BN, BH>(wring, 0, wave, w_src, 0);  // group 0: W tile 0 + slice 0's window (vmcnt retires in issue order)
   stage_win<BN, BH>(p, wins, 0, wave, wsrc, wok);
 #pragma unroll
@@ -191,7 +197,6 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   int so = 0;
   int64_t koff = (int64_t)(C::S - 1) * 64;  // W source offset of the tile staged next (kt + S - 1)
   for (int s = 0; s < nslice; ++s) {
-    const bool last = s == nslice - 1;
     // recomputed per slice (8 VGPRs live in the slice loop, not 8 more hoisted across it): the empty asm hides
     // wp0's loop invariance from LICM
     int wpl = wp0;
@@ -202,17 +207,14 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
       a_off[r] = wpl * 64 + (win_pos(g, wpl + r) << 4) + (int)(wins - lds) + (s & 1) * C::WBYTES;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
-      // groups issued after kt's that may stay in flight: W tiles kt+1 .. kt+S-2 (+ the window riding with the next
-      // slice's first tap), fewer in the last slice
-      if (!last) vm_wait(C::NWG * (C::S - 2) + (tap >= 11 - C::S ? C::WROUNDS : 0));
-      else vm_wait(C::NWG * min(C::S - 2, 8 - tap));
+      // groups issued after kt's, still allowed in flight: W tiles kt+1 .. kt+S-2, plus the window riding with the
+      // next slice's first tap
+      vm_wait(C::NWG * (C::S - 2) + (tap >= 11 - C::S ? C::WROUNDS : 0));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
       __builtin_amdgcn_sched_barrier(0);
-      if (!last || tap + C::S - 1 < 9) {
-        stage_w<BN, BH>(wring, so == 0 ? C::S - 1 : so - 1, wave, w_src, koff);
-        if (tap + C::S - 1 == 9 && !last) stage_win<BN, BH>(p, wins, s + 1, wave, wsrc, wok);
-      }
+      stage_w<BN, BH>(wring, so == 0 ? C::S - 1 : so - 1, wave, w_src, koff < klast ? koff : klast);
+      if (tap + C::S - 1 == 9) stage_win<BN, BH>(p, wins, s + 1, wave, wsrc, wok, s + 1 == nslice);
       koff += 64;
       const char* Ws = wring + so * C::WT + b_off;
       so = so + 1 == C::S ? 0 : so + 1;

@@ -221,6 +221,40 @@ def test_split_precision_conv_halo_window(nat):
     assert rel_l2(out.cpu(), ref) < 2e-5
 
 
+def test_regressor_head_out_repeatable(nat):
+    """The fused regressor head is bit-for-bit repeatable launch to launch (tools/ho_det.py: with -O3 SLP packing of
+    dense_head_pixel into v_pk_*_f32, one 16-lane row per wave of the pts3d y components came out different from
+    launch to launch on MI355X; conv_halo.o is built with -fno-slp-vectorize)."""
+    n, H, W, C = 2, 518, 518, 128
+    M = n * H * W
+    xr = _rand(M, C, seed=70).relu()
+    wk = _rand(C, 9, C, scale=(9 * C) ** -0.5, seed=71)
+    b2, w6, b6 = _rand(C, seed=72), _rand(6, C, scale=C ** -0.5, seed=73), _rand(6, seed=74)
+    a = torch.empty(M, 2 * C, dtype=torch.bfloat16, device="cuda")
+    nat.split_bf16x3(xr, M, C, C, a)
+    whi = wk.to(torch.bfloat16)
+    wlo = (wk - whi.float()).to(torch.bfloat16)
+    wp = torch.stack([whi, wlo, whi], 2).reshape(C, 9, 3 * C).reshape(C, 9, 12, 32).permute(0, 2, 1, 3)
+    wp = wp.contiguous().reshape(C, -1)
+    wp._mapa_split = True
+    wp._mapa_kblock = 32
+    pose_out, scale = torch.empty(n, 19, device="cuda"), torch.empty(1, device="cuda")
+    nat.pose_scale_finalize(_rand(n, 7, seed=75), _rand(1, seed=76), n, 1, pose_out, scale,
+                            torch.empty(n, 4, 4, device="cuda"))
+
+    def run():
+        o = [torch.empty((n, H, W, 3), device="cuda") for _ in range(3)] + [torch.empty((n, H, W, 1), device="cuda")] + \
+            [torch.empty((n, H, W), device="cuda") for _ in range(2)] + \
+            [torch.empty((n, H, W), dtype=torch.uint8, device="cuda")]
+        nat.gemm(a, wp, M, C, 9 * 3 * C, bias=b2, act=nat.ACT_RELU, conv=(3 * C, H, W, H, W, 1),
+                 head_out=(w6, b6, pose_out, scale, *o))
+        return o
+    first = run()
+    for _ in range(6):
+        for x, y in zip(first, run()):
+            assert torch.equal(x, y)
+
+
 @pytest.mark.parametrize("split", [False, True])
 @pytest.mark.parametrize("n,H,W", [(2, 37, 29), (1, 48, 64), (3, 16, 16)])
 def test_regressor_head_out_fused(nat, split, n, H, W):

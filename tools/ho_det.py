@@ -1,0 +1,64 @@
+"""Repeatability of the fused regressor-head conv (mapa_regressor_head_out) on fixed inputs: N launches, every
+output compared bit for bit with the first; prints where pts3d differs.  python tools/ho_det.py [reps] [lib]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "map-anything_amd"))
+import torch  # noqa: E402
+
+from mapanything import _native as nat  # noqa: E402
+
+if len(sys.argv) > 2:
+    nat.load_library(sys.argv[2])
+
+
+def rnd(*s, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*s, generator=g) * scale).cuda()
+
+
+def main():
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    n, H, W, C = 8, 518, 518, 128
+    M = n * H * W
+    xr = rnd(M, C, seed=60).relu()
+    wk = rnd(C, 9, C, scale=(9 * C) ** -0.5, seed=61)
+    b2, w6, b6 = rnd(C, seed=62), rnd(6, C, scale=C ** -0.5, seed=63), rnd(6, seed=64)
+    a = torch.empty(M, 2 * C, dtype=torch.bfloat16, device="cuda")
+    nat.split_bf16x3(xr, M, C, C, a)
+    whi = wk.to(torch.bfloat16)
+    wlo = (wk - whi.float()).to(torch.bfloat16)
+    wp = torch.stack([whi, wlo, whi], 2).reshape(C, 9, 3 * C)
+    Cl = 3 * C
+    wp = wp.reshape(C, 9, Cl // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(C, -1)
+    wp._mapa_split = True
+    wp._mapa_kblock = 32
+    pose_out = torch.empty(n, 19, device="cuda")
+    scale = torch.empty(1, device="cuda")
+    nat.pose_scale_finalize(rnd(n, 7, seed=65), rnd(1, seed=66), n, 1, pose_out, scale,
+                            torch.empty(n, 4, 4, device="cuda"))
+    conv = (Cl, H, W, H, W, 1)
+
+    def run():
+        f = dict(device="cuda")
+        o = [torch.empty((n, H, W, 3), **f) for _ in range(3)] + [torch.empty((n, H, W, 1), **f)] + \
+            [torch.empty((n, H, W), **f) for _ in range(2)] + [torch.empty((n, H, W), dtype=torch.uint8, device="cuda")]
+        nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scale, *o))
+        torch.cuda.synchronize()
+        return o
+    names = ["pts3d", "pts3d_cam", "rays", "depth", "conf", "logits", "mask"]
+    first = run()
+    nbad = 0
+    for r in range(reps):
+        o = run()
+        for nm, x, y in zip(names, first, o):
+            if not torch.equal(x, y):
+                nbad += 1
+                d = (x.float() - y.float()).abs().reshape(n, H, W, -1).amax(-1)
+                idx = (d > 0).nonzero()
+                print(f"rep {r}: {nm} differs at {idx.shape[0]} px, e.g. {idx[:4].tolist()}", flush=True)
+    print("ho_det:", "repeatable" if nbad == 0 else f"{nbad} mismatching outputs", flush=True)
+
+
+if __name__ == "__main__":
+    main()
