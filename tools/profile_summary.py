@@ -5,6 +5,7 @@
   python tools/profile_summary.py mfma <kernel-regex> <pmc.csv>...           -> MFMA-pipe utilisation at the real clock
   python tools/profile_summary.py mfma_groups <pmc.csv> [launch_log.json]   -> the same per kernel group (bench run)
   python tools/profile_summary.py kinds <kernel_trace.csv> <launch_log.json> -> per bench.py kind (calls / avg / total)
+  python tools/profile_summary.py headline <kernel_trace.csv> <bench.json>   -> groups over the headline infers only
 
 With a launch log (MAPA_LAUNCH_LOG, mapanything/_native.py) every GEMM / attention dispatch is named exactly as
 bench.py names it ("gemm", "gemm_split", "conv3x3", "conv3x3_split", "attention", "attention_global"): the n-th
@@ -90,6 +91,35 @@ def stats(path, bench=None):
         if rf.get("kernel") in out:
             out["bench_dominant"]["rocprof_avg_us"] = out[rf["kernel"]]["avg_us"]
             out["bench_dominant"]["ratio"] = rf["avg_launch_us"] / out[rf["kernel"]]["avg_us"]
+    return out
+
+
+def headline(trace_csv, bench):
+    """Per-group launch stats over the bench's HEADLINE infers only, from the kernel trace of the driver's full command
+    (which also runs the fast mode and the 100-view strong job): dispatches are cut into infers at every
+    patchify_kernel launch (one per infer) and the first warmup + steps (graph replay) + steps (the eager timing pass)
+    infers are kept — the launches bench.py's roofline times."""
+    b = json.loads(open(bench).read().strip().splitlines()[-1])
+    n_keep = b["warmup"] + 2 * b["steps"]
+    rows = list(csv.DictReader(open(trace_csv)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    g = defaultdict(lambda: {"calls": 0, "total_ns": 0.0})
+    infer = 0
+    for r in rows:
+        if "patchify_kernel" in r["Kernel_Name"]:
+            infer += 1
+        if infer < 1 or infer > n_keep:
+            continue
+        k = group(r["Kernel_Name"])
+        g[k]["calls"] += 1
+        g[k]["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    out = {k: dict(v, avg_us=v["total_ns"] / v["calls"] / 1e3) for k, v in g.items()}
+    rf = b.get("roofline") or {}
+    out["infers"] = n_keep
+    out["bench_dominant"] = {"kernel": rf.get("kernel"), "avg_launch_us": rf.get("avg_launch_us")}
+    if rf.get("kernel") in out:
+        out["bench_dominant"]["rocprof_avg_us"] = out[rf["kernel"]]["avg_us"]
+        out["bench_dominant"]["ratio"] = rf["avg_launch_us"] / out[rf["kernel"]]["avg_us"]
     return out
 
 
@@ -197,6 +227,8 @@ if __name__ == "__main__":
         print(json.dumps(mfma(a[2], a[3:]), indent=1))
     elif a[1] == "stats":
         print(json.dumps(stats(a[2], a[3] if len(a) > 3 else None), indent=1))
+    elif a[1] == "headline":
+        print(json.dumps(headline(a[2], a[3]), indent=1))
     elif a[1] == "kinds":
         print(json.dumps(kinds(a[2], a[3]), indent=1))
     else:
