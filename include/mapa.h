@@ -104,7 +104,8 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
 /* Tuning / test hook: force one kernel variant for every later mapa_gemm call (0 = automatic per-shape choice,
  * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
  * 2560..2574 = 256-row tiles, 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one
- * the automatic choice runs), 2584..2586 / 2588 = LDS halo-window conv, 2587 = 192x192 tiles.  (The round-2 opt-in
+ * the automatic choice runs), 2584..2586 / 2588 = LDS halo-window conv, 2589 = the same on flat-raster blocks with
+ * split K (needs a workspace when it splits), 2587 = 192x192 tiles.  (The round-2 opt-in
  * main-loop experiments — phase-interleaved and four-wave tiles — measured slower on every path shape and were
  * removed from the library) */
 int mapa_gemm_set_variant(int variant);
@@ -120,10 +121,15 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
 /* Tuning / A-B hooks of the automatic kernel choice (process-wide):
  *   MAPA_TUNE_CONV_HALO (default 1): stride-1 bf16 convs in the 32-channel-slice K order (conv_kblock = 32) run on
  *     the LDS halo-window conv (N = 256: 8x16-pixel blocks, 256-wide tiles; else 16x16 blocks); 2 keeps 16x16
- *     blocks for every N; 0 keeps them on the implicit GEMM (variants 2584 / 2585 / 2586 / 2588 force one);
+ *     blocks for every N; 3 is the default without the flat-raster blocks below; 0 keeps them on the implicit GEMM
+ *     (variants 2584 / 2585 / 2586 / 2588 force one);
+ *     With the default, the stride-1 convs too small for 16x16 blocks (up to 62 pixels wide: the 19^2 / 37^2 DPT
+ *     convs) run the halo conv on flat-raster blocks with their 32-channel slices split over several workgroups per
+ *     tile (variant 2589 forces it; needs the workspace mapa_gemm_workspace_bytes reports);
  *   MAPA_TUNE_TAIL_STREAMK (default 0): dense bf16 GEMMs whose 256x128 tiles leave a nearly empty last wave use
- *     the tail-only stream-K schedule (2582) when a workspace is passed. */
-enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1 };
+ *     the tail-only stream-K schedule (2582) when a workspace is passed;
+ *   MAPA_TUNE_HALO_SPLIT (default 0 = automatic): the K part count of the flat-raster halo conv (1..64). */
+enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2 };
 int mapa_gemm_tune(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------------------

@@ -63,6 +63,23 @@ struct HeadOut {
   uint8_t* mask;
 };
 
+// Flat-raster blocks (FLAT = true; maps up to 62 pixels wide: the 19^2 / 37^2 DPT convs, where 16x16 blocks leave
+// 41-65 % of the pixels idle and give only 26-144 tiles): a block is 256 consecutive positions of the images' padded
+// raster (mapa_idx::flat_pixel: rows of OW + 1, OH + 1 rows per image, 94-95 % of the positions real pixels); the 9
+// taps read the 1-D window of 256 + 2(OW+1) + 2 positions at shifts dy(OW+1) + dx.  Too few tiles for the CUs, so
+// the 32-channel slices are split over nsplit workgroups per tile: each stores its fp32 partial sums to a slab with
+// write-through (sc1) stores and draws a ticket (agent-scope relaxed add, as gemm_big.hip's stream-K); the last
+// arriver reads every slab with sc1 loads, sums them in part order (bit-reproducible whatever the arrival order),
+// re-zeroes the ticket and runs the epilogue.  No workgroup waits on another.
+struct HSplit {
+  int nsplit;    // K parts per tile (1: no slabs, no tickets)
+  int nblk;      // flat blocks
+  int* tickets;  // [tiles], zero between launches
+  float* slabs;  // [tiles * nsplit][256 * BN] fp32 accumulator images in fragment order
+};
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int FLAT_MAX_WP = 63;  // window of 256 + 2 * Wp + 2 <= 384 positions (the 3-round window buffer)
+
 __device__ __forceinline__ int swz64(int row) { return (0x1320 >> (((row >> 2) & 3) * 4)) & 3; }
 
 template <int N>
@@ -126,9 +143,10 @@ __device__ __forceinline__ void stage_win(const GemmArgs& p, char* wins, int sli
                                      0, 0);
 }
 
-template <int BN, bool HO = false, int BH = 16>
-__global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel(GemmArgs p, HeadOut ho) {
+template <int BN, bool HO = false, int BH = 16, bool FLAT = false>
+__global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel(GemmArgs p, HeadOut ho, HSplit sp) {
   using C = HCfg<BN, BH>;
+  static_assert(!FLAT || (BN == 128 && BH == 16 && !HO), "flat blocks: 128-wide tiles of 256 positions");
   __shared__ __attribute__((aligned(1024))) char lds[C::LDS];
   char* const wring = lds;
   char* const wins = lds + C::S * C::WT;
@@ -136,13 +154,24 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / C::WN, wn = wave % C::WN;
-  // ---- tile: (img, block row, block col, column tile), XCD-contiguous ranges of neighbouring blocks
-  const int nbx = (p.cv_OW + BW - 1) / BW, nby = (p.cv_OH + BH - 1) / BH, ntn = p.N / BN;
+  // ---- tile: (img, block row, block col, column tile), XCD-contiguous ranges of neighbouring blocks; FLAT: (flat
+  // block, column tile, K part)
+  const int ntn = p.N / BN;
   const int imgs = p.M / (p.cv_OH * p.cv_OW);
-  int img, by, bx, tn;
-  mapa_idx::halo_block(blockIdx.x, imgs, nby, nbx, ntn, img, by, bx, tn);
+  const int Wp = p.cv_OW + 1, Hp = p.cv_OH + 1;  // FLAT raster geometry
+  int img = 0, by = 0, bx = 0, tn, fb = 0, kp = 0;
+  if constexpr (FLAT) {
+    mapa_idx::halo_flat_tile(blockIdx.x, sp.nblk, ntn, sp.nsplit, fb, tn, kp);
+  } else {
+    const int nbx = (p.cv_OW + BW - 1) / BW, nby = (p.cv_OH + BH - 1) / BH;
+    mapa_idx::halo_block(blockIdx.x, imgs, nby, nbx, ntn, img, by, bx, tn);
+  }
   const int bn = tn * BN;
   const int nk = p.K / 32;  // 9 taps x (logical channels / 32)
+  const int nslice = nk / 9;
+  // this workgroup's slices [s_lo, s_hi): all of them, or K part kp of nsplit
+  const int s_lo = FLAT ? (int)((int64_t)kp * nslice / sp.nsplit) : 0;
+  const int s_hi = FLAT ? (int)((int64_t)(kp + 1) * nslice / sp.nsplit) : nslice;
 
   // ---- window staging geometry (this thread's WROUNDS pieces; pixel offsets are slice-invariant)
   int64_t wsrc[C::WROUNDS];
@@ -152,10 +181,17 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
     const int q = r * HT + tid;
     const int wp = q >> 2, cl = q & 3;
     const int cs = win_chunk(cl, wp);  // LDS position cl holds channel chunk cs
-    const int wy = wp / WE, wx = wp - wy * WE;
-    const int iy = by * BH - 1 + wy, ix = bx * BW - 1 + wx;
-    wok[r] = q < C::WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-    wsrc[r] = wok[r] ? ((int64_t)(img * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
+    if constexpr (FLAT) {
+      int im, iy, ix;  // window position wp = raster position fb*256 - Wp - 1 + wp
+      wok[r] = wp < 256 + 2 * Wp + 2 &&
+               mapa_idx::flat_pixel(fb * 256 - Wp - 1 + wp, Wp, Hp, p.cv_OH, p.cv_OW, imgs, im, iy, ix);
+      wsrc[r] = wok[r] ? ((int64_t)(im * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
+    } else {
+      const int wy = wp / WE, wx = wp - wy * WE;
+      const int iy = by * BH - 1 + wy, ix = bx * BW - 1 + wx;
+      wok[r] = q < C::WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+      wsrc[r] = wok[r] ? ((int64_t)(img * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
+    }
   }
   // ---- W staging geometry: instruction i of this wave covers ring rows (i*8 + wave)*16 + [0, 16)
   const char* w_src[C::NWG];
@@ -177,34 +213,38 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   // fragment j sits at b_off + j*1024 (an immediate offset of one address)
   const int rb0 = wn * C::TN + r16;
   const int b_off = rb0 * 64 + ((g ^ swz64(rb0)) << 4);
-  const int wp0 = (wm * C::FM) * WE + r16;  // window pixel of (block row wm*FM, px = r16) at tap (0, 0)
+  // window pixel of (block row wm*FM, px = r16) at tap (0, 0); FLAT: of position (wm*FM)*16 + r16
+  const int wp0 = (wm * C::FM) * (FLAT ? BW : WE) + r16;
   // A fragment of window pixel wp0 + c: byte (wp0 + c)*64 + win_pos(g, wp0 + c)*16, and bit 2 of wp0 + c depends on
-  // c mod 8 only -> a_off[c % 8] + c*64, an immediate offset for every (tap, row) pair
+  // c mod 8 only -> a_off[c % 8] + c*64, an immediate offset for every (tap, row) pair.  FLAT: the tap shift
+  // dy*Wp + dx is a runtime value, so each tap gets one address (+ i*1024 per block row i: 16 positions on)
 
   // K loop: slices of 32 channels, the 9 taps of a slice unrolled, so the tap shift, the vmcnt depth of every step
-  // and which steps stage a window are compile-time constants.  K tile kt = slice*9 + tap lives in ring slot kt % S
-  // (`so`); the DMA group issued at step kt is W tile kt+S-1 (+ the next slice's window when kt+S-1 starts it).
-  // Every step issues exactly one group, also past the end (the last slice re-stages the last W tile and its own
-  // window into slots / the buffer nobody reads any more), so the counted waits hold in every slice with no
-  // last-slice branch: a peeled last slice spilled VGPRs, and scratch traffic inside a counted-vmcnt region breaks
+  // and which steps stage a window are compile-time constants.  K tile kt = slice*9 + tap lives in ring slot
+  // (kt - 9 s_lo) % S (`so`); the DMA group issued at step kt is W tile kt+S-1 (+ the next slice's window when kt+S-1
+  // starts it).  Every step issues exactly one group, also past the end (the last slice re-stages the last W tile
+  // and its own window into slots / the buffer nobody reads any more), so the counted waits hold in every slice with
+  // no last-slice branch: a peeled last slice spilled VGPRs, and scratch traffic inside a counted-vmcnt region breaks
   // the count (a spill store can retire before an older LDS-DMA).
-  const int nslice = nk / 9;
-  const int64_t klast = (int64_t)(nk - 1) * 64;
-  stage_w<BN, BH>(wring, 0, wave, w_src, 0);  // group 0: W tile 0 + slice 0's window (vmcnt retires in issue order)
-  stage_win<BN, BH>(p, wins, 0, wave, wsrc, wok);
+  const int64_t kfirst = (int64_t)s_lo * 9 * 64;
+  const int64_t klast = ((int64_t)s_hi * 9 - 1) * 64;
+  stage_w<BN, BH>(wring, 0, wave, w_src, kfirst);  // group 0: the first W tile + the first slice's window
+  stage_win<BN, BH>(p, wins, s_lo, wave, wsrc, wok);
 #pragma unroll
-  for (int s0 = 1; s0 < C::S - 1; ++s0) stage_w<BN, BH>(wring, s0, wave, w_src, (int64_t)s0 * 64);
+  for (int s0 = 1; s0 < C::S - 1; ++s0) stage_w<BN, BH>(wring, s0, wave, w_src, kfirst + (int64_t)s0 * 64);
   int so = 0;
-  int64_t koff = (int64_t)(C::S - 1) * 64;  // W source offset of the tile staged next (kt + S - 1)
-  for (int s = 0; s < nslice; ++s) {
+  int64_t koff = kfirst + (int64_t)(C::S - 1) * 64;  // W source offset of the tile staged next (kt + S - 1)
+  for (int s = s_lo; s < s_hi; ++s) {
     // recomputed per slice (8 VGPRs live in the slice loop, not 8 more hoisted across it): the empty asm hides
     // wp0's loop invariance from LICM
     int wpl = wp0;
     asm volatile("" : "+v"(wpl));
+    const int woff = (int)(wins - lds) + (s & 1) * C::WBYTES;
     int a_off[8];
+    if constexpr (!FLAT) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r)
-      a_off[r] = wpl * 64 + (win_pos(g, wpl + r) << 4) + (int)(wins - lds) + (s & 1) * C::WBYTES;
+      for (int r = 0; r < 8; ++r) a_off[r] = wpl * 64 + (win_pos(g, wpl + r) << 4) + woff;
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       // groups issued after kt's, still allowed in flight: W tiles kt+1 .. kt+S-2, plus the window riding with the
@@ -214,17 +254,27 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
       __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
       __builtin_amdgcn_sched_barrier(0);
       stage_w<BN, BH>(wring, so == 0 ? C::S - 1 : so - 1, wave, w_src, koff < klast ? koff : klast);
-      if (tap + C::S - 1 == 9) stage_win<BN, BH>(p, wins, s + 1, wave, wsrc, wok, s + 1 == nslice);
+      if (tap + C::S - 1 == 9) stage_win<BN, BH>(p, wins, s + 1, wave, wsrc, wok, s + 1 == s_hi);
       koff += 64;
       const char* Ws = wring + so * C::WT + b_off;
       so = so + 1 == C::S ? 0 : so + 1;
       b8 b[C::FN];
 #pragma unroll
       for (int j = 0; j < C::FN; ++j) b[j] = *reinterpret_cast<const b8*>(Ws + j * 1024);
+      const char* at = lds;
+      if constexpr (FLAT) {
+        const int wt = wpl + (tap / 3) * Wp + tap % 3;  // window position of (tap, block row 0)
+        at = lds + wt * 64 + (win_pos(g, wt) << 4) + woff;
+      }
 #pragma unroll
       for (int i = 0; i < C::FM; ++i) {
-        const int c = (tap / 3 + i) * WE + tap % 3;  // window pixel offset of (tap, block row i)
-        const b8 a = *reinterpret_cast<const b8*>(lds + a_off[c & 7] + c * 64);
+        b8 a;
+        if constexpr (FLAT) {
+          a = *reinterpret_cast<const b8*>(at + i * 1024);
+        } else {
+          const int c = (tap / 3 + i) * WE + tap % 3;  // window pixel offset of (tap, block row i)
+          a = *reinterpret_cast<const b8*>(lds + a_off[c & 7] + c * 64);
+        }
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
@@ -233,6 +283,61 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // LDS becomes the epilogue staging area
+
+  if constexpr (FLAT) {
+    if (sp.nsplit > 1) {
+      // ---- split K: publish this part's partial sums; the last arriver sums every part's slab in part order
+      constexpr int SLAB = 256 * BN;
+      const int tile = fb * ntn + tn;
+      const int voff = lane * 16;
+      {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(sp.slabs + ((int64_t)tile * sp.nsplit + kp) * SLAB, 0,
+                                                          SLAB * 4, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rs, voff,
+                                                   ((wave * C::FM + i) * C::FN + j) * 1024, 16);  // sc1
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through stores
+      __syncthreads();
+      int* last_word = reinterpret_cast<int*>(lds + C::LDS - 16);  // above the epilogue staging rows
+      if (tid == 0) {
+        const int ticket = __hip_atomic_fetch_add(&sp.tickets[tile], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = ticket == sp.nsplit - 1;
+        if (last) __hip_atomic_store(&sp.tickets[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last_word = last;
+      }
+      __syncthreads();
+      const int last = *last_word;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the slab loads below the ticket
+      if (!last) return;
+      for (int b = 0; b < sp.nsplit; ++b) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(sp.slabs + ((int64_t)tile * sp.nsplit + b) * SLAB, 0,
+                                                          SLAB * 4, 0x00020000);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {  // half a slab in flight at a time
+          f32x4 v[C::FM / 2][C::FN];
+#pragma unroll
+          for (int i = 0; i < C::FM / 2; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j)
+              v[i][j] = __builtin_bit_cast(
+                  f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                             rs, voff, ((wave * C::FM + h * (C::FM / 2) + i) * C::FN + j) * 1024, 16));
+#pragma unroll
+          for (int i = 0; i < C::FM / 2; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) {
+              f32x4& a = acc[h * (C::FM / 2) + i][j];
+              a = b == 0 ? v[i][j] : a + v[i][j];
+            }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+  }
 
   if constexpr (HO) {
     // ---- fused regressor tail.  Lane (r16, g) holds relu(acc + bias) of pixels g*4 + r of block rows wm*FM + i at
@@ -317,10 +422,18 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
 #pragma unroll 2
     for (int pass = 0; pass < 4; ++pass) {
       const int rloc = pass * 8 + (lane >> 3);  // row of the 32-row pass: block row wm*FM + part*2 + rloc/16, px rloc%16
-      const int oy = by * BH + wm * C::FM + part * 2 + (rloc >> 4), ox = bx * BW + (rloc & 15);
-      if (oy < p.cv_OH && ox < p.cv_OW)
-        epi_store_row8<bf16_t>(p, ec, (img * p.cv_OH + oy) * p.cv_OW + ox,
-                               *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c8),
+      int m = -1;
+      if constexpr (FLAT) {
+        int im, oy, ox;
+        if (mapa_idx::flat_pixel(fb * 256 + (wm * C::FM + part * 2) * BW + rloc, Wp, Hp, p.cv_OH, p.cv_OW, imgs, im,
+                                 oy, ox))
+          m = (im * p.cv_OH + oy) * p.cv_OW + ox;
+      } else {
+        const int oy = by * BH + wm * C::FM + part * 2 + (rloc >> 4), ox = bx * BW + (rloc & 15);
+        if (oy < p.cv_OH && ox < p.cv_OW) m = (img * p.cv_OH + oy) * p.cv_OW + ox;
+      }
+      if (m >= 0)
+        epi_store_row8<bf16_t>(p, ec, m, *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c8),
                                *reinterpret_cast<const f32x4*>(ep + rloc * H_ELD + c8 + 4));
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -344,12 +457,62 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh) {
   const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + bh - 1) / bh) * ((a.cv_OW + BW - 1) / BW) * (a.N / bn);
   if (tiles >= (int64_t(1) << 31)) return false;
   const HeadOut none{};
+  const HSplit one{1, 0, nullptr, nullptr};
   if (bh == 8)
-    hipLaunchKernelGGL((conv_halo_kernel<256, false, 8>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+    hipLaunchKernelGGL((conv_halo_kernel<256, false, 8>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
   else if (bn == 256)
-    hipLaunchKernelGGL((conv_halo_kernel<256>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+    hipLaunchKernelGGL((conv_halo_kernel<256>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
   else
-    hipLaunchKernelGGL((conv_halo_kernel<128>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none);
+    hipLaunchKernelGGL((conv_halo_kernel<128>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
+  return true;
+}
+
+// ---- flat-raster blocks with split K
+static bool flat_ok(const GemmArgs& a) {
+  return a.cv_kb == 32 && a.cv_stride == 1 && a.cv_OH == a.cv_IH && a.cv_OW == a.cv_IW && a.K == 9 * a.cv_C &&
+         a.cv_OW + 1 <= FLAT_MAX_WP && a.N % 128 == 0 && (a.sp_half == 0x7fffffff || a.sp_half % 32 == 0);
+}
+static int64_t flat_blocks(const GemmArgs& a) {
+  return ((int64_t)(a.M / (a.cv_OH * a.cv_OW)) * (a.cv_OH + 1) * (a.cv_OW + 1) + 255) / 256;
+}
+
+int conv_halo_flat_split(const GemmArgs& a, int slots, int force) {
+  if (!flat_ok(a)) return 0;
+  const int64_t tiles = flat_blocks(a) * (a.N / 128);
+  const int nslice = a.K / 288;
+  if (force > 0) return force < nslice ? force : nslice;
+  // fill the resident slots (2 per CU) once, with at least two slices (18 K steps) per part and at most 8 parts:
+  // the last arriver sums the parts' 128-KiB slabs alone (flat_sweep.py, 8 views: l4rn@19 83.6 us on stream-K,
+  // 93.4 with 19 parts, 55.8 with 8; rn4@19 51.9 / 54.6 with 12 / 34.7 with 8; rn3@37 93.5 -> 59.2 with 5)
+  int64_t s = slots / (tiles > 0 ? tiles : 1);
+  int cap = nslice / 2 > 1 ? nslice / 2 : 1;
+  if (cap > 8) cap = 8;
+  if (s > cap) s = cap;
+  return s < 1 ? 1 : (int)s;
+}
+
+int64_t conv_halo_flat_workspace_bytes(const GemmArgs& a, int nsplit, int64_t ticket_bytes) {
+  if (!flat_ok(a) || nsplit <= 1) return 0;
+  const int64_t tiles = flat_blocks(a) * (a.N / 128);
+  if (tiles * 4 > ticket_bytes) return -1;  // more tiles than ticket words: not this kernel
+  return ticket_bytes + tiles * nsplit * 256 * 128 * 4;
+}
+
+bool launch_conv_halo_flat(const GemmArgs& a, int nsplit, void* ws, int64_t ws_bytes, int64_t ticket_bytes,
+                           hipStream_t stream) {
+  if (!flat_ok(a) || nsplit < 1) return false;
+  const int64_t nblk = flat_blocks(a), tiles = nblk * (a.N / 128);
+  if (tiles * nsplit >= (int64_t(1) << 31)) return false;
+  HSplit sp{nsplit, (int)nblk, nullptr, nullptr};
+  if (nsplit > 1) {
+    const int64_t need = conv_halo_flat_workspace_bytes(a, nsplit, ticket_bytes);
+    if (need <= 0 || !ws || ws_bytes < need) return false;
+    sp.tickets = reinterpret_cast<int*>(ws);
+    sp.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + ticket_bytes);
+  }
+  const HeadOut none{};
+  hipLaunchKernelGGL((conv_halo_kernel<128, false, 16, true>), dim3((unsigned)(tiles * nsplit)), dim3(HT), 0, stream,
+                     a, none, sp);
   return true;
 }
 
@@ -365,7 +528,8 @@ bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b
   h.w6 = w6; h.b6 = b6; h.pose = pose; h.scale = scale;
   h.pts3d = pts3d; h.pts3d_cam = pts3d_cam; h.rays = rays; h.depth = depth; h.conf = conf; h.logits = logits;
   h.mask = mask;
-  hipLaunchKernelGGL((conv_halo_kernel<128, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h);
+  hipLaunchKernelGGL((conv_halo_kernel<128, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h,
+                     HSplit{1, 0, nullptr, nullptr});
   return true;
 }
 

@@ -323,7 +323,16 @@ static bool pick_halo(int M, int N, int OH, int OW, int kb) {
 // 8-row blocks with 256-wide tiles only where they cover fewer idle rows than 16-row blocks (148^2: 152 vs 160
 // rows; 74^2: 80 either way, and there the 128-wide 16x16 tile is faster: rn2@74 149.9 vs 156.4 us)
 static bool halo_rows8(const GemmArgs& a) {
-  return a.N % 256 == 0 && g_halo == 1 && ((a.cv_OH + 7) / 8) * 8 < ((a.cv_OH + 15) / 16) * 16;
+  return a.N % 256 == 0 && (g_halo == 1 || g_halo == 3) && ((a.cv_OH + 7) / 8) * 8 < ((a.cv_OH + 15) / 16) * 16;
+}
+
+// Flat-raster halo conv with split K (conv_halo.hip FLAT) for the stride-1 convs too small for 16x16 blocks (the
+// 19^2 / 37^2 DPT convs: 26-144 tiles of 16x16 blocks, 41-65 % of their pixels idle), which the stream-K implicit
+// GEMM ran before.  Returns the K part count, 0 = not this kernel.
+static int g_halo_split = 0;  // mapa_gemm_tune(MAPA_TUNE_HALO_SPLIT, .): 0 = automatic part count
+static int pick_flat(const GemmArgs& a) {
+  if (g_halo != 1 || pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb)) return 0;
+  return conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split);
 }
 
 static int g_forced = -1;  // -1: not read yet; 0: automatic; else a kernel variant code (tuning / tests)
@@ -447,7 +456,12 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const bool halo = conv && d->dtype == MAPA_BF16 &&
                     (forced ? (forced >= 2584 && forced <= 2586) || forced == 2588
                             : pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb));
-  if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
+  const int flat = !conv || d->dtype != MAPA_BF16 ? 0
+                   : forced ? (forced == 2589 ? conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split) : 0)
+                            : pick_flat(a);
+  if (flat && launch_conv_halo_flat(a, flat, d->workspace, d->workspace_bytes, GEMM_TICKET_BYTES, stream)) {
+    // launched (flat-raster halo conv, split K)
+  } else if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
   } else if (halo && (forced ? launch_conv_halo(a, forced == 2585 || forced == 2588 ? 256 : 128, stream,
                                                 forced == 2588 ? 8 : 16)
@@ -488,8 +502,11 @@ extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6,
 }
 
 extern "C" int mapa_gemm_tune(int key, int value) {
-  MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK, "mapa_gemm_tune: unknown key %d", key);
-  if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 ? 2 : value ? 1 : 0;
+  MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK || key == MAPA_TUNE_HALO_SPLIT,
+                 "mapa_gemm_tune: unknown key %d", key);
+  MAPA_CHECK_ARG(key != MAPA_TUNE_HALO_SPLIT || (value >= 0 && value <= 64), "mapa_gemm_tune: split %d", value);
+  if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 || value == 3 ? value : value ? 1 : 0;
+  else if (key == MAPA_TUNE_HALO_SPLIT) g_halo_split = value;
   else g_tail_sk = value ? 1 : 0;
   return 0;
 }
@@ -497,7 +514,7 @@ extern "C" int mapa_gemm_tune(int key, int value) {
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
                      (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582) ||
-                     (variant >= 2584 && variant <= 2588),
+                     (variant >= 2584 && variant <= 2589),
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;
@@ -505,6 +522,17 @@ extern "C" int mapa_gemm_set_variant(int variant) {
 
 extern "C" int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d) {
   if (!d || d->dtype != MAPA_BF16 || d->M <= 0 || d->N <= 0 || d->K <= 0) return 0;
+  if (d->a_mode == MAPA_A_CONV3X3) {
+    GemmArgs a;
+    if (gemm_args(d, a) != 0) return 0;  // a bad descriptor is reported by mapa_gemm itself
+    const int forced = forced_variant();
+    const int flat = forced ? (forced == 2589 ? conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split) : 0)
+                            : pick_flat(a);
+    if (flat) {
+      const int64_t b = conv_halo_flat_workspace_bytes(a, flat, GEMM_TICKET_BYTES);
+      if (b >= 0) return b;
+    }
+  }
   const int sk = pick_streamk(d->dtype, d->a_mode == MAPA_A_CONV3X3, d->M, d->N, d->K);
   return sk ? streamk_workspace_bytes(d->M, d->N, sk - 2580) : 0;
 }

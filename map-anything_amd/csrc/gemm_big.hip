@@ -794,7 +794,7 @@ int gemm_streamk_slots(int variant) {
 
 // Ticket words live in a fixed-size head shared by every shape (a shape-dependent split would let one shape's slabs
 // overwrite another's tickets, which must stay zero between calls); shapes with more tiles use the DP schedule.
-constexpr int64_t SK_MAX_TILES = 65536, SK_TICKET_BYTES = SK_MAX_TILES * 4;
+constexpr int64_t SK_MAX_TILES = GEMM_TICKET_BYTES / 4, SK_TICKET_BYTES = GEMM_TICKET_BYTES;
 
 int64_t streamk_workspace_bytes(int M, int N, int variant) {
   if (variant < 0 || variant > 2) return 0;

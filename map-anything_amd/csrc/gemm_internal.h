@@ -347,6 +347,16 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh = 16
 bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b6, const float* pose,
                               const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
                               float* conf, float* logits, uint8_t* mask, hipStream_t stream);
+// The halo conv on flat-raster blocks with the 32-channel slices split over nsplit workgroups per tile (maps up to
+// 62 pixels wide; conv_halo.hip).  conv_halo_flat_split: the part count for `slots` resident workgroups (force > 0:
+// that many, capped at the slice count), 0 if the conv does not qualify.  Workspace: the ticket head of the GEMM
+// workspace (GEMM_TICKET_BYTES, shared with stream-K) + the parts' fp32 slabs; none for nsplit = 1.  The launch
+// returns false if the conv does not qualify or the workspace is missing / too small.
+constexpr int64_t GEMM_TICKET_BYTES = 65536 * 4;
+int conv_halo_flat_split(const GemmArgs& a, int slots, int force);
+int64_t conv_halo_flat_workspace_bytes(const GemmArgs& a, int nsplit, int64_t ticket_bytes);
+bool launch_conv_halo_flat(const GemmArgs& a, int nsplit, void* ws, int64_t ws_bytes, int64_t ticket_bytes,
+                           hipStream_t stream);
 // Stream-K bf16 kernel (gemm_big.hip): variant 0 = 256x128 tiles, 2 workgroups per CU; 1 = 256x256, 1 per CU.
 // streamk_workspace_bytes: bytes the launch needs (ticket words + partial-sum slabs); launch returns false if
 // the workspace is missing or too small.

@@ -155,6 +155,29 @@ MAPA_HD void halo_block(int bid, int imgs, int nby, int nbx, int ntn, int& img, 
   img = t / nby;
 }
 
+// ---- flat-raster halo conv (conv_halo.hip FLAT): the images laid end to end as one raster of rows of OW + 1
+// positions (the last a zero column: the left and right neighbour of the next / previous row's edge pixels) and
+// OH + 1 rows per image (the last a zero row, likewise shared), cut into blocks of 256 consecutive positions.  Every
+// 3x3 tap of a position is then a constant shift, dy*(OW+1) + dx, inside one 1-D window of 256 + 2*(OW+1) + 2.
+// Position P -> pixel (img, r, j); false for the pad positions and for P outside the raster.
+MAPA_HD bool flat_pixel(int P, int Wp, int Hp, int OH, int OW, int imgs, int& img, int& r, int& j) {
+  if (P < 0) return false;
+  const int R = P / Wp;
+  j = P - R * Wp;
+  img = R / Hp;
+  r = R - img * Hp;
+  return img < imgs && r < OH && j < OW;
+}
+// block id -> (flat block, column tile, K part) over nblk * ntn * nsplit workgroups: XCD-contiguous ranges with the
+// K parts of one tile adjacent, so the parts' partial-sum slabs meet in one L2
+MAPA_HD void halo_flat_tile(int bid, int nblk, int ntn, int nsplit, int& fb, int& tn, int& kp) {
+  int t = xcd_remap(bid, nblk * ntn * nsplit);
+  kp = t % nsplit;
+  t /= nsplit;
+  tn = t % ntn;
+  fb = t / ntn;
+}
+
 // ---- 3x3 conv as implicit GEMM: logical K column kc -> tap (0..8) and logical input channel, in the K order of
 // mapa_gemm_desc.conv_kblock (0: tap-major k = tap*C + c; kb: channel-block-major k = (c/kb)*9kb + tap*kb + c%kb)
 MAPA_HD void conv_kmap_logical(int kc, int kb, int C, int& tap, int& c) {

@@ -272,12 +272,13 @@ def attention_workspace(d) -> torch.Tensor:
     return ws
 
 
-TUNE_CONV_HALO, TUNE_TAIL_STREAMK = 0, 1
+TUNE_CONV_HALO, TUNE_TAIL_STREAMK, TUNE_HALO_SPLIT = 0, 1, 2
 
 
 def gemm_tune(key: int, value: int):
     """A-B hooks of the automatic kernel choice (include/mapa.h mapa_gemm_tune): TUNE_CONV_HALO (stride-1 head convs
-    on the LDS halo-window kernel, default on), TUNE_TAIL_STREAMK (tail-only stream-K for nearly empty last waves)."""
+    on the LDS halo-window kernel, default on), TUNE_TAIL_STREAMK (tail-only stream-K for nearly empty last waves),
+    TUNE_HALO_SPLIT (K part count of the flat-raster halo conv, 0 = automatic)."""
     check(lib().mapa_gemm_tune(key, value), "mapa_gemm_tune")
     _WS_NEED.clear()
 
@@ -331,7 +332,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     if pixshuf is not None:
         d.out_mode = OUT_PIXSHUF
         d.ps_s, d.ps_h, d.ps_w, d.ps_cout = pixshuf
-    key = (d.dtype, M, N, K, d.a_mode)
+    key = (d.dtype, M, N, K, d.a_mode, d.a_split, d.conv_kblock) + (tuple(conv) if conv is not None else ())
     need = _WS_NEED.get(key)
     if need is None:
         need = _WS_NEED[key] = int(lib().mapa_gemm_workspace_bytes(ctypes.byref(d)))

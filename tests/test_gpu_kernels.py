@@ -194,6 +194,71 @@ def test_conv3x3_halo_window(nat, variant, n, H, W, C, Co):
     assert torch.equal(out, again)
 
 
+@pytest.mark.parametrize("split", [0, 1, 2, 3, 7])
+@pytest.mark.parametrize("n,H,W,C,Co", [(2, 37, 37, 256, 256), (1, 19, 19, 96, 128), (2, 37, 29, 64, 256),
+                                        (3, 13, 21, 32, 128), (1, 61, 61, 64, 128), (2, 5, 7, 32, 128)])
+def test_conv3x3_halo_flat_split(nat, split, n, H, W, C, Co):
+    """The halo conv on flat-raster blocks (256 consecutive positions of the images' raster with one zero column per
+    row and one zero row per image; 1-D window of 256 + 2(W+1) + 2 positions) with the 32-channel slices split over
+    `split` workgroups per tile (0 = automatic; the parts meet in fp32 slabs, summed in part order by the last
+    arriver): every epilogue output, blocks straddling rows and images, maps up to 61 pixels wide, bitwise repeatable,
+    tickets back to zero."""
+    x = _rand(n, C, H, W, seed=56)
+    w = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=57)
+    b, r = _rand(Co, seed=58), _rand(n * H * W, Co, seed=59)
+    xl, wl = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    ref = F.conv2d(xl.float(), wl.float(), b, padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    ref = r + torch.relu(ref)
+    x_nhwc = xl.permute(0, 2, 3, 1).contiguous()
+    wkb = wl.permute(0, 2, 3, 1).reshape(Co, 9, C // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
+    wkb._mapa_kblock = 32
+    M = n * H * W
+    out = torch.full((M, Co), float("nan"), device="cuda")
+    lp = torch.empty(M, Co, device="cuda", dtype=torch.bfloat16)
+    s3 = torch.empty(M, 2 * Co, device="cuda", dtype=torch.bfloat16)
+    nat.gemm_set_variant(2589)
+    nat.gemm_tune(nat.TUNE_HALO_SPLIT, split)
+    try:
+        nat.gemm(x_nhwc, wkb, M, Co, 9 * C, bias=b, act=nat.ACT_RELU, resid1=r, out_f32=out, out_lp=lp, out_s3=s3,
+                 conv=(C, H, W, H, W, 1))
+        again = torch.empty_like(out)
+        nat.gemm(x_nhwc, wkb, M, Co, 9 * C, bias=b, act=nat.ACT_RELU, resid1=r, out_f32=again,
+                 conv=(C, H, W, H, W, 1))
+        torch.cuda.synchronize()
+    finally:
+        nat.gemm_set_variant(0)
+        nat.gemm_tune(nat.TUNE_HALO_SPLIT, 0)
+    assert rel_l2(out.cpu(), ref.cpu()) < 1e-4
+    assert rel_l2(lp.float().cpu(), ref.cpu()) < 5e-3
+    assert torch.equal(s3, _split_expect(out))
+    assert torch.equal(out, again)
+    ws = nat.gemm_workspace(0)
+    assert int(ws[: 4 * 65536].count_nonzero()) == 0
+
+
+def test_split_precision_conv_halo_flat(nat):
+    """Split-precision activations through the flat-raster split-K halo conv at the DPT's 37^2 (automatic choice:
+    no forced variant) stay within ~1e-5 of the fp64 conv."""
+    n, h, w, C, Co = 3, 37, 37, 256, 256
+    x = _rand(n, C, h, w, seed=60)
+    wt = _rand(Co, C, 3, 3, scale=C ** -0.5 / 3, seed=61)
+    ref = F.conv2d(x.cpu().double(), wt.cpu().double(), padding=1).permute(0, 2, 3, 1).reshape(-1, Co)
+    M = n * h * w
+    xr = x.permute(0, 2, 3, 1).reshape(M, C).contiguous()
+    a = torch.empty(M, 2 * C, dtype=torch.bfloat16, device="cuda")
+    nat.split_bf16x3(xr, M, C, C, a)
+    wk = wt.permute(0, 2, 3, 1).reshape(Co, 9, C)
+    whi = wk.to(torch.bfloat16)
+    wlo = (wk - whi.float()).to(torch.bfloat16)
+    wp = torch.stack([whi, wlo, whi], 2).reshape(Co, 9, 3 * C)
+    wp = wp.reshape(Co, 9, 3 * C // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
+    wp._mapa_split = True
+    wp._mapa_kblock = 32
+    out = torch.empty(M, Co, device="cuda")
+    nat.gemm(a, wp, M, Co, 9 * 3 * C, out_f32=out, conv=(3 * C, h, w, h, w, 1))
+    assert rel_l2(out.cpu(), ref) < 2e-5
+
+
 def test_split_precision_conv_halo_window(nat):
     """Split-precision activations ([hi | lo] stored, [hi | hi | lo] logical, 32-channel slices mapped per slice)
     through the halo-window conv stay within ~1e-5 of the fp64 conv."""

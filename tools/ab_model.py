@@ -37,6 +37,9 @@ def main():
     elif what == "halo8":  # N = 256 halo convs: 8x16-pixel blocks / 256-wide tiles vs 16x16 / 128-wide
         arms = [("rows8", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 1)),
                 ("rows16", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 2))]
+    elif what == "flat":  # 19^2 / 37^2 stride-1 head convs: flat-raster split-K halo conv vs stream-K implicit GEMM
+        arms = [("flat", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 1)),
+                ("streamk", lambda: nat.gemm_tune(nat.TUNE_CONV_HALO, 3))]
     elif what == "tailsk":
         arms = [("tailsk", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 1)),
                 ("dataparallel", lambda: nat.gemm_tune(nat.TUNE_TAIL_STREAMK, 0))]

@@ -122,6 +122,47 @@ static void check_halo(int imgs, int nby, int nbx, int ntn) {
   }
 }
 
+// flat-raster halo conv: (a) the workgroup -> (block, column tile, K part) map is a bijection, (b) over the blocks'
+// positions every pixel of every image is produced exactly once, and (c) every 3x3 neighbour of a pixel sits at its
+// position + dy*Wp + dx, inside the block's window [P0 - Wp - 1, P0 + 256 + Wp + 1) and <= 384 positions long, and
+// reads a zero (a pad position) exactly where the conv's zero padding is
+static void check_flat(int imgs, int OH, int OW, int ntn, int nsplit) {
+  const int Wp = OW + 1, Hp = OH + 1;
+  const int nblk = (int)(((int64_t)imgs * Hp * Wp + 255) / 256);
+  REQUIRE(256 + 2 * Wp + 2 <= 384, "window %d", 256 + 2 * Wp + 2);
+  const int n = nblk * ntn * nsplit;
+  std::vector<char> seen((size_t)n, 0);
+  for (int b = 0; b < n; ++b) {
+    int fb, tn, kp;
+    halo_flat_tile(b, nblk, ntn, nsplit, fb, tn, kp);
+    REQUIRE(fb >= 0 && fb < nblk && tn >= 0 && tn < ntn && kp >= 0 && kp < nsplit, "flat %d", b);
+    char& s = seen[((size_t)fb * ntn + tn) * nsplit + kp];
+    REQUIRE(!s, "flat tile twice");
+    s = 1;
+  }
+  std::vector<char> pix((size_t)imgs * OH * OW, 0);
+  for (int P = 0; P < nblk * 256; ++P) {
+    int img, r, j;
+    if (!flat_pixel(P, Wp, Hp, OH, OW, imgs, img, r, j)) continue;
+    REQUIRE(img < imgs && r >= 0 && r < OH && j >= 0 && j < OW, "P %d", P);
+    char& s = pix[((size_t)img * OH + r) * OW + j];
+    REQUIRE(!s, "pixel twice");
+    s = 1;
+    const int P0 = P / 256 * 256;
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int Q = P + dy * Wp + dx;
+        REQUIRE(Q >= P0 - Wp - 1 && Q < P0 + 256 + Wp + 1, "tap outside the window");
+        int i2, r2, j2;
+        const bool real = flat_pixel(Q, Wp, Hp, OH, OW, imgs, i2, r2, j2);
+        const bool inside = r + dy >= 0 && r + dy < OH && j + dx >= 0 && j + dx < OW;
+        REQUIRE(real == inside, "tap (%d,%d) of (%d,%d,%d): real %d inside %d", dy, dx, img, r, j, real, inside);
+        if (real) REQUIRE(i2 == img && r2 == r + dy && j2 == j + dx, "tap lands on the wrong pixel");
+      }
+  }
+  for (char c : pix) REQUIRE(c, "pixel never produced");
+}
+
 static void check_kmap(int C, int kb) {
   std::vector<char> seen((size_t)9 * C, 0);
   for (int kc = 0; kc < 9 * C; ++kc) {
@@ -197,6 +238,14 @@ int main() {
     for (int bh : {8, 16})
       for (int ntn : {1, 2})
         for (int imgs : {1, 2, 8}) check_halo(imgs, (hw + bh - 1) / bh, (hw + 15) / 16, ntn);
+
+  for (int hw : {37, 19, 5, 61, 1})
+    for (int imgs : {1, 2, 8, 3})
+      for (int ntn : {1, 2, 6})
+        for (int nsplit : {1, 5, 12}) check_flat(imgs, hw, hw, ntn, nsplit);
+  check_flat(2, 37, 29, 2, 3);
+  check_flat(3, 13, 21, 1, 1);
+  check_flat(250, 37, 37, 2, 1);
 
   // conv K orders: logical (split) channel counts of the path convs
   const int convC[] = {96 * 3, 192 * 3, 384 * 3, 768 * 3, 256 * 3, 128 * 3, 96, 192, 256, 768, 588, 3 * 592};
