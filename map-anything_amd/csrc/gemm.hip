@@ -353,6 +353,8 @@ static int forced_variant() {
 // convs at 19x19 and 37x37: K = 27*C = 6912..20736, M = views*361 or views*1369) leave most of the chip idle in
 // the data-parallel schedule; splitting K over the persistent grid measured 1.5-3.2x faster (kbench, 8 views:
 // layer4_rn 392 -> 122 us, input_process.3 conv 394 -> 177, layer3_rn 194 -> 102, refinenet3/4 convs 142 -> 100).
+// The stride-1 ones among them now run the flat-raster halo conv (pick_flat, checked first in mapa_gemm); the
+// stride-2 input_process.3 conv stays here.
 int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   const int f = forced_variant();
   if (f) return f >= 2580 && f <= 2582 ? f : 0;
