@@ -117,7 +117,9 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 // one output row's (pixel, channel-group) pairs, y over output rows (strided past 65535 rows), so the row's source
 // rows and weights are block-uniform and a thread splits its index with one shift (c8 a power of two) — the
 // grid-stride form spent more on 64-bit index division than on its memory traffic.
-template <typename TI, typename TO, bool S3 = false>  // S3: split operand rows [hi | lo] (2C wide)
+// BIL_ROWS: output rows per thread (8 for the x2 upsamples: 74 -> 148 60.3 -> 42.3 us, 148 -> 296 split 222 -> 161;
+// 4 for 296 -> 518: 339 -> 254, 264 with 8; kbench 'bil', 8 views, interleaved against the one-row kernel)
+template <typename TI, typename TO, bool S3 = false, int BIL_ROWS = 4>  // S3: split operand rows [hi | lo] (2C wide)
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                    int OW, int c8_shift, TO* __restrict__ out) {
   const int c8 = C / 8;
@@ -131,40 +133,59 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
   const int x0 = (int)fx;
   const int x1 = x0 + (x0 < IW - 1 ? 1 : 0);
   const float lx1 = fx - x0, lx0 = 1.f - lx1;
-  for (int r = blockIdx.y; r < n * OH; r += gridDim.y) {
-    const int im = r / OH, oy = r - im * OH;
-    const float fy = sh * oy;
-    const int y0 = (int)fy;
-    const int y1 = y0 + (y0 < IH - 1 ? 1 : 0);
-    const float ly1 = fy - y0, ly0 = 1.f - ly1;
-    const TI* base = in + (size_t)im * IH * IW * C + c;
-    const size_t o00 = ((size_t)y0 * IW + x0) * C, o01 = ((size_t)y0 * IW + x1) * C;
-    const size_t o10 = ((size_t)y1 * IW + x0) * C, o11 = ((size_t)y1 * IW + x1) * C;
-    TO* op = out + ((size_t)r * OW + ox) * (S3 ? 2 * C : C) + c;
-    f32x4 a0, a1, b0, b1, c0, c1, d0, d1;
-    load8(base + o00, a0, a1);
-    load8(base + o01, b0, b1);
-    load8(base + o10, c0, c1);
-    load8(base + o11, d0, d1);
-    const f32x4 r0 = ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0);
-    const f32x4 r1 = ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1);
-    if constexpr (S3) {  // 8 channels: one 16-B store of hi and one of lo
-      uint4 h, l;
-      uint32_t* hp = &h.x;
-      uint32_t* lp = &l.x;
+  // blockIdx.y walks groups of BIL_ROWS output rows: each row re-uses the previous row's source rows when they
+  // coincide (align_corners upsampling: rows oy and oy+1 share y0, or the previous row's y1 is this row's y0), so
+  // the 296 -> 518 resize loads ~1.2 instead of 2 source rows per output row through L2
+  const int rows = n * OH;
+  for (int r = BIL_ROWS * blockIdx.y; r < rows; r += BIL_ROWS * gridDim.y) {
+    f32x4 a0, a1, b0, b1, c0, c1, d0, d1;  // taps (y0, x0), (y0, x1), (y1, x0), (y1, x1) of the current row
+    int pim = -1, py0 = -1, py1 = -1;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float v0 = k < 2 ? r0[2 * k] : r1[2 * k - 4], v1 = k < 2 ? r0[2 * k + 1] : r1[2 * k - 3];
-        const bf16_t h0 = f32_to_bf16(v0), h1 = f32_to_bf16(v1);
-        hp[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-        lp[k] = pack_bf16x2(v0 - bf16_to_f32(h0), v1 - bf16_to_f32(h1));
+    for (int h = 0; h < BIL_ROWS; ++h) {
+      const int rr = r + h;
+      if (rr >= rows) break;
+      const int im = rr / OH, oy = rr - im * OH;
+      const float fy = sh * oy;
+      const int y0 = (int)fy;
+      const int y1 = y0 + (y0 < IH - 1 ? 1 : 0);
+      const float ly1 = fy - y0, ly0 = 1.f - ly1;
+      const TI* base = in + (size_t)im * IH * IW * C + c;
+      const size_t o00 = ((size_t)y0 * IW + x0) * C, o01 = ((size_t)y0 * IW + x1) * C;
+      const size_t o10 = ((size_t)y1 * IW + x0) * C, o11 = ((size_t)y1 * IW + x1) * C;
+      if (im == pim && y0 == py0 && y1 == py1) {
+        // same source rows as the previous row
+      } else if (im == pim && y0 == py1) {
+        a0 = c0; a1 = c1; b0 = d0; b1 = d1;  // the previous row's bottom taps are this row's top taps
+        load8(base + o10, c0, c1);
+        load8(base + o11, d0, d1);
+      } else {
+        load8(base + o00, a0, a1);
+        load8(base + o01, b0, b1);
+        load8(base + o10, c0, c1);
+        load8(base + o11, d0, d1);
       }
-      typedef uint32_t nt4 __attribute__((ext_vector_type(4)));
-      // 1.1 GB at 518^2: streamed past the caches
-      __builtin_nontemporal_store(nt4{h.x, h.y, h.z, h.w}, reinterpret_cast<nt4*>(op));
-      __builtin_nontemporal_store(nt4{l.x, l.y, l.z, l.w}, reinterpret_cast<nt4*>(op + C));
-    } else {
-      store8(op, r0, r1);
+      pim = im; py0 = y0; py1 = y1;
+      TO* op = out + ((size_t)rr * OW + ox) * (S3 ? 2 * C : C) + c;
+      const f32x4 r0 = ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0);
+      const f32x4 r1 = ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1);
+      if constexpr (S3) {  // 8 channels: one 16-B store of hi and one of lo
+        uint4 hv, lv;
+        uint32_t* hp = &hv.x;
+        uint32_t* lp = &lv.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float v0 = k < 2 ? r0[2 * k] : r1[2 * k - 4], v1 = k < 2 ? r0[2 * k + 1] : r1[2 * k - 3];
+          const bf16_t h0 = f32_to_bf16(v0), h1 = f32_to_bf16(v1);
+          hp[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+          lp[k] = pack_bf16x2(v0 - bf16_to_f32(h0), v1 - bf16_to_f32(h1));
+        }
+        typedef uint32_t nt4 __attribute__((ext_vector_type(4)));
+        // 1.1 GB at 518^2: streamed past the caches
+        __builtin_nontemporal_store(nt4{hv.x, hv.y, hv.z, hv.w}, reinterpret_cast<nt4*>(op));
+        __builtin_nontemporal_store(nt4{lv.x, lv.y, lv.z, lv.w}, reinterpret_cast<nt4*>(op + C));
+      } else {
+        store8(op, r0, r1);
+      }
     }
   }
 }
@@ -394,34 +415,44 @@ extern "C" int mapa_add_rowvec(float* x, int64_t ldx, int r0, int r1, int dim, c
   return 0;
 }
 
+template <int RW>
+static void bilinear_launch(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH, int OW,
+                            int c8_shift, void* out, int out_dtype, hipStream_t stream) {
+  const int64_t groups = ((int64_t)n * OH + RW - 1) / RW;
+  const dim3 g((unsigned)((OW * (C / 8) + TPB - 1) / TPB), (unsigned)std::min<int64_t>(groups, 65535)), b(TPB);
+  if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32)
+    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, true, RW>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
+                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
+  else if (out_dtype == MAPA_BF16X3)
+    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, true, RW>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW,
+                       C, OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
+  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
+    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, false, RW>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW,
+                       C, OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
+  else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16)
+    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, false, RW>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
+                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
+  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_F32)
+    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, float, false, RW>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW,
+                       C, OHf, OWf, OH, OW, c8_shift, (float*)out);
+  else
+    hipLaunchKernelGGL((bilinear_ac_kernel<float, float, false, RW>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
+                       OHf, OWf, OH, OW, c8_shift, (float*)out);
+}
+
 extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                 int OW, void* out, int out_dtype, hipStream_t stream) {
   MAPA_CHECK_ARG(in && out && C % 8 == 0 && OH <= OHf && OW <= OWf, "mapa_bilinear_ac: bad args (C %% 8 == 0)");
   const int c8 = C / 8, c8_shift = (c8 & (c8 - 1)) == 0 ? __builtin_ctz(c8) : -1;
-  const int rows = n * OH;
-  MAPA_CHECK_ARG((int64_t)OW * c8 < (1LL << 31) && (int64_t)n * OH < (1LL << 31), "mapa_bilinear_ac: too large");
-  const dim3 g((unsigned)((OW * c8 + TPB - 1) / TPB), (unsigned)std::min(rows, 65535)), b(TPB);
+  MAPA_CHECK_ARG((int64_t)OW * c8 < (1LL << 31) && (int64_t)n * OH + 8 * 65536 < (1LL << 31),
+                 "mapa_bilinear_ac: too large");
   MAPA_CHECK_ARG((in_dtype == MAPA_F32 || in_dtype == MAPA_BF16) &&
                      (out_dtype == MAPA_F32 || out_dtype == MAPA_BF16 || out_dtype == MAPA_BF16X3),
                  "mapa_bilinear_ac: bad dtypes");
-  if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32)
-    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, true>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (out_dtype == MAPA_BF16X3)
-    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, true>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
-    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
-                       OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16)
-    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t>), g, b, 0, stream, (const float*)in, n, IH, IW, C, OHf, OWf,
-                       OH, OW, c8_shift, (bf16_t*)out);
-  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_F32)
-    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, float>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW, C, OHf,
-                       OWf, OH, OW, c8_shift, (float*)out);
+  if (OH >= 2 * IH - 1)
+    bilinear_launch<8>(in, in_dtype, n, IH, IW, C, OHf, OWf, OH, OW, c8_shift, out, out_dtype, stream);
   else
-    hipLaunchKernelGGL((bilinear_ac_kernel<float, float>), g, b, 0, stream, (const float*)in, n, IH, IW, C, OHf, OWf,
-                       OH, OW, c8_shift, (float*)out);
+    bilinear_launch<4>(in, in_dtype, n, IH, IW, C, OHf, OWf, OH, OW, c8_shift, out, out_dtype, stream);
   MAPA_CHECK_LAUNCH("mapa_bilinear_ac");
   return 0;
 }

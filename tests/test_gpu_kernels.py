@@ -531,10 +531,12 @@ def test_layernorm(nat, dim):
     assert rel_l2(yg.cpu(), F.layer_norm(x[idx], (dim,), w, b, 1e-6).cpu()) < 1e-6
 
 
-@pytest.mark.parametrize("IH,IW,OHf,OWf,OH,OW", [(19, 19, 38, 38, 37, 37), (37, 37, 74, 74, 74, 74),
-                                                 (296, 296, 518, 518, 518, 518), (16, 16, 224, 224, 224, 224)])
-def test_bilinear_align_corners(nat, IH, IW, OHf, OWf, OH, OW):
-    n, C = 2, 128
+@pytest.mark.parametrize("n,IH,IW,OHf,OWf,OH,OW", [(2, 19, 19, 38, 38, 37, 37), (2, 37, 37, 74, 74, 74, 74),
+                                                   (2, 296, 296, 518, 518, 518, 518), (2, 16, 16, 224, 224, 224, 224),
+                                                   (1, 19, 19, 38, 38, 37, 37), (3, 7, 5, 13, 9, 13, 9)])
+def test_bilinear_align_corners(nat, n, IH, IW, OHf, OWf, OH, OW):
+    """Row pairs share source rows (odd row counts, pairs straddling two images included)."""
+    C = 128
     x = _rand(n, C, IH, IW, seed=23)
     ref = F.interpolate(x, size=(OHf, OWf), mode="bilinear", align_corners=True)[:, :, :OH, :OW]
     out = torch.empty(n, OH, OW, C, device="cuda")
