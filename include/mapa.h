@@ -74,9 +74,10 @@ typedef struct {
   int64_t ldo;
   int out_mode; /* MAPA_OUT_ROWMAJOR or MAPA_OUT_PIXSHUF (n = (ky*s+kx)*cout + co, m = img*h*w + y*w + x) */
   int ps_s, ps_h, ps_w, ps_cout;
-  /* Optional scratch for the stream-K schedule (bf16 shapes whose tile count divides badly over the CUs):
-   * device memory, ZERO-FILLED before its first use, used by one stream at a time; mapa_gemm leaves it zeroed
-   * again when each call completes.  NULL / too small -> the data-parallel schedule (same results to rounding). */
+  /* Optional scratch for the stream-K schedule (bf16 shapes whose tile count divides badly over the CUs) and for
+   * the split-K flat-raster halo conv (the 19^2 / 37^2 convs): device memory, ZERO-FILLED before its first use, used
+   * by one stream at a time; mapa_gemm leaves it zeroed again when each call completes.  Size:
+   * mapa_gemm_workspace_bytes.  NULL / too small -> a data-parallel schedule (same results to rounding). */
   void* workspace;
   int64_t workspace_bytes;
   /* Split-precision operand outputs (dtype BF16 only; NULL = off): row r of out_s3 is 2*ld bf16 wide (ld = ldo, or
