@@ -76,7 +76,8 @@ typedef struct {
   int ps_s, ps_h, ps_w, ps_cout;
   /* Optional scratch for the stream-K schedule (bf16 shapes whose tile count divides badly over the CUs) and for
    * the split-K flat-raster halo conv (the 19^2 / 37^2 convs): device memory, ZERO-FILLED before its first use, used
-   * by one stream at a time; mapa_gemm leaves it zeroed again when each call completes.  Size:
+   * by one stream at a time.  Only its head (the 256 KiB of ticket words) is returned to zero when each call
+   * completes; the rest holds fp32 partial-sum slabs (scratch data) afterwards.  Size:
    * mapa_gemm_workspace_bytes.  NULL / too small -> a data-parallel schedule (same results to rounding). */
   void* workspace;
   int64_t workspace_bytes;

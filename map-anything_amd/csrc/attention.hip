@@ -119,17 +119,16 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
   // Staging: piece = i*NW + wave is 8 rows x 128 B of K (piece < 8) or V; this lane's 16 B sit at tile row
   // srow[i] (XOR-swizzled 16-B column on the source so the LDS image stays lane-linear).  The byte offset inside
   // a tile is loop-invariant; a full tile adds one wave-uniform base per tile.
-  int srow[NP];
+  // (the row and column are recomputed from the lane where the slow path needs them: keeping them as arrays
+  // costs the segmented kernel its last free registers)
+  auto srow = [&](int i) __attribute__((always_inline)) { return ((i * NW + wave) & 7) * 8 + (lane >> 3); };
+  auto scol = [&](int i) __attribute__((always_inline)) {
+    const int row = srow(i), pos = lane & 7;
+    return (i >= NP / 2 ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7))) * 16;
+  };
   uint32_t soff[NP];
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const int piece = i * NW + wave;
-    const bool isv = i >= NP / 2;
-    const int row = (piece & 7) * 8 + (lane >> 3), pos = lane & 7;
-    const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
-    srow[i] = row;
-    soff[i] = (uint32_t)(row * (isv ? p.vr : p.kr) * 2 + c * 16);
-  }
+  for (int i = 0; i < NP; ++i) soff[i] = (uint32_t)(srow(i) * (i >= NP / 2 ? p.vr : p.kr) * 2 + scol(i));
   // physical row of logical key `key0` when the whole tile [key0, key0+64) sits in one K/V segment, else -1
   auto seg_base = [&](int key0) -> int {
     if (!SEG) return key0;
@@ -169,9 +168,9 @@ __global__ void __launch_bounds__(NW * 64, 2) attn_fwd_bf16(AttnArgs p, SplitArg
 #pragma unroll
         for (int i = 0; i < NP; ++i) {
           const bool isv = i >= NP / 2;
-          const int key = key0 + srow[i];
+          const int key = key0 + srow(i);
           const int pr = SEG ? kv_row(p, key) : key;
-          const int c_off = (int)(soff[i] - (uint32_t)(srow[i] * (isv ? p.vr : p.kr) * 2));
+          const int c_off = scol(i);
           const char* src = key < p.seq_kv
                                 ? (isv ? vbase : kbase) + (int64_t)pr * (isv ? p.vr : p.kr) * 2 + c_off
                                 : zero;

@@ -40,11 +40,14 @@ extern "C" int mapa_device_check(int device) {
 
 // Debug / serialize mode (MAPA_SERIALIZE=1, or AMD_SERIALIZE_KERNEL / HIP_LAUNCH_BLOCKING set): the binding calls
 // this after every launch, so a faulting or failing kernel is reported by the launch that caused it instead of by
-// whatever synchronises next.
+// whatever synchronises next.  Launch errors are already reported (and cleared) by each entry point's own
+// hipGetLastError (MAPA_CHECK_LAUNCH), so this only synchronises and PEEKS: a sticky error left by an unrelated
+// earlier call is reported as such but not cleared, so the caller still sees the real error state.
 extern "C" int mapa_stream_check(hipStream_t stream, const char* what) {
-  hipError_t e = hipStreamSynchronize(stream);
-  if (e == hipSuccess) e = hipGetLastError();
-  if (e != hipSuccess) return mapa_set_error("%s: device error after launch: %s", what ? what : "launch",
-                                             hipGetErrorString(e));
+  const hipError_t s = hipStreamSynchronize(stream);
+  const hipError_t e = s != hipSuccess ? s : hipPeekAtLastError();
+  if (e != hipSuccess)
+    return mapa_set_error("%s: device error after launch: %s (hipError %d)", what ? what : "launch",
+                          hipGetErrorString(e), (int)e);
   return 0;
 }

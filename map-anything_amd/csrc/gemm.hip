@@ -101,7 +101,7 @@ __device__ __forceinline__ void mfma_kgroup(const char* As, const char* Bs, int 
 template <typename Tr, int AMODE, int RB>
 __device__ __forceinline__ void stage_tile(const GemmArgs& p, char* lds, int buf, int kt, int lds_base, bool k_exact,
                                            const char* const* a_src, const char* const* w_src, const int* sc,
-                                           const int* cv_base, const int* cv_iy, const int* cv_ix) {
+                                           const int* cv_pix, const int* cv_yx) {
   using T = typename Tr::T;
   constexpr int E = Tr::E;
   constexpr int BK = (RB / 16) * E;
@@ -123,10 +123,9 @@ __device__ __forceinline__ void stage_tile(const GemmArgs& p, char* lds, int buf
       int tap, ci;
       conv_kmap(p, kc, tap, ci);
       const int ky = tap / 3, kx = tap - ky * 3;
-      const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
-      const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+      const bool ok = kin && conv_tap_in(p, cv_yx[i], ky, kx);
       src = ok ? reinterpret_cast<const char*>(p.A) +
-                     ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_Cp + ci) * sizeof(T)
+                     ((int64_t)(cv_pix[i] + ky * p.cv_IW + kx) * p.cv_Cp + ci) * sizeof(T)
                : zero;
     }
     __builtin_amdgcn_global_load_lds(src, As + off, 16, 0, 0);
@@ -163,7 +162,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
   const char* a_src[NLD];
   const char* w_src[NLD];
   int sc[NLD];
-  int cv_base[NLD], cv_iy[NLD], cv_ix[NLD];
+  int cv_pix[NLD], cv_yx[NLD];
 #pragma unroll
   for (int i = 0; i < NLD; ++i) {
     const int r = (i * 4 + wave) * RPI + lrow;
@@ -176,9 +175,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
       const int hw = p.cv_OH * p.cv_OW;
       const int img = m / hw, rem = m - img * hw;
       const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
-      cv_base[i] = img * p.cv_IH * p.cv_IW;
-      cv_iy[i] = oy * p.cv_stride - 1;
-      cv_ix[i] = ox * p.cv_stride - 1;
+      conv_row_setup(p, img, oy, ox, cv_pix[i], cv_yx[i]);
     }
   }
   const int nk = (p.K + BK - 1) / BK;
@@ -193,11 +190,11 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   if constexpr (STAGES == 2) {
-    stage_tile<Tr, AMODE, RB>(p, lds, 0, 0, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+    stage_tile<Tr, AMODE, RB>(p, lds, 0, 0, lds_base, k_exact, a_src, w_src, sc, cv_pix, cv_yx);
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      if (kt + 1 < nk) stage_tile<Tr, AMODE, RB>(p, lds, cur ^ 1, kt + 1, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+      if (kt + 1 < nk) stage_tile<Tr, AMODE, RB>(p, lds, cur ^ 1, kt + 1, lds_base, k_exact, a_src, w_src, sc, cv_pix, cv_yx);
       const char* As = lds + cur * 2 * TILE_BYTES;
       const char* Bs = As + TILE_BYTES;
 #pragma unroll
@@ -208,7 +205,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
     // prologue: tiles 0 .. STAGES-2 in flight
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
-      if (s0 < nk) stage_tile<Tr, AMODE, RB>(p, lds, s0, s0, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+      if (s0 < nk) stage_tile<Tr, AMODE, RB>(p, lds, s0, s0, lds_base, k_exact, a_src, w_src, sc, cv_pix, cv_yx);
     for (int kt = 0; kt < nk; ++kt) {
       // tile kt landed (this thread's DMAs): later tiles may stay in flight
       if (kt + STAGES - 2 < nk) {
@@ -219,7 +216,7 @@ __global__ void __launch_bounds__(NTHREADS) gemm_kernel(GemmArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMA for tile kt landed; every wave done with tile kt-1
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + STAGES - 1 < nk) stage_tile<Tr, AMODE, RB>(p, lds, (kt + STAGES - 1) % STAGES, kt + STAGES - 1, lds_base, k_exact, a_src, w_src, sc, cv_base, cv_iy, cv_ix);
+      if (kt + STAGES - 1 < nk) stage_tile<Tr, AMODE, RB>(p, lds, (kt + STAGES - 1) % STAGES, kt + STAGES - 1, lds_base, k_exact, a_src, w_src, sc, cv_pix, cv_yx);
       const char* As = lds + (kt % STAGES) * 2 * TILE_BYTES;
       const char* Bs = As + TILE_BYTES;
 #pragma unroll
@@ -362,7 +359,9 @@ int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
   // 256x256 stream-K tiles from N = 512 up at a few thousand rows (the stride-2 768-channel DPT conv at 37 -> 19,
   // M = views * 361: 244 -> 152 us); the 224^2 geometric encoders (M = views * 256) keep 256x128
-  if (big_tiles < 256 && K >= 4096) return N >= 512 && M >= 2048 ? 2581 : 2580;
+  // (convs always take the 256x256 form: the 256x128 conv instantiation at 2 workgroups / CU does not fit its
+  // 128-VGPR budget without scratch)
+  if (big_tiles < 256 && K >= 4096) return conv || (N >= 512 && M >= 2048) ? 2581 : 2580;
   // tail-only stream-K where the 256x128 data-parallel schedule leaves a nearly empty last wave (enc.qkv / aat.fc1
   // at 8 views: 1032 tiles on 512 slots -> a third wave of 8 tiles)
   if (g_tail_sk && !conv) {

@@ -52,8 +52,8 @@ __device__ __forceinline__ int swz(int row) {
 // LDS-DMA of K tile kt into stage buf: NLA 1-KiB wave instructions of A rows, NLB of W rows per wave.
 template <int AMODE, int BN, int RB, int BM = BBM>
 __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf, int kt, int lds_wave, bool k_exact,
-                                          const char* const* a_src, const int* a_sc, const int* cv_base,
-                                          const int* cv_iy, const int* cv_ix, const char* const* w_src,
+                                          const char* const* a_src, const int* a_sc, const int* cv_pix,
+                                          const int* cv_yx, const char* const* w_src,
                                           const int* w_sc) {
   using C = Cfg<BN, RB, BM>;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
@@ -71,9 +71,8 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
       int tap, ci;
       conv_kmap(p, kc, tap, ci);
       const int ky = tap / 3, kx = tap - ky * 3;
-      const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
-      const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-      src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_Cp + ci) * 2
+      const bool ok = kin && conv_tap_in(p, cv_yx[i], ky, kx);
+      src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_pix[i] + ky * p.cv_IW + kx) * p.cv_Cp + ci) * 2
                : zero;
     }
     __builtin_amdgcn_global_load_lds(src, As + lds_wave + i * 8192, 16, 0, 0);
@@ -153,7 +152,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
   const char* a_src[C::NLA];
   int a_sc[C::NLA];
-  int cv_base[C::NLA], cv_iy[C::NLA], cv_ix[C::NLA];
+  int cv_pix[C::NLA], cv_yx[C::NLA];
   const char* w_src[C::NLB];
   int w_sc[C::NLB];
 #pragma unroll
@@ -167,9 +166,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
       const int hw = p.cv_OH * p.cv_OW;
       const int img = m / hw, rem = m - img * hw;
       const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
-      cv_base[i] = img * p.cv_IH * p.cv_IW;
-      cv_iy[i] = oy * p.cv_stride - 1;
-      cv_ix[i] = ox * p.cv_stride - 1;
+      conv_row_setup(p, img, oy, ox, cv_pix[i], cv_yx[i]);
     }
   }
 #pragma unroll
@@ -190,9 +187,37 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int g = lane >> 4, r16 = lane & 15;
+  // The implicit conv's staging state does not leave registers for every k-group's fragments of a 256x256 tile
+  // (128 accumulators): there the fragments of one 32-deep k-group are read at a time (no scratch; the code-object
+  // test checks every kernel).
+  constexpr bool KG_AHEAD = !(AMODE == 1 && C::FM * C::FN >= 32 && C::KG > 1);
   auto compute = [&](int slot) __attribute__((always_inline)) {
     const char* As = lds + slot * C::STAGE;
     const char* Bs = As + C::A_BYTES;
+    if constexpr (!KG_AHEAD) {
+#pragma unroll
+      for (int kg = 0; kg < C::KG; ++kg) {
+        const int chunk = kg * 4 + g;
+        bf16x8 a[C::FM], b[C::FN];
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const int rb = wn * C::TN + j * 16 + r16;
+          b[j] = *reinterpret_cast<const bf16x8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const int ra = wm * C::TM + i * 16 + r16;
+          a[i] = *reinterpret_cast<const bf16x8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
+        }
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma16x16x32<F16>(a[i], b[j], acc[i][j]);
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+      }
+      return;
+    }
     bf16x8 a[C::KG][C::FM], b[C::KG][C::FN];
 #pragma unroll
     for (int kg = 0; kg < C::KG; ++kg) {  // every k-group's fragment reads in flight before the first MFMA
@@ -221,12 +246,12 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   };
 
   if constexpr (STAGES == 2) {
-    stage_big<AMODE, BN, RB, BM>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
+    stage_big<AMODE, BN, RB, BM>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src, w_sc);
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // tile kt landed (vmcnt(0) before the barrier); every wave is done with tile kt-1
       if (kt + 1 < nk && DIAG != 1)
-        stage_big<AMODE, BN, RB, BM>(p, lds, (kt + 1) & 1, kt + 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
-                                 cv_ix, w_src, w_sc);
+        stage_big<AMODE, BN, RB, BM>(p, lds, (kt + 1) & 1, kt + 1, lds_wave, k_exact, a_src, a_sc, cv_pix,
+                                 cv_yx, w_src, w_sc);
       if (DIAG != 2) compute(kt & 1);
     }
   } else {
@@ -234,7 +259,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
       if (s0 < nk)
-        stage_big<AMODE, BN, RB, BM>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src, w_sc);
+        stage_big<AMODE, BN, RB, BM>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src, w_sc);
     int slot = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int ahead = min(STAGES - 2, nk - 1 - kt);  // tiles issued after kt that may still be in flight
@@ -247,8 +272,8 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
       __builtin_amdgcn_sched_barrier(0);
       if (kt + STAGES - 1 < nk) {
         const int ns = slot == 0 ? STAGES - 1 : slot - 1;  // (kt + STAGES - 1) % STAGES
-        stage_big<AMODE, BN, RB, BM>(p, lds, ns, kt + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
-                                 cv_ix, w_src, w_sc);
+        stage_big<AMODE, BN, RB, BM>(p, lds, ns, kt + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_pix,
+                                 cv_yx, w_src, w_sc);
       }
       compute(slot);
       slot = slot + 1 == STAGES ? 0 : slot + 1;
@@ -288,7 +313,7 @@ __global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
   const char* a_src[C::NLA];
   int a_sc[C::NLA];
-  int cv_base[C::NLA], cv_iy[C::NLA], cv_ix[C::NLA];
+  int cv_pix[C::NLA], cv_yx[C::NLA];
   const char* w_src[C::NLB];
   int w_sc[C::NLB];
 #pragma unroll
@@ -302,9 +327,7 @@ __global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
       const int hw = p.cv_OH * p.cv_OW;
       const int img = m / hw, rem = m - img * hw;
       const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
-      cv_base[i] = img * p.cv_IH * p.cv_IW;
-      cv_iy[i] = oy * p.cv_stride - 1;
-      cv_ix[i] = ox * p.cv_stride - 1;
+      conv_row_setup(p, img, oy, ox, cv_pix[i], cv_yx[i]);
     }
   }
 #pragma unroll
@@ -332,9 +355,8 @@ __global__ void __launch_bounds__(BTHREADS, 1) gemm_pp_kernel(GemmArgs p) {
         int tap, ci;
       conv_kmap(p, kc, tap, ci);
         const int ky = tap / 3, kx = tap - ky * 3;
-        const int iy = cv_iy[i] + ky, ix = cv_ix[i] + kx;
-        const bool ok = kin && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-        src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_base[i] + iy * p.cv_IW + ix) * p.cv_Cp + ci) * 2
+        const bool ok = kin && conv_tap_in(p, cv_yx[i], ky, kx);
+        src = ok ? reinterpret_cast<const char*>(p.A) + ((int64_t)(cv_pix[i] + ky * p.cv_IW + kx) * p.cv_Cp + ci) * 2
                  : zero;
       }
       __builtin_amdgcn_global_load_lds(src, As + lds_wave + i * 8192, 16, 0, 0);
@@ -528,7 +550,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
 
     const char* a_src[C::NLA];
     int a_sc[C::NLA];
-    int cv_base[C::NLA], cv_iy[C::NLA], cv_ix[C::NLA];
+    int cv_pix[C::NLA], cv_yx[C::NLA];
     const char* w_src[C::NLB];
     int w_sc[C::NLB];
 #pragma unroll
@@ -542,9 +564,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
         const int hw = p.cv_OH * p.cv_OW;
         const int img = m / hw, rem = m - img * hw;
         const int oy = rem / p.cv_OW, ox = rem - oy * p.cv_OW;
-        cv_base[i] = img * p.cv_IH * p.cv_IW;
-        cv_iy[i] = oy * p.cv_stride - 1;
-        cv_ix[i] = ox * p.cv_stride - 1;
+        conv_row_setup(p, img, oy, ox, cv_pix[i], cv_yx[i]);
       }
     }
 #pragma unroll
@@ -596,7 +616,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
       if (s0 < n)
-        stage_big<AMODE, BN, RB>(p, lds, s0, k0 + s0, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy, cv_ix, w_src,
+        stage_big<AMODE, BN, RB>(p, lds, s0, k0 + s0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src,
                                  w_sc);
     int slot = 0;
     for (int kk = 0; kk < n; ++kk) {
@@ -610,8 +630,8 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
       __builtin_amdgcn_sched_barrier(0);
       if (kk + STAGES - 1 < n) {
         const int ns = slot == 0 ? STAGES - 1 : slot - 1;
-        stage_big<AMODE, BN, RB>(p, lds, ns, k0 + kk + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_base, cv_iy,
-                                 cv_ix, w_src, w_sc);
+        stage_big<AMODE, BN, RB>(p, lds, ns, k0 + kk + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_pix,
+                                 cv_yx, w_src, w_sc);
       }
       compute(slot);
       slot = slot + 1 == STAGES ? 0 : slot + 1;
@@ -807,7 +827,7 @@ int64_t streamk_workspace_bytes(int M, int N, int variant) {
 }
 
 bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
-  if (variant < 0 || variant > 2 || !ws) return false;
+  if (variant < 0 || variant > 2 || !ws || (conv && variant != 1)) return false;  // convs: 256x256 only
   const int64_t need = streamk_workspace_bytes(a.M, a.N, variant);
   if (need == 0 || ws_bytes < need) return false;
   int bn, per_cu;
@@ -825,7 +845,7 @@ bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, in
   s.tickets = reinterpret_cast<int*>(ws);
   s.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + SK_TICKET_BYTES);
   void (*k)(GemmArgs, SkArgs);
-  if (variant != 1) k = conv ? gemm_sk_kernel<1, 128, 64, 3, 1, 4> : gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
+  if (variant != 1) k = gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
   else k = conv ? gemm_sk_kernel<1, 256, 64, 3, 1, 1> : gemm_sk_kernel<0, 256, 64, 3, 1, 1>;
   hipLaunchKernelGGL(k, dim3(G), dim3(BTHREADS), 0, stream, a, s);
   return true;

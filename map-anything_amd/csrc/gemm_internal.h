@@ -56,6 +56,18 @@ __device__ __forceinline__ void conv_kmap(const GemmArgs& p, int kc, int& tap, i
   ci = split_col(p, c);
 }
 
+// Implicit 3x3 conv (pad 1) staging state of one A row, two ints: the input pixel index of its (ky, kx) = (0, 0)
+// tap, and the tap window's top-left corner + 1 packed as y | x << 16 (both >= 0, images < 65535 pixels a side).
+__device__ __forceinline__ void conv_row_setup(const GemmArgs& p, int img, int oy, int ox, int& pix, int& yx) {
+  const int iy0 = oy * p.cv_stride - 1, ix0 = ox * p.cv_stride - 1;
+  pix = img * p.cv_IH * p.cv_IW + iy0 * p.cv_IW + ix0;
+  yx = (iy0 + 1) | ((ix0 + 1) << 16);
+}
+// tap (ky, kx) of that row inside the image (false = a padding tap, read from the zero page)
+__device__ __forceinline__ bool conv_tap_in(const GemmArgs& p, int yx, int ky, int kx) {
+  return (unsigned)((yx & 0xffff) + ky - 1) < (unsigned)p.cv_IH && (unsigned)((yx >> 16) + kx - 1) < (unsigned)p.cv_IW;
+}
+
 // Per-thread column state of the epilogue: 4 consecutive output columns n0..n0+3.
 struct EpiCol {
   int n0;

@@ -47,7 +47,20 @@ def main():
         torch.cuda.synchronize()
         return o
     names = ["pts3d", "pts3d_cam", "rays", "depth", "conf", "logits", "mask"]
+    po = pose_out.double().cpu()
+    sc = float(scale.double().cpu()[0])
+
+    def wrong(o):
+        """pixels whose pts3d is not R pts3d_cam + t*scale (fp64 on the host, same pose and pts3d_cam)"""
+        cam = o[1].double().cpu().reshape(n, -1, 3)
+        R, t = po[:, 7:16].reshape(n, 3, 3), po[:, 16:19]
+        exp = torch.einsum("nij,npj->npi", R, cam) + t[:, None, :] * sc
+        got = o[0].double().cpu().reshape(n, -1, 3)
+        bad = (got - exp).abs() > 1e-5 * (1 + exp.abs())
+        return bad, got, exp
     first = run()
+    b0, _, _ = wrong(first)
+    print(f"first run: {int(b0.any(-1).sum())} px off the host recomputation (x/y/z: {b0.sum((0, 1)).tolist()})")
     nbad = 0
     for r in range(reps):
         o = run()
@@ -57,6 +70,12 @@ def main():
                 d = (x.float() - y.float()).abs().reshape(n, H, W, -1).amax(-1)
                 idx = (d > 0).nonzero()
                 print(f"rep {r}: {nm} differs at {idx.shape[0]} px, e.g. {idx[:4].tolist()}", flush=True)
+                if nm == "pts3d":
+                    b, got, exp = wrong(o)
+                    k = b.any(-1).nonzero()
+                    print(f"   this run: {k.shape[0]} px off the host recomputation (x/y/z: {b.sum((0, 1)).tolist()})")
+                    for v_, p_ in k[:3].tolist():
+                        print(f"   view {v_} px {p_}: got {got[v_, p_].tolist()} expected {exp[v_, p_].tolist()}")
     print("ho_det:", "repeatable" if nbad == 0 else f"{nbad} mismatching outputs", flush=True)
 
 
