@@ -17,6 +17,7 @@ from conftest import REPO
 
 LIB = os.path.join(REPO, "map-anything_amd", "mapanything", "_lib", "libmapa.so")
 READELF = "/opt/rocm/llvm/bin/llvm-readelf"
+OBJDUMP = "/opt/rocm/llvm/bin/llvm-objdump"
 BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
 
 
@@ -40,18 +41,26 @@ def _code_objects(data):
 
 
 @pytest.fixture(scope="module")
-def kernels(tmp_path_factory):
+def code_object_files(tmp_path_factory):
     if not os.path.exists(LIB):
         pytest.skip("libmapa.so not built")
-    if not os.path.exists(READELF):
-        pytest.skip("llvm-readelf not available")
+    if not (os.path.exists(READELF) and os.path.exists(OBJDUMP)):
+        pytest.skip("llvm-readelf / llvm-objdump not available")
     objs = _code_objects(open(LIB, "rb").read())
     assert objs, "no gfx950 code object in libmapa.so"
     d = tmp_path_factory.mktemp("co")
-    res = {}
+    paths = []
     for n, co in enumerate(objs):
         p = d / f"co{n}.elf"
         p.write_bytes(co)
+        paths.append(p)
+    return paths
+
+
+@pytest.fixture(scope="module")
+def kernels(code_object_files):
+    res = {}
+    for p in code_object_files:
         notes = subprocess.run([READELF, "--notes", str(p)], check=True, capture_output=True, text=True).stdout
         # one metadata map per kernel: .name comes after the resource fields of the same map
         for blk in re.split(r"\n\s+- \.", notes):
@@ -74,3 +83,14 @@ def test_every_kernel_metadata_read(kernels):
 def test_no_scratch_in_any_kernel(kernels):
     bad = {k: v for k, v in kernels.items() if v != (0, 0)}
     assert not bad, "kernels with scratch (bytes, vgpr spills): " + "; ".join(f"{k}: {v}" for k, v in bad.items())
+
+
+def test_no_packed_fp32_instructions(code_object_files):
+    """Every object is built with the packed-fp32-ops target feature off (csrc/Makefile): a v_pk_mul_f32 whose two
+    halves read each other's source register gave wrong low halves in lanes 48-63 on MI355X (Determinism).
+    No v_pk_{add,mul,fma}_f32 may appear in any kernel."""
+    bad = []
+    for p in code_object_files:
+        dis = subprocess.run([OBJDUMP, "-d", str(p)], check=True, capture_output=True, text=True).stdout
+        bad += [ln.strip() for ln in dis.splitlines() if re.search(r"\bv_pk_(add|mul|fma)_f32\b", ln)]
+    assert not bad, f"{len(bad)} packed f32 instructions, e.g. {bad[:3]}"
