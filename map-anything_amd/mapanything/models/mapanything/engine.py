@@ -934,6 +934,15 @@ class MapaEngine:
                 if first is None:
                     first = self.head_rows(fused_f32[:VB * T])
                 l11, l17 = inter
+            return self.heads(first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=taps, dpt_chunk=dpt_chunk)
+
+    def heads(self, first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=None, dpt_chunk=None):
+        """downstream_head + output assembly (model.py:1774-1923): pose head on the final features, scale head on the
+        scale-token feature, DPT + regressor + dense head on [first, l11, l17, final].  first / l11 / l17 / fin_lp are
+        head operands (head_rows: split rows in the bf16 recipe, fp32 rows in fp32 mode; fin_lp may carry the scale
+        token as its last row); tok is the fp32 scale-token feature (1, dim)."""
+        T = hp * wp
+        with torch.cuda.device(self.device):
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)

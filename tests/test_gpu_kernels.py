@@ -88,10 +88,12 @@ def test_gemm_gelu_epilogue_fp32_exactness(nat, dtype):
 
 
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2587])
-@pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72)])
+@pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72),
+                                   (3000, 200, 256), (10960, 3072, 1024), (700, 4100, 128)])
 def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
     """Every 256-row schedule, incl. the stream-K ones (split tiles summed by the last arriver), on the path's
-    narrow-N shapes and on ragged tails; stream-K must be bit-reproducible and leave its workspace zeroed."""
+    narrow-N shapes, on more tiles than CUs and on ragged tails; stream-K must be bit-reproducible and leave its
+    workspace tickets zeroed."""
     A = _rand(M, K, seed=21).to(torch.bfloat16)
     W = _rand(N, K, scale=K ** -0.5, seed=22).to(torch.bfloat16)
     b, g, r = _rand(N, seed=23), _rand(N, seed=24), _rand(M, N, seed=25)

@@ -192,6 +192,46 @@ def test_fp32_taps_match_reference(model, golden):
     assert rel_l2(taps["scale_raw"].cpu().numpy().reshape(1, 1, 1), g["tap_scale_raw"]) < 1e-4
 
 
+def test_split_precision_heads_match_fp32_heads_at_cfg2_size(model):
+    """Stage-level pin of the production (bf16-recipe) heads at configs[1]'s size, 8 views at 518x518: the fp32 engine's
+    DPT / pose / scale inputs (fusion LayerNorm output, IFR taps L11 / L17, final features + scale token — each pinned
+    to the reference at 1e-4 by the tap tests) go through the bf16 engine's split-precision heads (halo-window and
+    flat split-K convs, stream-K convs, split GEMMs, split bilinear resizes incl. 296 -> 518, the fused regressor tail)
+    and through the fp32 engine's exact-fp32 heads; every head output agrees to <= 1e-4 rel-L2.  This is what catches
+    a tile-order or split-K indexing error that only the cfg2 shapes exercise (the kernel tests run 37^2 - 148^2)."""
+    case = CASES["cfg2_518"]
+    imgs = torch.cat([v["img"] for v in _views(case)], 0).cuda()
+    V, H, W = case["views"], case["h"], case["w"]
+    hp, wp = H // 14, W // 14
+    e32, e16 = model.engine("fp32"), model.engine("bf16")
+    assert not e32.hsplit and e16.hsplit
+    taps = {}
+    e32.run(imgs, taps=taps)
+    tok = taps["scale_token"].view(1, -1).contiguous()
+    fin = torch.cat([taps["aat_final"], tok], 0).contiguous()
+    res = {}
+    for name, eng in (("fp32", e32), ("split", e16)):
+        t2 = {}
+        out = eng.heads(eng.head_rows(taps["fused"].contiguous()), eng.head_rows(taps["aat_l11"].contiguous()),
+                        eng.head_rows(taps["aat_l17"].contiguous()), eng.head_rows(fin), tok, V, hp, wp, H, W,
+                        taps=t2)
+        torch.cuda.synchronize()
+        res[name] = dict(out, pose_raw=t2["pose_raw"], scale_raw=t2["scale_raw"], dpt_feature=t2["dpt_feature"])
+    print("\n[split heads vs fp32 heads, 8 x 518^2, identical fp32 inputs] rel-L2:")
+    bad = {}
+    for k in ("dpt_feature", "pts3d", "pts3d_cam", "ray_directions", "depth_along_ray", "conf",
+              "non_ambiguous_mask_logits", "pose_raw", "scale_raw", "cam_trans", "cam_quats", "metric_scaling_factor"):
+        e = rel_l2(res["split"][k].float().cpu().numpy(), res["fp32"][k].float().cpu().numpy())
+        print(f"  {k:28s} {e:.3e}")
+        if not e <= 1e-4:
+            bad[k] = e
+    assert not bad, bad
+    # the mask: identical wherever the logit is not within rounding of the threshold
+    lg = res["fp32"]["non_ambiguous_mask_logits"]
+    sure = lg.abs() > 1e-3
+    assert torch.equal(res["split"]["non_ambiguous_mask"][sure], res["fp32"]["non_ambiguous_mask"][sure])
+
+
 def test_fp32_geometric_fused_tap(model, golden):
     """Encoder + ray / depth / depth-scale / camera features + fusion LayerNorm against the reference tap."""
     from mapanything.utils.inference import (preprocess_input_views_for_inference,
