@@ -63,6 +63,8 @@ def main():
                     help="also time a fixed job of this many views over the N ranks (configs[2]); 0 = skip")
     ap.add_argument("--strong-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--batch-scenes", type=int, default=2,
+                    help="N=1: also time B scenes of views-per-gpu views per infer (batched scenes); 0 = skip")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--geometric", action="store_true",
                     help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
@@ -188,6 +190,23 @@ def main():
         del fm
         torch.cuda.empty_cache()
 
+    batched = None
+    if world == 1 and args.batch_scenes > 1 and not args.geometric and not args.total_views:
+        # B scenes x V views per infer (each view's img (B, 3, H, W)), run as one batched engine call
+        B = args.batch_scenes
+        b_imgs = synthetic.synthetic_images(V_total, H, W, seed=2, batch=B)
+        b_views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in b_imgs]
+        del b_imgs
+        for _ in range(max(1, args.warmup)):
+            model.infer(b_views, **amp)
+        bdt = timed_fn(lambda: model.infer(b_views, **amp), args.steps)
+        batched = {"scenes": B, "views_per_scene": V_total, "value": B * V_total * args.steps / bdt, "unit": "views/s",
+                   "ms_per_step": bdt / args.steps * 1e3, "steps": args.steps,
+                   "workload": f"{B} scenes x {V_total} views {H}x{W} per infer (batched: one engine call)",
+                   "vs_single_scene": (B * V_total * args.steps / bdt) / value}
+        del b_views
+        torch.cuda.empty_cache()
+
     strong = None
     if args.strong_views and not args.total_views and not args.geometric and args.strong_views >= world:
         # configs[2]: a fixed job of strong_views views split over the N ranks (strong scaling)
@@ -280,6 +299,7 @@ def main():
             "roofline": roofline,
             "cross_view_attention": xattn,
             "cpu_baseline": cpu,
+            "batched_scenes": batched,
             "fast_mode_bf16_heads": fast,
             "strong_scaling": strong,
             "hip_graphs": bool(model.hip_graphs and world == 1 and not args.geometric),

@@ -115,9 +115,11 @@ int mapa_gemm_set_variant(int variant);
  * 1865-2150): d describes the 3x3 conv 128 -> 128 (bf16, stride 1, conv_kblock 32, act MAPA_ACT_RELU, bias; no
  * outputs of its own); its ReLU'd hidden map never leaves the chip — the epilogue applies the 1x1 conv w6 [6][128] +
  * b6, the ray / depth / confidence / mask adaptors and the output assembly of mapa_dense_head_out (pose_out: the
- * launch's views' rows, scale: the metric scale; outputs as there).  Replaces mapa_gemm + mapa_dense_head_out. */
+ * launch's views' rows, scale: the metric scales, image i of the launch using scale[i / views_per_scale] —
+ * views_per_scale = the launch's image count for one scene, 1 with one scale per image for batched scenes; outputs as
+ * there).  Replaces mapa_gemm + mapa_dense_head_out. */
 int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const float* b6, const float* pose_out,
-                            const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                            const float* scale, int views_per_scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
                             float* conf, float* logits, uint8_t* mask, mapa_stream_t stream);
 
 /* Tuning / A-B hooks of the automatic kernel choice (process-wide):

@@ -58,7 +58,8 @@ struct HeadOut {
   const float* w6;    // [6][128]
   const float* b6;    // [6]
   const float* pose;  // [views][19] pose_out rows of this launch's views
-  const float* scale; // [1] metric scale
+  const float* scale; // metric scale: scale[img / vps] for the launch's image img
+  int vps;            // consecutive images sharing one scale value (>= the launch's images: one scene)
   float *pts3d, *pts3d_cam, *rays, *depth, *conf, *logits;
   uint8_t* mask;
 };
@@ -398,7 +399,7 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
 #pragma unroll
         for (int o = 0; o < 6; ++o) raw[o] = ho.b6[o] + part[(tid * 2) * 6 + o] + part[(tid * 2 + 1) * 6 + o];
         const int64_t q = ((int64_t)img * p.cv_OH + oy) * p.cv_OW + ox;
-        dense_head_pixel(raw, ho.pose + img * 19, ho.scale[0], q, ho.pts3d, ho.pts3d_cam, ho.rays, ho.depth, ho.conf,
+        dense_head_pixel(raw, ho.pose + img * 19, ho.scale[img / ho.vps], q, ho.pts3d, ho.pts3d_cam, ho.rays, ho.depth, ho.conf,
                          ho.logits, ho.mask);
       }
     }
@@ -517,7 +518,7 @@ bool launch_conv_halo_flat(const GemmArgs& a, int nsplit, void* ws, int64_t ws_b
 }
 
 bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b6, const float* pose,
-                              const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                              const float* scale, int vps, float* pts3d, float* pts3d_cam, float* rays, float* depth,
                               float* conf, float* logits, uint8_t* mask, hipStream_t stream) {
   if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
   if (a.N != 128 || !a.bias || a.act != MAPA_ACT_RELU || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
@@ -525,7 +526,8 @@ bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b
   const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + 15) / 16) * ((a.cv_OW + BW - 1) / BW);
   if (tiles >= (int64_t(1) << 31)) return false;
   HeadOut h;
-  h.w6 = w6; h.b6 = b6; h.pose = pose; h.scale = scale;
+  if (vps <= 0) return false;
+  h.w6 = w6; h.b6 = b6; h.pose = pose; h.scale = scale; h.vps = vps;
   h.pts3d = pts3d; h.pts3d_cam = pts3d_cam; h.rays = rays; h.depth = depth; h.conf = conf; h.logits = logits;
   h.mask = mask;
   hipLaunchKernelGGL((conv_halo_kernel<128, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h,

@@ -485,17 +485,19 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
 }
 
 extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const float* b6,
-                                       const float* pose_out, const float* scale, float* pts3d, float* pts3d_cam,
+                                       const float* pose_out, const float* scale, int views_per_scale,
+                                       float* pts3d, float* pts3d_cam,
                                        float* rays, float* depth, float* conf, float* logits, uint8_t* mask,
                                        hipStream_t stream) {
   GemmArgs a;
   if (int rc = gemm_args(d, a)) return rc;
   MAPA_CHECK_ARG(w6 && b6 && pose_out && scale && pts3d && pts3d_cam && rays && depth && conf && logits && mask,
                  "mapa_regressor_head_out: null output or parameter");
+  MAPA_CHECK_ARG(views_per_scale > 0, "mapa_regressor_head_out: views_per_scale %d must be > 0", views_per_scale);
   MAPA_CHECK_ARG(d->dtype == MAPA_BF16 && d->a_mode == MAPA_A_CONV3X3 && !d->out_f32 && !d->out_lp &&
                      !d->out_lp_relu && !d->out_s3 && !d->out_s3_relu && !d->resid1 && !d->resid2 && !d->gamma,
                  "mapa_regressor_head_out: needs a bf16 3x3 conv descriptor without other outputs");
-  MAPA_CHECK_ARG(launch_conv_halo_headout(a, w6, b6, pose_out, scale, pts3d, pts3d_cam, rays, depth, conf, logits,
+  MAPA_CHECK_ARG(launch_conv_halo_headout(a, w6, b6, pose_out, scale, views_per_scale, pts3d, pts3d_cam, rays, depth, conf, logits,
                                           mask, stream),
                  "mapa_regressor_head_out: conv must be stride 1, conv_kblock 32, N 128, ReLU with bias");
   MAPA_CHECK_LAUNCH("mapa_regressor_head_out");

@@ -357,7 +357,7 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh = 16
 // The halo conv with the regressor tail fused into its epilogue (conv_halo.hip): conv3x3 128->128 + ReLU, 1x1 128->6,
 // adaptors and output assembly.  false unless the conv qualifies (bf16, stride 1, conv_kblock 32, N 128, ReLU, bias).
 bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b6, const float* pose,
-                              const float* scale, float* pts3d, float* pts3d_cam, float* rays, float* depth,
+                              const float* scale, int vps, float* pts3d, float* pts3d_cam, float* rays, float* depth,
                               float* conf, float* logits, uint8_t* mask, hipStream_t stream);
 // The halo conv on flat-raster blocks with the 32-channel slices split over nsplit workgroups per tile (maps up to
 // 62 pixels wide; conv_halo.hip).  conv_halo_flat_split: the part count for `slots` resident workgroups (force > 0:

@@ -102,7 +102,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_linear_small.argtypes = [vp, i, i, vp, vp, i, i, vp, vp]
     L.mapa_pose_scale_finalize.argtypes = [vp, vp, i, i, vp, vp, vp, vp]
     L.mapa_dense_head_out.argtypes = [vp, i, i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp]
-    L.mapa_regressor_head_out.argtypes = [vp] + [vp] * 11 + [vp]
+    L.mapa_regressor_head_out.argtypes = [vp] * 5 + [i] + [vp] * 7 + [vp]
     L.mapa_convert_rows.argtypes = [vp, i64, i, i, vp, i, i64, vp]
     L.mapa_fill_splitmix.argtypes = [vp, i64, u64, f, f, vp]
     L.mapa_postprocess_mask.argtypes = [vp, vp, vp, vp, i, i, i, f, f, i, vp, vp]
@@ -297,8 +297,9 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     operands (W._mapa_split, engine._split_pack) marks A as a compact split operand (mapa_gemm_desc.a_split): K is
     then the logical 3C, the stored A row 2C wide.  A conv weight tagged W._mapa_kblock = B holds its columns in the
     channel-block-major K order (mapa_gemm_desc.conv_kblock).
-    head_out=(w6, b6, pose_out, scale, pts3d, pts3d_cam, rays, depth, conf, logits, mask): the conv is the regressor's
-    conv2 and its hidden map goes straight into the dense head (mapa_regressor_head_out; no other outputs)."""
+    head_out=(w6, b6, pose_out, scale, views_per_scale, pts3d, pts3d_cam, rays, depth, conf, logits, mask): the conv
+    is the regressor's conv2 and its hidden map goes straight into the dense head (mapa_regressor_head_out; no other
+    outputs; image i uses scale[i // views_per_scale])."""
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype
@@ -341,7 +342,9 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     tok = _tic()
     if head_out is not None:
-        check(lib().mapa_regressor_head_out(ctypes.byref(d), *(ptr(t) for t in head_out), stream()),
+        w6, b6, po, sc, vps, *outs = head_out
+        check(lib().mapa_regressor_head_out(ctypes.byref(d), ptr(w6), ptr(b6), ptr(po), ptr(sc), int(vps),
+                                            *(ptr(t) for t in outs), stream()),
               "mapa_regressor_head_out")
     else:
         check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")

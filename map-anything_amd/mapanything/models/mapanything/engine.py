@@ -33,6 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import _native as nat
+from ...parallel import force_collectives
 from .spec import RELEASED_INFO, InfoSharingSpec
 
 ENC_DIM, ENC_HEADS, PATCH, KPAD = 1024, 16, 14, 640
@@ -403,11 +404,12 @@ class MapaEngine:
                  resid1=x, out_f32=x)
 
     # ------------------------------------------------------------------------------------------- encoder
-    def encode(self, imgs, taps=None, geo: Optional[GeoInputs] = None):
+    def encode(self, imgs, taps=None, geo: Optional[GeoInputs] = None, scenes: int = 1):
         """DINOv2 ViT-L/14 + final norm [+ geometric-input features] + fusion LayerNorm.  Returns fused_lp
-        [VB*T+1][1024] (last row = the scale token), the same rows in f32 if taps is not None or the transformer
-        has no input projection (else None), and the token grid."""
+        [VB*T+B][1024] (the last B rows = the B scenes' scale tokens), the same rows in f32 if taps is not None or the
+        transformer has no input projection (else None), and the token grid."""
         w = self.w
+        B = scenes
         VB, _, H, W = imgs.shape
         hp, wp = H // PATCH, W // PATCH
         T = hp * wp
@@ -416,14 +418,15 @@ class MapaEngine:
             taps["encoder"] = enc.clone()
         if geo is not None and not geo.empty():
             self.geometric(enc, geo, VB, H, W)
-        fused_lp = self._empty(VB * T + 1, ENC_DIM)
+        fused_lp = self._empty(VB * T + B, ENC_DIM)
         identity = w.pe_proj is None  # the transformer reads the fp32 fused rows directly
         need_f32 = taps is not None or identity or self.hsplit  # split heads read the fp32 fused rows (DPT input 0)
-        fused_f32 = self._empty(VB * T + 1, ENC_DIM, dtype=torch.float32) if need_f32 else None
+        fused_f32 = self._empty(VB * T + B, ENC_DIM, dtype=torch.float32) if need_f32 else None
         self._ln(enc, VB * T, ENC_DIM, w.fus_w, w.fus_b, y_lp=fused_lp, y_f32=fused_f32)
-        nat.convert_rows(w.scale_token.view(1, -1), ENC_DIM, 1, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
+        # the scale token of every scene (source row stride 0: one row replicated)
+        nat.convert_rows(w.scale_token.view(1, -1), 0, B, ENC_DIM, fused_lp[VB * T:], ENC_DIM)
         if fused_f32 is not None:
-            fused_f32[VB * T].copy_(w.scale_token)
+            fused_f32[VB * T:].copy_(w.scale_token.view(1, -1).expand(B, -1))
         if taps is not None:
             taps["fused"] = fused_f32[:VB * T]
         return fused_lp, fused_f32, (hp, wp)
@@ -582,17 +585,23 @@ class MapaEngine:
         return y
 
     # ----------------------------------------------------------------------------------------------- AAT
-    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None, pe_idx=None, fused_f32=None):
+    def aat(self, fused_lp, VB, T, taps=None, shard=None, comm=None, pe_idx=None, fused_f32=None, scenes: int = 1):
         """The multi-view transformer with intermediate-feature return: AAT (alternating_attention_transformer.py:
         530-771; released config: 24 blocks, taps after 11 and 17) or GAT (global_attention_transformer.py:458-640:
         every block global), per self.info.  Returns the list of normed taps (2 or 3, VB*T rows) and the final
         features as head operands (_hop: split rows or lp), and the final scale-token feature (f32, dim).  fused_f32: the fp32 fused rows (with the scale token), needed
         when proj_embed is the identity.  pe_idx: (V_total,) int64 device tensor of view-PE table rows (row 0 for the
         reference view) when the variant encodes non-reference views too.  With `shard` (parallel.ShardPlan) this
-        rank holds only its views (+ the scale-token replica) and the global layers all-gather K/V through `comm`."""
+        rank holds only its views (+ the scale-token replica) and the global layers all-gather K/V through `comm`.
+        scenes = B > 1 (no shard): VB = B x V images scene-major, rows [image][token] then the B scale tokens; frame
+        layers run over all images at once, global layers attend within each scene (its tokens + its scale token)."""
         w, info = self.w, self.info
         D, NH = info.dim, info.heads
-        L = VB * T + 1
+        B = scenes
+        if B > 1 and (shard is not None or taps is not None or VB % B):
+            raise ValueError("batched scenes: no view sharding or taps, and VB a multiple of the scene count")
+        V = VB // B
+        L = VB * T + B
         if w.pe_proj is None:  # identity projection: the residual stream starts from the fp32 fused features
             if fused_f32 is None:
                 raise ValueError("this info-sharing variant has no input projection: pass fused_f32")
@@ -601,14 +610,17 @@ class MapaEngine:
             y = self._empty(L, D, dtype=torch.float32)
             nat.gemm(fused_lp, w.pe_proj, L, D, ENC_DIM, bias=w.pe_proj_b, out_f32=y)
         first = 0 if shard is None else shard.starts[shard.rank]  # global index of this rank's first view
-        if info.nonref_pe:  # view PE on every view: table rows pe_idx (row 0 on the reference view)
-            vecs = w.view_pos.index_select(0, pe_idx[first:first + VB]).contiguous()
+        if info.nonref_pe:  # view PE on every view: table rows pe_idx (row 0 on the reference view); one draw for
+            # all scenes, as the reference's forward draws once and repeats it over the batch
+            vecs = w.view_pos.index_select(0, pe_idx[first:first + V]).repeat(B, 1).contiguous()
             nat.add_view_vectors(y, T, D, VB, vecs, self._ones(VB), 1)
-        elif info.ref_pe and first == 0:  # reference-view PE on view 0 only
-            nat.add_rowvec(y, D, 0, T, D, w.view_pe)
+        elif info.ref_pe and first == 0:  # reference-view PE on view 0 (of every scene) only
+            for b in range(B):
+                nat.add_rowvec(y, D, b * V * T, b * V * T + T, D, w.view_pe)
         yn, qkv, ao = self._empty(L, D), self._empty(L, 3 * D), self._empty(L, D)
         hbuf = self._empty(L, 4 * D)
-        L_all = L if shard is None else shard.total_kv  # tokens of a global block (every view + the scale token)
+        # tokens one global block attends to (a scene's views + its scale token)
+        L_all = V * T + 1 if shard is None else shard.total_kv
         g_scale = 0.125 * info.q_scale(L_all) if (info.scalable_softmax or info.entropy_scaling) else None
         f_scale = 0.125 * info.q_scale(T) if (info.scalable_softmax or info.entropy_scaling) else None
         if shard is not None:
@@ -617,9 +629,11 @@ class MapaEngine:
         inter = {}
         for d, p in enumerate(w.aat):
             if info.is_global(d):   # global attention over every view + the scale token
-                if shard is None:
+                if shard is None and B == 1:
                     self._block(y, yn, qkv, ao, hbuf, L, D, NH, p, attn_batch=1, attn_seq=L, gamma=False,
                                 attn_kind="attention_global", attn_scale=g_scale)
+                elif shard is None:
+                    self._block_global_scenes(y, yn, qkv, ao, hbuf, L, p, B, V, T, g_scale)
                 else:
                     self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, g_scale)
             else:                   # frame attention inside each view; the scale token bypasses the block
@@ -639,7 +653,7 @@ class MapaEngine:
         fin_lp = self._hop(L, D)  # the final features feed the DPT and the pose head only
         fin_f32 = self._empty(L, D, dtype=torch.float32)
         self._ln_head(y, L, D, w.aat_nw, w.aat_nb, fin_lp, y_f32=fin_f32)
-        if shard is not None and shard.world > 1:
+        if shard is not None and (shard.world > 1 or force_collectives()):
             # the scale-token replicas round differently per rank (query blocking, merge order): rank 0's final
             # scale-token feature is the one every rank's scale head reads (one D-float broadcast)
             comm.broadcast_(fin_f32[VB * T:], 0)
@@ -656,6 +670,27 @@ class MapaEngine:
             self._ones_buf = o
         return o
 
+    def _block_global_scenes(self, y, yn, qkv, ao, hbuf, L, p, B, V, T, scale=None):
+        """Global SelfAttentionBlock of B batched scenes (rows [image][token] scene-major, then the B scale tokens):
+        LayerNorm / GEMMs over all rows at once; per scene one attention of its token rows and one of its scale-token
+        row, both over the scene's keys through the segment table (its V*T token rows + its scale-token row)."""
+        C, NH = self.info.dim, self.info.heads
+        rs = 3 * C
+        self._ln(y, L, C, p["n1w"], p["n1b"], y_lp=yn)
+        nat.gemm(yn, p["qkv"], L, rs, C, bias=p["qkv_b"], out_lp=qkv)
+        k, v = qkv[:, C:], qkv[:, 2 * C:]
+        kw = dict(batch=1, heads=NH, q_bstride=0, q_rstride=rs, k_bstride=0, k_rstride=rs, v_bstride=0, v_rstride=rs,
+                  o_bstride=0, o_rstride=C, scale=scale, kind="attention_global")
+        for b in range(B):
+            r0, tok = b * V * T, V * T * B + b
+            segs = [(r0, V * T), (tok, 1)]
+            nat.attention(qkv[r0:], k, v, ao[r0:], seq_q=V * T, seq_kv=V * T + 1, kv_segments=segs, **kw)
+            nat.attention(qkv[tok:], k, v, ao[tok:], seq_q=1, seq_kv=V * T + 1, kv_segments=segs, **kw)
+        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
+        self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)
+        nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
+        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y)
+
     def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, scale=None):
         """Global SelfAttentionBlock on a view shard: Q for the local rows, K/V of all ranks (one all-gather).
         The all-gather runs on the communicator's stream while the local queries attend to this rank's own keys;
@@ -669,10 +704,10 @@ class MapaEngine:
         strides = dict(batch=1, heads=NH, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
                        v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C, scale=scale)
         overlap = hasattr(comm, "allgather_slots_async") and os.environ.get("MAPA_KV_OVERLAP", "1") != "0"
-        if shard.world == 1:  # a one-rank group: every key is local, nothing to exchange
+        if shard.world == 1 and not force_collectives():  # a one-rank group: every key is local
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
                           kv_segments=shard.kv_segments(), kind="attention_global", **strides)
-        elif not overlap:
+        elif not overlap or shard.world == 1:  # gather first (forced collectives on one rank: nothing remote)
             comm.allgather_slots(kv_full, shard.max_rows)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
                           kv_segments=shard.kv_segments(), kind="attention_global", **strides)
@@ -880,15 +915,16 @@ class MapaEngine:
         return raw
 
     def scale(self, tok, taps=None):
-        """MLPHead (mlp_head.py:13-92) on the scale-token feature -> raw (1,)."""
+        """MLPHead (mlp_head.py:13-92) on the scale-token feature(s) (B, dim) -> raw (B,)."""
         w = self.w.scale_mlp
-        a = self._empty(1, 196, dtype=torch.float32)
-        b = self._empty(1, 196, dtype=torch.float32)
-        nat.linear_small(tok, 1, self.info.dim, w[0][0], w[0][1], 196, nat.ACT_NONE, a)
-        nat.linear_small(a, 1, 196, w[1][0], w[1][1], 196, nat.ACT_RELU, b)
-        nat.linear_small(b, 1, 196, w[2][0], w[2][1], 196, nat.ACT_RELU, a)
-        raw = self._empty(1, dtype=torch.float32)
-        nat.linear_small(a, 1, 196, w[3][0], w[3][1], 1, nat.ACT_NONE, raw)
+        m = tok.shape[0] if tok.dim() == 2 else 1
+        a = self._empty(m, 196, dtype=torch.float32)
+        b = self._empty(m, 196, dtype=torch.float32)
+        nat.linear_small(tok, m, self.info.dim, w[0][0], w[0][1], 196, nat.ACT_NONE, a)
+        nat.linear_small(a, m, 196, w[1][0], w[1][1], 196, nat.ACT_RELU, b)
+        nat.linear_small(b, m, 196, w[2][0], w[2][1], 196, nat.ACT_RELU, a)
+        raw = self._empty(m, dtype=torch.float32)
+        nat.linear_small(a, m, 196, w[3][0], w[3][1], 1, nat.ACT_NONE, raw)
         if taps is not None:
             taps["scale_raw"] = raw
         return raw
@@ -897,20 +933,25 @@ class MapaEngine:
     @torch.no_grad()
     def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None,
             geo: Optional[GeoInputs] = None, dpt_chunk: Optional[int] = None,
-            pe_idx: Optional[torch.Tensor] = None) -> Dict[str, torch.Tensor]:
+            pe_idx: Optional[torch.Tensor] = None, scenes: int = 1) -> Dict[str, torch.Tensor]:
         """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
         per-pixel / per-view outputs of MapAnything.forward, view-major.  With `shard`/`comm`, imgs are this
         rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'.  `geo` carries the
         optional geometric inputs of these views (GeoInputs).  dpt_chunk: run the dense head over at most that many
-        views at a time (memory_efficient_inference, model.py:1479-1516); None = all views at once."""
+        views at a time (memory_efficient_inference, model.py:1479-1516); None = all views at once.
+        scenes = B > 1: imgs are B scenes of V views, scene-major ((B*V, 3, H, W), image b*V + v), run as one batch
+        (the reference's batched forward, model.py:687-721): outputs scene-major, metric_scaling_factor (B, 1)."""
         if imgs.dim() != 4 or imgs.shape[1] != 3:
             raise AssertionError("images must be (V, 3, H, W)")
         VB, _, H, W = imgs.shape
         if H % PATCH or W % PATCH:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
+        B = scenes
+        if B > 1 and (shard is not None or geo is not None or taps is not None or VB % B):
+            raise ValueError("batched scenes run image-only, unsharded, without taps, with VB a multiple of B")
         with torch.cuda.device(self.device):
-            fused_lp, fused_f32, (hp, wp) = self.encode(imgs, taps, geo)
+            fused_lp, fused_f32, (hp, wp) = self.encode(imgs, taps, geo, scenes=B)
             T = hp * wp
             if shard is not None and (shard.counts[shard.rank] != VB or shard.tokens_per_view != T):
                 raise AssertionError("shard plan does not match the local views")
@@ -927,28 +968,37 @@ class MapaEngine:
                 elif self.w.pe_proj is None:
                     first = self.head_rows(fused_f32[:VB * T])
             inter, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx,
-                                          fused_f32=fused_f32)
+                                          fused_f32=fused_f32, scenes=B)
             if len(inter) == 3:
                 first, l11, l17 = inter
             else:
                 if first is None:
                     first = self.head_rows(fused_f32[:VB * T])
                 l11, l17 = inter
-            return self.heads(first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=taps, dpt_chunk=dpt_chunk)
+            return self.run_heads(first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=taps, dpt_chunk=dpt_chunk,
+                              scenes=B)
 
-    def heads(self, first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=None, dpt_chunk=None):
+    def run_heads(self, first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=None, dpt_chunk=None, scenes: int = 1):
         """downstream_head + output assembly (model.py:1774-1923): pose head on the final features, scale head on the
         scale-token feature, DPT + regressor + dense head on [first, l11, l17, final].  first / l11 / l17 / fin_lp are
         head operands (head_rows: split rows in the bf16 recipe, fp32 rows in fp32 mode; fin_lp may carry the scale
-        token as its last row); tok is the fp32 scale-token feature (1, dim)."""
+        tokens as its last rows); tok is the fp32 scale-token feature (B, dim) of the B = scenes scenes, whose VB = B x V
+        images are scene-major."""
         T = hp * wp
+        B = scenes
+        V = VB // B
         with torch.cuda.device(self.device):
             pose_raw = self.pose(fin_lp, VB, T, taps)
             scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)
-            scale = self._empty(1, dtype=torch.float32)
+            scale = self._empty(B, dtype=torch.float32)
             poses44 = self._empty(VB, 4, 4, dtype=torch.float32)
-            nat.pose_scale_finalize(pose_raw, scale_raw, VB, 1, pose_out, scale, poses44)
+            for b in range(B):  # each scene's views take its own metric scale
+                sl = slice(b * V, (b + 1) * V)
+                nat.pose_scale_finalize(pose_raw[sl], scale_raw[b:b + 1], V, 1, pose_out[sl], scale[b:b + 1],
+                                        poses44[sl])
+            # one scale per image for the dense head when scenes are batched (image i: scale[i // V])
+            scale_img = scale if B == 1 else scale.repeat_interleave(V)
             f = torch.float32
             out = dict(
                 pts3d=self._empty(VB, H, W, 3, dtype=f), pts3d_cam=self._empty(VB, H, W, 3, dtype=f),
@@ -960,16 +1010,18 @@ class MapaEngine:
             for v0 in range(0, VB, chunk):
                 n = min(chunk, VB - v0)
                 r0, r1 = v0 * T, (v0 + n) * T
-                head = (pose_out[v0:v0 + n], scale) + tuple(
-                    out[k][v0:v0 + n] for k in ("pts3d", "pts3d_cam", "ray_directions", "depth_along_ray", "conf",
-                                                "non_ambiguous_mask_logits", "non_ambiguous_mask"))
+                # (pose rows, scales, images per scale value) of these images
+                sc = (scale, n) if B == 1 else (scale_img[v0:v0 + n], 1)
+                outs = tuple(out[k][v0:v0 + n] for k in ("pts3d", "pts3d_cam", "ray_directions", "depth_along_ray",
+                                                         "conf", "non_ambiguous_mask_logits", "non_ambiguous_mask"))
                 hid = self.dpt(first[r0:r1], l11[r0:r1], l17[r0:r1], fin_lp[r0:r1], n, hp, wp, H, W,
-                               taps if n == VB else None, head=head if fuse else None)
-                if not fuse:
-                    nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, *head[:2], 1, *head[2:])
+                               taps if n == VB else None, head=(pose_out[v0:v0 + n],) + sc + outs if fuse else None)
+                if not fuse:  # the unfused head's batch = scales: scale[i % batch] (one scale, or one per image)
+                    nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, pose_out[v0:v0 + n], sc[0],
+                                       1 if B == 1 else n, *outs)
                 del hid
             out["cam_trans"] = pose_out[:, 0:3]
             out["cam_quats"] = pose_out[:, 3:7]
-            out["metric_scaling_factor"] = scale.view(1, 1)
+            out["metric_scaling_factor"] = scale.view(B, 1)
             out["camera_poses"] = poses44
         return out

@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ... import _native as nat
+from ...parallel import force_collectives
 from ...utils.inference import (postprocess_outputs, preprocess_input_views_for_inference,
                                 validate_input_views_for_inference)
 from .spec import InfoSharingSpec, aliases, canonical_spec, full_spec
@@ -112,6 +113,8 @@ class MapAnything:
         # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
         self.hip_graphs = hip_graphs and os.environ.get("MAPA_HIP_GRAPHS", "1") != "0"
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
+        # sharded capture: off with MAPA_SHARD_GRAPHS=0, or on every rank once any rank's capture has failed
+        self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "1") != "0"
         self._modules: Dict[str, Any] = {}
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)
@@ -396,17 +399,35 @@ class MapAnything:
         Views are in the preprocessed form (ray_directions_cam, depth_along_ray, camera_pose_quats/trans,
         is_metric_scale); every provided geometric input is used (infer()'s deterministic masks)."""
         B = self._check_views(views)
-        if B > 1:
+        if B > 1 and not self._batchable(views):
             return self._merge_scenes([self.forward(self._scene_views(views, b, B), memory_efficient_inference,
                                                     precision) for b in range(B)])
         dnt = views[0].get("data_norm_type", ["dinov2"])
         if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
         local, plan = self._local_views(views)
-        geo = self._geo_inputs(views, plan, self._metric_flags(views))
-        imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
-        raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference))
-        return self._finish(raw, plan, len(views), with_post=False)
+        geo = self._geo_inputs(views, plan, self._metric_flags(views)) if B == 1 else None
+        imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
+        raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference),
+                               scenes=B)
+        return self._finish(raw, plan, len(views), with_post=False, scenes=B)
+
+    # entries a view may carry and still run in a batched-scene engine call (image-only, no geometric inputs)
+    _IMAGE_ONLY_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label"))
+
+    def _batchable(self, views) -> bool:
+        """B > 1 scenes run as ONE engine call (encoder / frame layers / heads over all B x V images, the global
+        layers per scene; the reference's batched forward, model.py:687-721) when the views carry images only and
+        the model is not view-sharded; otherwise scene by scene."""
+        return self._comm is None and all(set(v.keys()) <= self._IMAGE_ONLY_KEYS for v in views)
+
+    @staticmethod
+    def _scene_major(imgs, B: int):
+        """View-major (V*B, ...) images (the per-view (B, ...) tensors concatenated) -> scene-major (B*V, ...)."""
+        if B == 1:
+            return imgs
+        V = imgs.shape[0] // B
+        return imgs.view(V, B, *imgs.shape[1:]).transpose(0, 1).reshape(imgs.shape).contiguous()
 
     _MAX_GRAPHS = 4
 
@@ -425,17 +446,24 @@ class MapAnything:
             rest = torch.arange(1, num_views)
         return torch.cat([torch.zeros(1, dtype=torch.int64), rest.to(torch.int64)]).to(self._device)
 
-    def _run_engine(self, eng, imgs, plan, geo, dpt_chunk):
-        """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: one device, no
-        geometric inputs, no chunked dense head, no per-launch kernel timing, not in the serialize debug mode (every
-        launch checked, nat.SERIALIZE).  The graph is keyed on the image
-        batch shape and precision; inputs are copied into its static buffer and outputs cloned out of it, so
+    def _run_engine(self, eng, imgs, plan, geo, dpt_chunk, scenes: int = 1):
+        """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: no geometric inputs, no
+        chunked dense head, no per-launch kernel timing, not in the serialize debug mode (every launch checked,
+        nat.SERIALIZE), and either one device or a view shard whose communicator enqueues its collectives on the
+        device (DistComm over RCCL: the K/V all-gathers and the scale-token broadcast are captured with the
+        kernels, forking to and joining from the communicator's stream).  The graph is keyed on the image batch
+        shape, precision and shard plan; inputs are copied into its static buffer and outputs cloned out of it, so
         results never alias a later call's."""
-        pe_idx = self._view_pe_rows(plan.num_views if plan is not None else imgs.shape[0])
-        if (not self.hip_graphs or plan is not None or geo is not None or dpt_chunk is not None
+        pe_idx = self._view_pe_rows(plan.num_views if plan is not None else imgs.shape[0] // scenes)
+        shard_ok = plan is None or (self._shard_graphs and getattr(self._comm, "graph_safe", False))
+        if (not self.hip_graphs or not shard_ok or geo is not None or dpt_chunk is not None
                 or nat._timing is not None or nat.SERIALIZE or imgs.device.type != "cuda"):
-            return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx)
-        key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index)
+            return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx,
+                           scenes=scenes)
+        pkey = None if plan is None else (plan.world, plan.rank, tuple(plan.counts), force_collectives(),
+                                          os.environ.get("MAPA_KV_OVERLAP", "1"))
+        key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index, scenes, pkey)
+        comm = self._comm if plan is not None else None
         with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
             entry = self._graphs.get(key)
             if entry is None:
@@ -444,13 +472,31 @@ class MapAnything:
                 side = torch.cuda.Stream(imgs.device)
                 side.wait_stream(torch.cuda.current_stream(imgs.device))
                 with torch.cuda.stream(side):  # eager warm-up: lazy packing, pos-embed caches
-                    eng.run(static_in, pe_idx=static_pe)
+                    eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
                 torch.cuda.current_stream(imgs.device).wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
                 # captured on the warm-up stream: the per-stream GEMM / attention workspaces made in the warm-up
-                # are the ones the graph uses (no allocation or zero-fill inside the capture)
-                with torch.cuda.graph(graph, stream=side):
-                    static_out = eng.run(static_in, pe_idx=static_pe)
+                # are the ones the graph uses (no allocation or zero-fill inside the capture).  With a shard the
+                # capture is thread-local: the communicator's watchdog thread keeps querying its events meanwhile
+                mode = "global" if plan is None else "thread_local"
+                if plan is None:
+                    with torch.cuda.graph(graph, stream=side, capture_error_mode=mode):
+                        static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
+                else:
+                    # every rank captures the same collectives in the same order, so a capture that fails on one
+                    # rank fails on all; the ranks still agree (one eager all-reduce) before any replays, and fall
+                    # back to the eager sharded path together, whose collectives match a replay's one for one
+                    err = None
+                    try:
+                        with torch.cuda.graph(graph, stream=side, capture_error_mode=mode):
+                            static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
+                    except Exception as e:  # noqa: BLE001 -- any capture failure: agree, then run eager
+                        err = e
+                    if not self._comm.all_agree(err is None, imgs.device):
+                        warnings.warn(f"sharded HIP-graph capture failed ({err or 'on another rank'}); "
+                                      "running the sharded path eagerly")
+                        self._shard_graphs = False
+                        return eng.run(imgs, shard=plan, comm=self._comm, pe_idx=pe_idx, scenes=scenes)
                 # the side stream is kept with the graph: its handle keys the per-stream workspaces the graph
                 # captured (_native._WS/_AWS), so it must not be destroyed and its handle reused while the graph lives
                 entry = (graph, static_in, static_out, static_pe, side)
@@ -485,7 +531,8 @@ class MapAnything:
             precision = "fp32"
         validated = validate_input_views_for_inference(views)
         B = self._check_views(validated)
-        if B > 1:  # scene by scene (module docstring), outputs concatenated per view as the reference returns them
+        if B > 1 and not self._batchable(validated):
+            # scene by scene (module docstring), outputs concatenated per view as the reference returns them
             kw = dict(memory_efficient_inference=memory_efficient_inference, use_amp=use_amp, amp_dtype=amp_dtype,
                       apply_mask=apply_mask, mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
                       edge_depth_threshold=edge_depth_threshold, apply_confidence_mask=apply_confidence_mask,
@@ -510,15 +557,15 @@ class MapAnything:
                                use_depth=not ignore_depth_inputs, use_pose=not ignore_pose_inputs,
                                use_depth_scale=not ignore_depth_scale_inputs,
                                use_pose_scale=not ignore_pose_scale_inputs)
-        imgs = torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32)
+        imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         eng = self.engine(precision)
-        raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference))
+        raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)
         post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
                                    mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
                                    edge_depth_threshold=edge_depth_threshold,
                                    apply_confidence_mask=apply_confidence_mask,
                                    confidence_percentile=confidence_percentile)
-        return self._finish(post, plan, len(views), with_post=True)
+        return self._finish(post, plan, len(views), with_post=True, scenes=B)
 
     def _dpt_chunk(self, memory_efficient: bool):
         """Views per dense-head pass.  memory_efficient_inference mirrors _compute_adaptive_minibatch_size
@@ -540,11 +587,12 @@ class MapAnything:
         plan = ShardPlan(len(views), self._comm.world, self._comm.rank, (H // 14) * (W // 14))
         return [views[i] for i in plan.local_views], plan
 
-    def _finish(self, batched, plan, V, with_post):
+    def _finish(self, batched, plan, V, with_post, scenes: int = 1):
         """Batched view-major outputs of this rank -> the reference's per-view list (gathered across ranks when
-        enable_view_sharding(gather_outputs=...) asks for it)."""
+        enable_view_sharding(gather_outputs=...) asks for it).  scenes > 1: scene-major outputs of B batched scenes
+        -> per view (B, ...) tensors."""
         if plan is None:
-            return split_views(batched, V, with_post)
+            return split_views(batched, V, with_post, scenes)
         if self._gather is not None and plan.world > 1:
             dst = 0 if self._gather == "rank0" else None
             full = {}
@@ -562,20 +610,25 @@ class MapAnything:
     __call__ = forward
 
 
-def split_views(out: Dict[str, torch.Tensor], V: int, with_post: bool) -> List[Dict[str, torch.Tensor]]:
-    """Batched view-major outputs -> the reference's list of per-view dicts (B = 1), as views (no copies)."""
+def split_views(out: Dict[str, torch.Tensor], V: int, with_post: bool, scenes: int = 1) -> List[Dict[str, torch.Tensor]]:
+    """Batched outputs -> the reference's list of per-view dicts: B = 1 as views of the view-major rows (no copies);
+    B = scenes > 1 from scene-major rows (image b*V + v) gathered into (B, ...) per view."""
     res = []
+    B = scenes
     for i in range(V):
         d = {}
+        sel = None if B == 1 else torch.arange(B, device=next(iter(out.values())).device) * V + i
         for k, t in out.items():
-            if k == "metric_scaling_factor":
+            if k == "metric_scaling_factor":  # one row per scene, shared by its views
                 d[k] = t
-            elif k == "non_ambiguous_mask":
-                d[k] = t[i:i + 1].bool()
+                continue
+            x = t[i:i + 1] if sel is None else t.index_select(0, sel)
+            if k == "non_ambiguous_mask":
+                d[k] = x.bool()
             elif k == "mask":
-                d[k] = t[i:i + 1].bool().unsqueeze(-1)
+                d[k] = x.bool().unsqueeze(-1)
             else:
-                d[k] = t[i:i + 1]
+                d[k] = x
         if "pts3d_cam" in d:
             d["depth_z"] = d["pts3d_cam"][..., 2:3]
         res.append(d)

@@ -26,6 +26,13 @@ from typing import List, Optional, Tuple
 import torch
 
 
+def force_collectives() -> bool:
+    """Debug switch MAPA_FORCE_COLLECTIVES=1: a one-rank shard still runs the K/V all-gather (gather-first form) and
+    the scale-token broadcast through its communicator, so the collective path — RCCL under HIP-graph capture
+    included — runs on a single GPU."""
+    return os.environ.get("MAPA_FORCE_COLLECTIVES", "0") == "1"
+
+
 class CommError(RuntimeError):
     """A collective of the view-sharded path failed or timed out (dead peer, RCCL / gloo error).  Raised instead of
     hanging; the process is expected to exit non-zero (bench.py does)."""
@@ -115,6 +122,9 @@ class DistComm:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        # RCCL collectives are enqueued on the device and can be captured into a HIP graph (fork / join with the
+        # communicator's stream); gloo's run on the host
+        self.graph_safe = dist.get_backend(group) == "nccl"
 
     def _call(self, what, fn, *a, **k):
         """Run one collective; a backend error (gloo raises on a dead peer / timeout, RCCL's watchdog on a timed-out
@@ -149,6 +159,12 @@ class DistComm:
         """In place: every rank's t = rank src's t."""
         self._call("scale-token broadcast", self.dist.broadcast, t, src, group=self.group)
 
+    def all_agree(self, ok: bool, device) -> bool:
+        """True on every rank iff ok on every rank (an eager MIN all-reduce of one int, never captured)."""
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+        self._call("agreement all-reduce", self.dist.all_reduce, flag, op=self.dist.ReduceOp.MIN, group=self.group)
+        return bool(flag.item())
+
     def gather_views(self, local: torch.Tensor, counts: List[int], dst: Optional[int]) -> Optional[torch.Tensor]:
         """View-major local rows [counts[rank], ...] -> [sum(counts), ...] in rank order on rank dst (None: on
         every rank); other ranks get None.  Slots are padded to max(counts) so one collective moves them."""
@@ -174,6 +190,8 @@ class ThreadComm:
     """In-process communicator for tests: P threads (one engine each, same device) exchange slots through a
     barrier; the exchanged bytes are identical to what all_gather_into_tensor delivers.  Each rank thread must
     launch on its own HIP stream (as separate processes do): the library's scratch buffers are per stream."""
+
+    graph_safe = False  # host synchronisation inside every exchange
 
     def __init__(self, world: int):
         self.world = world

@@ -1,0 +1,64 @@
+"""Worker of tests/test_gpu_distcomm.py::test_one_rank_rccl_sharded_graph: a real one-rank RCCL ("nccl") process
+group on the test box's GPU, MAPA_FORCE_COLLECTIVES=1 so the K/V all-gathers and the scale-token broadcast run
+through RCCL although the shard holds every view; the sharded forward runs eager and HIP-graph captured / replayed.
+Writes its result as JSON to argv[1]."""
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "map-anything_amd"))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+KEYS = ("pts3d", "conf", "depth_along_ray", "ray_directions", "cam_quats", "cam_trans", "metric_scaling_factor")
+
+
+def main():
+    out = sys.argv[1]
+    torch.cuda.set_device(0)
+    os.environ["MAPA_FORCE_COLLECTIVES"] = "1"
+    from mapanything.models import MapAnything
+    from mapanything.parallel import init_distributed
+    from mapanything.utils import synthetic
+    from tests_helpers import released_config
+
+    rank, world = init_distributed("nccl", torch.device("cuda", 0))
+    assert world == 1 and dist.get_backend() == "nccl"
+    V = 3
+    views = [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]}
+             for i in synthetic.synthetic_images(V, 224, 224, 41)]
+    res = {}
+    for prec in ("fp32", "bf16"):
+        model = MapAnything(**released_config(), precision=prec).load_synthetic_weights().to("cuda")
+        kw = dict(use_amp=prec == "bf16", apply_mask=False)
+        single = model.infer(views, **kw)  # unsharded (graph-replayed on one GPU)
+        model.enable_view_sharding(dist.group.WORLD)
+        model.hip_graphs = False
+        eager = model.infer(views, **kw)
+        model.hip_graphs = True
+        g1 = model.infer(views, **kw)  # captures the sharded forward (RCCL collectives inside the graph)
+        g2 = model.infer(views, **kw)  # replays it
+        torch.cuda.synchronize()
+        res[prec] = {
+            "sharded_graph_keys": sum(1 for k in model._graphs if k[-1] is not None),
+            "graph_eq_eager": all(torch.equal(a[k], b[k]) for a, b in zip(g1, eager) for k in KEYS),
+            "replay_eq_eager": all(torch.equal(a[k], b[k]) for a, b in zip(g2, eager) for k in KEYS),
+            "eager_eq_single": all(torch.equal(a[k], b[k]) for a, b in zip(eager, single) for k in KEYS),
+            "err_vs_single": {k: max(rel(eager[v][k], single[v][k]) for v in range(V)) for k in KEYS},
+        }
+    with open(out, "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,13 +24,19 @@ def _free_port():
     return p
 
 
+def _rank_errors(r):
+    """The ranks' own tracebacks ([rankN]: lines), which torch.distributed.run's summary would push out of view."""
+    lines = [ln for ln in (r.stdout + r.stderr).splitlines() if ln.startswith("[rank")]
+    return "\n".join(lines[-80:]) or (r.stdout[-3000:] + r.stderr[-3000:])
+
+
 def test_two_process_view_sharding_over_distcomm(tmp_path):
     prefix = str(tmp_path / "res")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "dist_worker.py"), prefix]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _rank_errors(r)
     res = [json.load(open(f"{prefix}.{k}.json")) for k in range(2)]
     for ov in ("1", "0"):
         s = res[0][f"scales_{ov}"]
@@ -38,3 +44,23 @@ def test_two_process_view_sharding_over_distcomm(tmp_path):
         assert res[0][f"n_views_{ov}"] == 3 and res[1][f"n_views_{ov}"] == 1  # gathered on rank 0 only
         err = res[0][f"err_{ov}"]
         assert all(e < 2e-5 for e in err.values()), (ov, err)
+
+
+def test_one_rank_rccl_sharded_graph(tmp_path):
+    """A real one-rank RCCL process group (tests/nccl1_worker.py, MAPA_FORCE_COLLECTIVES=1): the sharded forward with
+    its K/V all-gathers and scale-token broadcast through RCCL, eager and HIP-graph captured / replayed, in fp32 and
+    in the bf16 recipe.  Graph-replayed == eager bitwise; sharded == unsharded (fp32 within 2e-5: the sharded global
+    layers project Q and K/V in two GEMMs and attend through the segment table)."""
+    out = str(tmp_path / "nccl1.json")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(HERE, "nccl1_worker.py"), out]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, _rank_errors(r)
+    res = json.load(open(out))
+    print("\n[one-rank RCCL sharded forward]", json.dumps(res, indent=1))
+    for prec in ("fp32", "bf16"):
+        d = res[prec]
+        assert d["sharded_graph_keys"] == 1, d
+        assert d["graph_eq_eager"] and d["replay_eq_eager"], d
+    assert all(e < 2e-5 for e in res["fp32"]["err_vs_single"].values()), res["fp32"]

@@ -314,7 +314,7 @@ def test_regressor_head_out_repeatable(nat):
             [torch.empty((n, H, W), device="cuda") for _ in range(2)] + \
             [torch.empty((n, H, W), dtype=torch.uint8, device="cuda")]
         nat.gemm(a, wp, M, C, 9 * 3 * C, bias=b2, act=nat.ACT_RELU, conv=(3 * C, H, W, H, W, 1),
-                 head_out=(w6, b6, pose_out, scale, *o))
+                 head_out=(w6, b6, pose_out, scale, n, *o))
         return o
     first = run()
     for _ in range(6):
@@ -364,10 +364,18 @@ def test_regressor_head_out_fused(nat, split, n, H, W):
     ref = outs()
     nat.dense_head_out(hid, n, H * W, w6, b6, pose_out, scale, 1, *ref)
     got = outs()
-    nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scale, *got))
+    nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scale, n, *got))
     torch.cuda.synchronize()
     for r, g in zip(ref[:6], got[:6]):
         assert torch.isfinite(g).all()
+        assert rel_l2(g.cpu(), r.cpu()) < 1e-5
+    # one metric scale per image (batched scenes, views_per_scale = 1) against the unfused head with batch = n
+    scales = torch.rand(n, device="cuda") + 0.5
+    ref_b, got_b = outs(), outs()
+    nat.dense_head_out(hid, n, H * W, w6, b6, pose_out, scales, n, *ref_b)
+    nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scales, 1, *got_b))
+    torch.cuda.synchronize()
+    for r, g in zip(ref_b[:6], got_b[:6]):
         assert rel_l2(g.cpu(), r.cpu()) < 1e-5
     logits = ref[5].cpu()
     decided = logits.abs() > 1e-4

@@ -212,9 +212,9 @@ def test_split_precision_heads_match_fp32_heads_at_cfg2_size(model):
     res = {}
     for name, eng in (("fp32", e32), ("split", e16)):
         t2 = {}
-        out = eng.heads(eng.head_rows(taps["fused"].contiguous()), eng.head_rows(taps["aat_l11"].contiguous()),
-                        eng.head_rows(taps["aat_l17"].contiguous()), eng.head_rows(fin), tok, V, hp, wp, H, W,
-                        taps=t2)
+        out = eng.run_heads(eng.head_rows(taps["fused"].contiguous()), eng.head_rows(taps["aat_l11"].contiguous()),
+                            eng.head_rows(taps["aat_l17"].contiguous()), eng.head_rows(fin), tok, V, hp, wp, H, W,
+                            taps=t2)
         torch.cuda.synchronize()
         res[name] = dict(out, pose_raw=t2["pose_raw"], scale_raw=t2["scale_raw"], dpt_feature=t2["dpt_feature"])
     print("\n[split heads vs fp32 heads, 8 x 518^2, identical fp32 inputs] rel-L2:")
@@ -230,6 +230,45 @@ def test_split_precision_heads_match_fp32_heads_at_cfg2_size(model):
     lg = res["fp32"]["non_ambiguous_mask_logits"]
     sure = lg.abs() > 1e-3
     assert torch.equal(res["split"]["non_ambiguous_mask"][sure], res["fp32"]["non_ambiguous_mask"][sure])
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_batched_scenes_match_scene_by_scene(model, precision):
+    """B = 2 scenes x 3 image-only views (each view's img (2, 3, H, W)) run as ONE engine call — images scene-major,
+    encoder / frame layers / heads over all six images, each global layer per scene over its tokens + its scale
+    token, one metric scale per scene (the reference's batched forward, model.py:687-721) — against each scene run
+    alone: fp32 within 2e-5 (the attention work split depends on the task count), the bf16 recipe within the
+    reference's bf16 spread (b2_224).
+    Also the HIP-graph replay of the batched call == its eager run."""
+    from mapanything.utils import synthetic
+
+    imgs = synthetic.synthetic_images(3, 224, 224, seed=51, batch=2)
+    views = [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]} for i in imgs]
+    kw = dict(use_amp=precision == "bf16", apply_mask=False)
+    assert model._batchable(views)
+    batched = model.infer(views, **kw)
+    assert any(k[4] == 2 for k in model._graphs), "the batched call is graph-captured with scenes = 2"
+    again = model.infer(views, **kw)  # graph replay
+    model.hip_graphs = False
+    try:
+        eager = model.infer(views, **kw)
+    finally:
+        model.hip_graphs = True
+    per = [model.infer([{"img": torch.from_numpy(i[b:b + 1]), "data_norm_type": ["dinov2"]} for i in imgs], **kw)
+           for b in range(2)]
+    spread = _spread("b2_224")
+    for v in range(3):
+        for k in ("pts3d", "conf", "depth_along_ray", "ray_directions", "cam_quats", "cam_trans", "intrinsics",
+                  "metric_scaling_factor"):
+            # bf16: two executions of the recipe that round differently (GEMM rows, attention splits) — within the
+            # reference's own bf16-vs-fp32 spread on two-scene 224^2 inputs (b2_224)
+            tol = 2e-5 if precision == "fp32" else spread["out_" + k]
+            ref = torch.cat([per[b][v][k] for b in range(2)], 0)
+            assert batched[v][k].shape == ref.shape, (k, batched[v][k].shape, ref.shape)
+            e = rel_l2(batched[v][k].float().cpu().numpy(), ref.float().cpu().numpy())
+            print(f"  view {v} {k:22s} {e:.3e} (bound {tol:.1e})")
+            assert e < tol, (v, k, e, tol)
+            assert torch.equal(batched[v][k], again[v][k]) and torch.equal(batched[v][k], eager[v][k]), (v, k)
 
 
 def test_fp32_geometric_fused_tap(model, golden):

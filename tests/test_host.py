@@ -159,3 +159,29 @@ def test_save_pretrained_round_trip(tmp_path):
         assert np.array_equal(m._sd[k], src._sd[k]), k
     with pytest.raises(FileNotFoundError):
         MapAnything.from_pretrained(str(tmp_path / "missing"))
+
+
+def test_batched_scene_layout_round_trip():
+    """B scenes x V views: the per-view (B, ...) image tensors concatenated view-major -> scene-major engine rows
+    (image b*V + v) -> split_views gives each view back its (B, ...) rows in scene order (reference model.py:687-721
+    batches scenes along dim 0 of every view)."""
+    from mapanything.models.mapanything.model import MapAnything, split_views
+
+    V, B = 3, 2
+    per_view = [torch.arange(B * 4, dtype=torch.float32).view(B, 1, 2, 2) + 100 * v for v in range(V)]
+    rows = MapAnything._scene_major(torch.cat(per_view, 0), B)
+    for b in range(B):
+        for v in range(V):
+            assert torch.equal(rows[b * V + v], per_view[v][b])
+    msf = torch.tensor([[1.5], [2.5]])
+    out = split_views({"pts3d": rows.permute(0, 2, 3, 1).expand(-1, -1, -1, 3).contiguous(),
+                       "non_ambiguous_mask": (rows[:, 0] > 102).to(torch.uint8), "metric_scaling_factor": msf},
+                      V, with_post=False, scenes=B)
+    assert len(out) == V
+    for v in range(V):
+        assert out[v]["pts3d"].shape == (B, 2, 2, 3)
+        assert torch.equal(out[v]["pts3d"][..., 0], per_view[v][:, 0])
+        assert out[v]["non_ambiguous_mask"].dtype == torch.bool
+        assert torch.equal(out[v]["non_ambiguous_mask"], per_view[v][:, 0] > 102)
+        assert torch.equal(out[v]["metric_scaling_factor"], msf)
+    assert torch.equal(MapAnything._scene_major(rows, 1), rows)

@@ -119,7 +119,7 @@ def test_sharded_global_attention_gloo(world, V, overlap):
 
 
 def _gather_worker(rank, world, port, q):
-    """DistComm.broadcast_ (the scale-token feature) and gather_views (outputs to rank 0 / to every rank) over a
+    """DistComm.broadcast_ (the scale-token feature), all_agree and gather_views (outputs to rank 0 / to every rank) over a
     real gloo group, and MapAnything._finish assembling the reference's per-view list from them."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -133,6 +133,8 @@ def _gather_worker(rank, world, port, q):
         tok = torch.full((1, 8), float(rank + 1))
         comm.broadcast_(tok, 0)
         ok_bcast = bool((tok == 1.0).all())
+        # the sharded graph-capture fallback's agreement: one failing rank makes every rank fall back
+        ok_bcast &= comm.all_agree(True, "cpu") and not comm.all_agree(rank != world - 1, "cpu")
         lv = list(plan.local_views)
         local = {"pts3d": torch.stack([torch.full((1, 2, 2, 3), float(v)) for v in lv], 0).view(len(lv), 2, 2, 3),
                  "non_ambiguous_mask": torch.tensor([[[v % 2 == 0]] for v in lv]).view(len(lv), 1, 1),

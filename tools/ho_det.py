@@ -43,7 +43,7 @@ def main():
         f = dict(device="cuda")
         o = [torch.empty((n, H, W, 3), **f) for _ in range(3)] + [torch.empty((n, H, W, 1), **f)] + \
             [torch.empty((n, H, W), **f) for _ in range(2)] + [torch.empty((n, H, W), dtype=torch.uint8, device="cuda")]
-        nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scale, *o))
+        nat.gemm(a, wp, M, C, 9 * Cl, bias=b2, act=nat.ACT_RELU, conv=conv, head_out=(w6, b6, pose_out, scale, n, *o))
         torch.cuda.synchronize()
         return o
     names = ["pts3d", "pts3d_cam", "rays", "depth", "conf", "logits", "mask"]
