@@ -237,8 +237,8 @@ def test_batched_scenes_match_scene_by_scene(model, precision):
     """B = 2 scenes x 3 image-only views (each view's img (2, 3, H, W)) run as ONE engine call — images scene-major,
     encoder / frame layers / heads over all six images, each global layer per scene over its tokens + its scale
     token, one metric scale per scene (the reference's batched forward, model.py:687-721) — against each scene run
-    alone: fp32 within 2e-5 (the attention work split depends on the task count), the bf16 recipe within the
-    reference's bf16 spread (b2_224).
+    alone: fp32 within 2e-5 (the attention work split depends on the task count), the bf16 recipe within twice
+    the reference's bf16 spread (b2_224).
     Also the HIP-graph replay of the batched call == its eager run."""
     from mapanything.utils import synthetic
 
@@ -260,9 +260,10 @@ def test_batched_scenes_match_scene_by_scene(model, precision):
     for v in range(3):
         for k in ("pts3d", "conf", "depth_along_ray", "ray_directions", "cam_quats", "cam_trans", "intrinsics",
                   "metric_scaling_factor"):
-            # bf16: two executions of the recipe that round differently (GEMM rows, attention splits) — within the
-            # reference's own bf16-vs-fp32 spread on two-scene 224^2 inputs (b2_224)
-            tol = 2e-5 if precision == "fp32" else spread["out_" + k]
+            # bf16: two executions of the recipe that round differently (GEMM rows, attention splits), each one
+            # within the reference's bf16-vs-fp32 spread on two-scene 224^2 inputs (b2_224) of the fp32 result:
+            # their difference within twice that spread
+            tol = 2e-5 if precision == "fp32" else 2 * spread["out_" + k]
             ref = torch.cat([per[b][v][k] for b in range(2)], 0)
             assert batched[v][k].shape == ref.shape, (k, batched[v][k].shape, ref.shape)
             e = rel_l2(batched[v][k].float().cpu().numpy(), ref.float().cpu().numpy())
