@@ -416,7 +416,7 @@ def test_hip_graph_replay_matches_eager(model, precision):
     assert model.hip_graphs
     g_a = model._run_engine(eng, imgs_a, None, None, None)
     g_b = model._run_engine(eng, imgs_b, None, None, None)  # replay of the graph captured by the first call
-    assert (precision, eng.heads, tuple(imgs_a.shape), imgs_a.device.index) in model._graphs
+    assert (precision, eng.heads, tuple(imgs_a.shape), imgs_a.device.index, 1, None) in model._graphs
     for k in eager_a:
         assert torch.equal(g_a[k], eager_a[k]), k
         assert torch.equal(g_b[k], eager_b[k]), k
