@@ -105,12 +105,15 @@ def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
         nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=r, out_f32=out, out_lp=lp)
         again = torch.empty_like(out)
         nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=r, out_f32=again)
+        inplace = r.clone()  # the transformer's residual update: x += gamma * (A W^T + b), residual loaded ahead
+        nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=inplace, out_f32=inplace)
         torch.cuda.synchronize()
     finally:
         nat.gemm_set_variant(0)
     assert rel_l2(out.cpu(), ref.cpu()) < 1e-4
     assert rel_l2(lp.float().cpu(), ref.cpu()) < 5e-3
     assert torch.equal(out, again)
+    assert torch.equal(out, inplace)
     if 2580 <= variant <= 2582:  # tickets (the workspace head) back to zero for the next call
         ws = nat.gemm_workspace(0)
         assert ws.numel() > 0 and int(ws[: 4 * 65536].count_nonzero()) == 0
