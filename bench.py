@@ -158,7 +158,8 @@ def main():
             dt = float(t.item())
         return dt
 
-    # timed region: the production path (single GPU: the engine's launches replayed from a HIP graph)
+    # timed region: the production path (the engine's launches replayed from a HIP graph: one GPU, or a view shard
+    # whose K/V all-gathers run on RCCL inside the graph)
     dt = timed(args.steps)
     ktimes, instr_ms = {}, None
     if not args.no_kernel_timing:
@@ -213,7 +214,7 @@ def main():
         s_imgs = synthetic.synthetic_images(args.strong_views, H, W, seed=3)
         s_views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in s_imgs]
         del s_imgs
-        model.infer(s_views, **amp)  # warm-up (graph capture at N=1)
+        model.infer(s_views, **amp)  # warm-up (graph capture)
         sdt = timed_fn(lambda: model.infer(s_views, **amp), args.strong_steps)
         strong = {"views": args.strong_views, "value": args.strong_views * args.strong_steps / sdt, "unit": "views/s",
                   "ms_per_step": sdt / args.strong_steps * 1e3, "steps": args.strong_steps, "warmup": 1,
@@ -302,7 +303,9 @@ def main():
             "batched_scenes": batched,
             "fast_mode_bf16_heads": fast,
             "strong_scaling": strong,
-            "hip_graphs": bool(model.hip_graphs and world == 1 and not args.geometric),
+            # one GPU, or a view shard over RCCL (kernels and collectives captured together; MAPA_SHARD_GRAPHS=0 or a
+            # failed capture on any rank: eager)
+            "hip_graphs": bool(model.hip_graphs and not args.geometric and (world == 1 or model._shard_graphs)),
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
