@@ -98,6 +98,21 @@ typedef struct {
    * taps of one B-channel slice, so the slice of the input window stays L2-resident across the taps instead of being
    * re-fetched per tap (the head convs' fabric traffic: 9-20x their algorithmic bytes tap-major). */
   int conv_kblock;
+  /* Fused LayerNorm of the output rows (ln_out NULL = off; round 4): after the epilogue, every row of out_f32 (the
+   * updated fp32 residual stream; N = the LayerNorm width, 256 / 512 / 768 / 1024) is normalised with ln_w / ln_b
+   * (fp32 [N]) and ln_eps and stored to ln_out in the GEMM's 16-bit dtype (fp32 for MAPA_F32), row stride ln_ldo —
+   * the next sub-block's nn.LayerNorm fused into the residual linear (dinov2 layers/block.py:93-118,
+   * transformer_blocks.py:452-469).  Needs out_f32, row-major.  For bf16 residual linears (out_f32 = resid1 +
+   * gamma * (acc + bias), nothing else) whose tiles are the 192-row data-parallel kernel, and with a workspace of
+   * mapa_gemm_workspace_bytes, the statistics combine across the row's column tiles inside the launch (two-pass per
+   * tile, Chan's merge across tiles: the standalone result up to fp32 rounding of mean / variance); otherwise the
+   * GEMM is followed by mapa_layernorm on the same stream.  A band barrier that does not complete within its bounded
+   * wait sets int word 65535 of the workspace (the last word of its 256 KiB head) to 1 instead of hanging. */
+  const float* ln_w;
+  const float* ln_b;
+  float ln_eps;
+  void* ln_out;
+  int64_t ln_ldo;
 } mapa_gemm_desc;
 
 int mapa_gemm(const mapa_gemm_desc* d, mapa_stream_t stream);
@@ -132,8 +147,13 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *     tile (variant 2589 forces it; needs the workspace mapa_gemm_workspace_bytes reports);
  *   MAPA_TUNE_TAIL_STREAMK (default 0): dense bf16 GEMMs whose 256x128 tiles leave a nearly empty last wave use
  *     the tail-only stream-K schedule (2582) when a workspace is passed;
- *   MAPA_TUNE_HALO_SPLIT (default 0 = automatic): the K part count of the flat-raster halo conv (1..64). */
-enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2 };
+ *   MAPA_TUNE_HALO_SPLIT (default 0 = automatic): the K part count of the flat-raster halo conv (1..64).
+ *   MAPA_TUNE_TILE_GROUP (default 0 = 4): the 256-row data-parallel GEMM kernels walk each XCD's tile range in
+ *     groups of this many tile rows (all tile columns of a group before the next group).
+ *   MAPA_TUNE_LN_FUSE (default 1, or the environment's MAPA_LN_FUSE): ln_out requests run fused into the residual
+ *     linear where it qualifies; 0 = always as a separate mapa_layernorm launch (A/B). */
+enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,
+       MAPA_TUNE_LN_FUSE = 4 };
 int mapa_gemm_tune(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------------------

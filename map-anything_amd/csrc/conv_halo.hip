@@ -495,7 +495,8 @@ int conv_halo_flat_split(const GemmArgs& a, int slots, int force) {
 int64_t conv_halo_flat_workspace_bytes(const GemmArgs& a, int nsplit, int64_t ticket_bytes) {
   if (!flat_ok(a) || nsplit <= 1) return 0;
   const int64_t tiles = flat_blocks(a) * (a.N / 128);
-  if (tiles * 4 > ticket_bytes) return -1;  // more tiles than ticket words: not this kernel
+  // more tiles than ticket words (the top LN_TICKET_WORDS are the LayerNorm-fused GEMM's): not this kernel
+  if ((tiles + LN_TICKET_WORDS) * 4 > ticket_bytes) return -1;
   return ticket_bytes + tiles * nsplit * 256 * 128 * 4;
 }
 

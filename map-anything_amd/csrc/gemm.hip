@@ -327,6 +327,16 @@ static bool halo_rows8(const GemmArgs& a) {
 // 19^2 / 37^2 DPT convs: 26-144 tiles of 16x16 blocks, 41-65 % of their pixels idle), which the stream-K implicit
 // GEMM ran before.  Returns the K part count, 0 = not this kernel.
 static int g_halo_split = 0;  // mapa_gemm_tune(MAPA_TUNE_HALO_SPLIT, .): 0 = automatic part count
+static int g_tile_gm = 4;     // mapa_gemm_tune(MAPA_TUNE_TILE_GROUP, .): tile rows per group of gemm_big_kernel
+static int g_ln_fuse = -1;    // mapa_gemm_tune(MAPA_TUNE_LN_FUSE, .) / env MAPA_LN_FUSE (A/B switch); -1: env not read
+
+// The residual linears whose automatic tile choice is the 192-row data-parallel kernel (the path's proj / fc2 at
+// 8 views) fuse a requested output LayerNorm (launch_gemm_big_ln); everything else runs it as its own launch.
+static int pick_ln_fused(const mapa_gemm_desc* d, int variant, int sk) {
+  if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? (atoi(getenv("MAPA_LN_FUSE")) != 0) : 1;
+  if (!d->ln_out || !g_ln_fuse || d->dtype != MAPA_BF16 || d->a_mode != MAPA_A_DENSE || d->a_split || sk) return 0;
+  return variant == 2574 ? 14 : variant == 2587 ? 15 : 0;
+}
 static int pick_flat(const GemmArgs& a) {
   if (g_halo != 1 || pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb)) return 0;
   return conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split);
@@ -439,6 +449,16 @@ static int gemm_args(const mapa_gemm_desc* d, GemmArgs& a) {
   a.out_s3 = d->out_s3; a.out_s3_relu = d->out_s3_relu;
   a.out_mode = d->out_mode; a.ps_s = d->ps_s; a.ps_h = d->ps_h; a.ps_w = d->ps_w; a.ps_cout = d->ps_cout;
   a.vec_ok = (d->N % 4 == 0) && (d->out_mode == MAPA_OUT_PIXSHUF || d->ldo % 4 == 0);
+  a.tile_gm = g_tile_gm;
+  if (d->ln_out) {
+    MAPA_CHECK_ARG(d->ln_w && d->ln_b && d->out_f32 && d->out_mode == MAPA_OUT_ROWMAJOR,
+                   "mapa_gemm: ln_out needs ln_w, ln_b and a row-major out_f32");
+    MAPA_CHECK_ARG(d->N == 256 || d->N == 512 || d->N == 768 || d->N == 1024, "mapa_gemm: LayerNorm width N=%d", d->N);
+    MAPA_CHECK_ARG(d->ln_ldo >= d->N && d->ln_ldo % 4 == 0 && d->ldo % 4 == 0,
+                   "mapa_gemm: ln_ldo must be >= N and ln_ldo, ldo multiples of 4");
+  }
+  a.ln_w = d->ln_w; a.ln_b = d->ln_b; a.ln_eps = d->ln_eps; a.ln_out = d->ln_out; a.ln_ldo = d->ln_ldo;
+  a.ln_ctr = nullptr; a.ln_stats = nullptr;
   MAPA_CHECK_ARG(a.vec_ok || d->out_mode == MAPA_OUT_ROWMAJOR, "mapa_gemm: pixel shuffle needs N %% 4 == 0");
   return 0;
 }
@@ -460,6 +480,11 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   const int flat = !conv || d->dtype != MAPA_BF16 ? 0
                    : forced ? (forced == 2589 ? conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split) : 0)
                             : pick_flat(a);
+  const int lnf = pick_ln_fused(d, variant, sk);
+  if (lnf && launch_gemm_big_ln(a, lnf, d->workspace, d->workspace_bytes, stream)) {
+    MAPA_CHECK_LAUNCH("mapa_gemm (LayerNorm fused)");
+    return 0;  // launched (residual linear + the LayerNorm of its output rows)
+  }
   if (flat && launch_conv_halo_flat(a, flat, d->workspace, d->workspace_bytes, GEMM_TICKET_BYTES, stream)) {
     // launched (flat-raster halo conv, split K)
   } else if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
@@ -481,6 +506,9 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
     else launch_variant<TraitsF32, 0>(variant, nblk, stream, a);
   }
   MAPA_CHECK_LAUNCH("mapa_gemm");
+  if (d->ln_out)  // the requested LayerNorm as its own launch (same stream, after the GEMM)
+    return mapa_layernorm(d->out_f32, d->ldo, d->M, d->N, d->ln_w, d->ln_b, d->ln_eps, nullptr, d->ln_out,
+                          d->dtype, d->ln_ldo, 0, 0, 0, stream);
   return 0;
 }
 
@@ -505,11 +533,15 @@ extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6,
 }
 
 extern "C" int mapa_gemm_tune(int key, int value) {
-  MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK || key == MAPA_TUNE_HALO_SPLIT,
+  MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK || key == MAPA_TUNE_HALO_SPLIT ||
+                     key == MAPA_TUNE_TILE_GROUP || key == MAPA_TUNE_LN_FUSE,
                  "mapa_gemm_tune: unknown key %d", key);
   MAPA_CHECK_ARG(key != MAPA_TUNE_HALO_SPLIT || (value >= 0 && value <= 64), "mapa_gemm_tune: split %d", value);
+  MAPA_CHECK_ARG(key != MAPA_TUNE_TILE_GROUP || (value >= 0 && value <= 1024), "mapa_gemm_tune: group %d", value);
   if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 || value == 3 ? value : value ? 1 : 0;
   else if (key == MAPA_TUNE_HALO_SPLIT) g_halo_split = value;
+  else if (key == MAPA_TUNE_TILE_GROUP) g_tile_gm = value ? value : 4;
+  else if (key == MAPA_TUNE_LN_FUSE) g_ln_fuse = value ? 1 : 0;
   else g_tail_sk = value ? 1 : 0;
   return 0;
 }
@@ -525,6 +557,13 @@ extern "C" int mapa_gemm_set_variant(int variant) {
 
 extern "C" int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d) {
   if (!d || d->dtype != MAPA_BF16 || d->M <= 0 || d->N <= 0 || d->K <= 0) return 0;
+  if (d->ln_out && !forced_variant()) {
+    const bool conv = d->a_mode == MAPA_A_CONV3X3;
+    const int lnf = pick_ln_fused(d, pick_variant(d->dtype, conv, d->M, d->N, d->K),
+                                  pick_streamk(d->dtype, conv, d->M, d->N, d->K));
+    const int64_t b = lnf ? ln_stats_bytes(d->M, d->N, lnf) : -1;
+    if (b >= 0) return GEMM_TICKET_BYTES + b;
+  }
   if (d->a_mode == MAPA_A_CONV3X3) {
     GemmArgs a;
     if (gemm_args(d, a) != 0) return 0;  // a bad descriptor is reported by mapa_gemm itself

@@ -131,12 +131,213 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& p, f32x4 (&acc)[FM]
   else epilogue(std::integral_constant<int, 0>());
 }
 
+// ---- LayerNorm-fused residual epilogue (LNF) ---------------------------------------------------------------------
+// The in-place residual pattern of epi_mode 2 (out_f32 = resid1 + gamma * (acc + bias): the arithmetic of
+// epi_store_row8_mode<2>), then nn.LayerNorm over each output row, whose N columns are the band's ntn tiles
+// (dinov2 layers/block.py:93-118 norm1 / norm2, transformer_blocks.py:452-469):
+//  1. every lane keeps its 8-column row segments of the new residual in registers (FM/2 parts x 4 passes);
+//  2. per tile row: the sum over the tile's columns (8-lane butterfly, then the WN column waves' partials in LDS in
+//     wave order), the tile mean, then M2 = sum (v - mean_t)^2 the same way (two-pass inside the tile);
+//  3. {sum, M2} of every row published as one 8-byte write-through granule per tile (agent-scope relaxed store),
+//     every storing wave drains (vmcnt 0), then one arrival on the band's counter; one lane polls the counter until
+//     the band's ntn tiles arrived (bounded: past LN_SPIN_LIMIT polls it sets the flag word and proceeds);
+//  4. per row, from the ntn granules read write-through in column order (the same value in every tile of the band):
+//     mean = sum / N, M2 = sum_t (M2_t + n_t (mean_t - mean)^2) (Chan's merge, exact up to rounding), rstd =
+//     rsqrt(M2 / N + eps);
+//  5. the band's last departing block re-zeroes its two counters; every tile writes y = (v - mean) * rstd * w + b as
+//     bf16 for its own columns.
+// Equal to the standalone two-pass LayerNorm (norm.hip) up to the fp32 rounding of the statistics.  The launch needs
+// N % BN == 0 (every tile holds BN columns of a row) and the row-major in-place residual outputs (epi_mode 2).
+constexpr unsigned LN_SPIN_LIMIT = 1u << 22;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) int gi32;
+
+template <int FM, int FN, int TM, int TN, int WN, int BM>
+__device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[FM][FN], char* lds, int tm, int tn,
+                                                int ntn, int wave, int wm, int wn, int lane, int tid) {
+  constexpr int NP = FM / 2, BN = TN * WN;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int bm = tm * BM, bn = tn * BN;
+  float* ep = reinterpret_cast<float*>(lds) + wave * 32 * ELD;
+  float* red = reinterpret_cast<float*>(lds + 8 * 32 * ELD * 4);  // [WN][BM] per-wave row partials
+  float* rmean = red + WN * BM;                                    // [BM] tile mean, then the row mean
+  float* rrstd = rmean + BM;                                       // [BM] row rstd
+  const int c8 = (lane & 7) * 8;
+  const bool col_ok = c8 < TN;  // TN = 48 (192-wide tiles): lanes 6, 7 of each row group idle
+  const int n0 = bn + wn * TN + (col_ok ? c8 : 0);
+  const EpiCol8 ec = epi_col_setup8(p, n0);
+  const f32x4 lw0 = *reinterpret_cast<const f32x4*>(p.ln_w + n0), lw1 = *reinterpret_cast<const f32x4*>(p.ln_w + n0 + 4);
+  const f32x4 lb0 = *reinterpret_cast<const f32x4*>(p.ln_b + n0), lb1 = *reinterpret_cast<const f32x4*>(p.ln_b + n0 + 4);
+  f32x4 keep[NP][4][2];
+  // 1. residual epilogue (the values stay in registers)
+#pragma unroll
+  for (int part = 0; part < NP; ++part) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(i * 16 + g * 4 + r) * ELD + j * 16 + r16] = acc[part * 2 + i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int rloc = pass * 8 + (lane >> 3);
+      const int m = bm + wm * TM + part * 32 + rloc;
+      f32x4 v0 = {0.f, 0.f, 0.f, 0.f}, v1 = {0.f, 0.f, 0.f, 0.f};
+      if (col_ok && m < p.M) {
+        const f32x4 lo = *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8);
+        const f32x4 hi = *reinterpret_cast<const f32x4*>(ep + rloc * ELD + c8 + 4);
+        const int64_t off = (int64_t)m * p.ldo + n0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v0[e] = lo[e] + ec.a.bv[e];
+          v1[e] = hi[e] + ec.b.bv[e];
+        }
+        if (p.gamma) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v0[e] *= ec.a.gv[e];
+            v1[e] *= ec.b.gv[e];
+          }
+        }
+        v0 += *reinterpret_cast<const f32x4*>(p.resid1 + off);
+        v1 += *reinterpret_cast<const f32x4*>(p.resid1 + off + 4);
+        *reinterpret_cast<f32x4*>(p.out_f32 + off) = v0;
+        *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = v1;
+      }
+      keep[part][pass][0] = v0;
+      keep[part][pass][1] = v1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  // 2. tile row sums -> tile means
+#pragma unroll
+  for (int part = 0; part < NP; ++part)
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const f32x4 a = keep[part][pass][0], b = keep[part][pass][1];
+      float s = ((a[0] + a[1]) + (a[2] + a[3])) + ((b[0] + b[1]) + (b[2] + b[3]));
+      s += __shfl_xor(s, 1);
+      s += __shfl_xor(s, 2);
+      s += __shfl_xor(s, 4);
+      if ((lane & 7) == 0) red[wn * BM + wm * TM + part * 32 + pass * 8 + (lane >> 3)] = s;
+    }
+  __syncthreads();
+  float tsum = 0.f;
+  if (tid < BM) {
+#pragma unroll
+    for (int w = 0; w < WN; ++w) tsum += red[w * BM + tid];
+    rmean[tid] = tsum * (1.f / BN);
+  }
+  __syncthreads();
+  // tile M2 about the tile mean
+#pragma unroll
+  for (int part = 0; part < NP; ++part)
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const float mu = rmean[wm * TM + part * 32 + pass * 8 + (lane >> 3)];
+      float q = 0.f;
+      if (col_ok) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float d = keep[part][pass][h][e] - mu;
+            q += d * d;
+          }
+      }
+      q += __shfl_xor(q, 1);
+      q += __shfl_xor(q, 2);
+      q += __shfl_xor(q, 4);
+      if ((lane & 7) == 0) red[wn * BM + wm * TM + part * 32 + pass * 8 + (lane >> 3)] = q;
+    }
+  __syncthreads();
+  // 3. publish {sum, M2} per row, arrive, wait for the band
+  gu64* stats = (gu64*)(p.ln_stats) + (int64_t)tm * ntn * BM;
+  gi32* arrive = (gi32*)(p.ln_ctr) + 2 * tm;
+  gi32* depart = arrive + 1;
+  gi32* flag = (gi32*)(p.ln_ctr) + (LN_TICKET_WORDS - 1);
+  if (tid < BM) {
+    float m2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < WN; ++w) m2 += red[w * BM + tid];
+    const unsigned long long gv =
+        (unsigned long long)__float_as_uint(tsum) | ((unsigned long long)__float_as_uint(m2) << 32);
+    __hip_atomic_store(stats + tn * BM + tid, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through granules
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntn) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > LN_SPIN_LIMIT) {  // a band tile never arrived: flag it, do not hang the device
+        __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the granule loads below the poll
+  // 4. merge the band's statistics (write-through loads, tiles in column order)
+  if (tid < BM) {
+    float sum = 0.f;
+    for (int t = 0; t < ntn; ++t) {
+      const unsigned long long gv = __hip_atomic_load(stats + t * BM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sum += __uint_as_float((unsigned)gv);
+    }
+    const float mean = sum / (float)p.N;
+    float m2 = 0.f;
+    for (int t = 0; t < ntn; ++t) {
+      const unsigned long long gv = __hip_atomic_load(stats + t * BM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const float d = __uint_as_float((unsigned)gv) * (1.f / BN) - mean;
+      m2 += __uint_as_float((unsigned)(gv >> 32)) + (float)BN * d * d;
+    }
+    rmean[tid] = mean;
+    rrstd[tid] = rsqrtf(m2 / (float)p.N + p.ln_eps);
+  }
+  __syncthreads();
+  if (tid == 0) {  // every tile of the band is past its poll: the last one out re-arms the counters
+    if (__hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntn - 1) {
+      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // 5. normalise this tile's columns
+  bf16_t* lout = reinterpret_cast<bf16_t*>(p.ln_out);
+#pragma unroll
+  for (int part = 0; part < NP; ++part)
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = wm * TM + part * 32 + pass * 8 + (lane >> 3);
+      const int m = bm + r;
+      if (!col_ok || m >= p.M) continue;
+      const float mu = rmean[r], rs = rrstd[r];
+      const f32x4 a = keep[part][pass][0], b = keep[part][pass][1];
+      f32x4 y0, y1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        y0[e] = (a[e] - mu) * rs * lw0[e] + lb0[e];
+        y1[e] = (b[e] - mu) * rs * lw1[e] + lb1[e];
+      }
+      const uint4 u = {pack_bf16x2(y0[0], y0[1]), pack_bf16x2(y0[2], y0[3]), pack_bf16x2(y1[0], y1[1]),
+                       pack_bf16x2(y1[2], y1[3])};
+      *reinterpret_cast<uint4*>(lout + (int64_t)m * p.ln_ldo + n0) = u;
+    }
+}
+
 template <int AMODE, int BN, int RB, int STAGES, int DIAG = 0, int PRIO = 0, int MINB = 1, int BM = BBM,
-          bool F16 = false>
+          bool F16 = false, bool LNF = false>
 __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   using C = Cfg<BN, RB, BM>;
   constexpr int MAIN = STAGES * C::STAGE;
-  constexpr int LDS = MAIN > C::EPI ? MAIN : C::EPI;
+  constexpr int EPI = C::EPI + (LNF ? (C::WN * BM + 2 * BM) * 4 : 0);  // + the LayerNorm row partials / statistics
+  constexpr int LDS = MAIN > EPI ? MAIN : EPI;
   constexpr int NPT = C::NLA + C::NLB;  // LDS-DMA instructions per thread per K tile
   __shared__ __attribute__((aligned(1024))) char lds[LDS];
 
@@ -145,7 +346,11 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   const int wm = wave / C::WN, wn = wave % C::WN;
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   int tm, tn;
-  tile_coords<4>(blockIdx.x, ntm, ntn, tm, tn);
+  if constexpr (LNF) {
+    if (!mapa_idx::lnf_coords(blockIdx.x, ntm, ntn, tm, tn)) return;  // idle block of an XCD with one band fewer
+  } else {
+    mapa_idx::tile_coords_rt(blockIdx.x, p.tile_gm, ntm, ntn, tm, tn);
+  }
   const int bm = tm * BM, bn = tn * BN;
 
   // ---- staging geometry: wave instruction i of this wave covers rows (i*8 + wave)*RPI .. +RPI-1
@@ -281,7 +486,10 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   }
   __syncthreads();  // all waves done with the last stage: LDS becomes the epilogue staging area
 
-  big_epilogue<C::FM, C::FN, C::TM, C::TN>(p, acc, lds, bm, bn, wave, wm, wn, lane);
+  if constexpr (LNF)
+    big_epilogue_ln<C::FM, C::FN, C::TM, C::TN, C::WN, BM>(p, acc, lds, tm, tn, ntn, wave, wm, wn, lane, tid);
+  else
+    big_epilogue<C::FM, C::FN, C::TM, C::TN>(p, acc, lds, bm, bn, wave, wm, wn, lane);
 }
 
 // ---- ping-pong schedule: two wave groups offset by one barrier ------------------------------------------------
@@ -789,6 +997,35 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
 }
 
 
+// LayerNorm-fused residual linears: variant 14 = 192x256 tiles (N = 1024: the encoder's proj / fc2), 15 = 192x192
+// (N = 768: the transformer's) — the shapes' data-parallel tiles, with the LNF epilogue and the band-major grid.
+static int ln_bn(int variant) { return variant == 14 ? 256 : variant == 15 ? 192 : 0; }
+
+int64_t ln_stats_bytes(int M, int N, int variant) {
+  const int bn = ln_bn(variant);
+  if (!bn || N % bn) return -1;
+  return (int64_t)((M + 191) / 192) * (N / bn) * 192 * 8;
+}
+
+bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
+  const int bn = ln_bn(variant);
+  if (!bn || a.N % bn || a.lp_f16 || !a.ln_out || !a.ln_w || !a.ln_b || a.ln_ldo % 8 != 0) return false;
+  // the in-place residual pattern (epi_mode 2): out_f32 = resid1 + gamma * (acc + bias), row-major, nothing else
+  if (a.out_mode != 0 || !a.out_f32 || !a.resid1 || a.resid2 || a.out_lp || a.out_lp_relu || a.out_s3 ||
+      a.out_s3_relu || a.act != MAPA_ACT_NONE || a.ldo % 8 != 0 || !a.vec_ok)
+    return false;
+  const int ntm = (a.M + 191) / 192, ntn = a.N / bn;
+  if (2 * ntm >= LN_TICKET_WORDS || !ws || ws_bytes < GEMM_TICKET_BYTES + ln_stats_bytes(a.M, a.N, variant))
+    return false;
+  GemmArgs b = a;
+  b.ln_ctr = reinterpret_cast<int*>(ws) + (GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS);
+  b.ln_stats = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + GEMM_TICKET_BYTES);
+  void (*k)(GemmArgs) = variant == 14 ? gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, false, true>
+                                      : gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, false, true>;
+  hipLaunchKernelGGL(k, dim3(mapa_idx::lnf_grid(ntm, ntn)), dim3(BTHREADS), 0, stream, b);
+  return true;
+}
+
 // Stream-K variants: 0 = 256x128 / 64-B rows / 3 stages / setprio / 2 per CU, 1 = 256x256 / 64-B rows / 3 stages
 // / setprio / 1 per CU.  Workspace: [tickets: 64 Ki words][slabs: G * 2 * 256 * BN * 4].
 static int sk_cus() {
@@ -814,7 +1051,8 @@ int gemm_streamk_slots(int variant) {
 
 // Ticket words live in a fixed-size head shared by every shape (a shape-dependent split would let one shape's slabs
 // overwrite another's tickets, which must stay zero between calls); shapes with more tiles use the DP schedule.
-constexpr int64_t SK_MAX_TILES = GEMM_TICKET_BYTES / 4, SK_TICKET_BYTES = GEMM_TICKET_BYTES;
+// the top LN_TICKET_WORDS words of the head belong to the LayerNorm-fused GEMM (launch_gemm_big_ln)
+constexpr int64_t SK_MAX_TILES = GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS, SK_TICKET_BYTES = GEMM_TICKET_BYTES;
 
 int64_t streamk_workspace_bytes(int M, int N, int variant) {
   if (variant < 0 || variant > 2) return 0;

@@ -34,6 +34,15 @@ struct GemmArgs {
   int ps_s, ps_h, ps_w, ps_cout;
   int vec_ok;    // N % 4 == 0, ldo % 4 == 0, ps_cout % 4 == 0: 4-wide epilogue
   int lp_f16;    // 16-bit operands (A, W) and out_lp / out_lp_relu are fp16 (MAPA_F16) instead of bf16
+  int tile_gm;   // gemm_big_kernel tile order: groups of tile_gm tile rows per XCD range (mapa_idx::tile_coords_rt)
+  // fused LayerNorm of the output rows (mapa_gemm_desc.ln_*; launch_gemm_big_ln): weight / bias over N, bf16 output
+  const float* ln_w;
+  const float* ln_b;
+  float ln_eps;
+  void* ln_out;
+  int64_t ln_ldo;
+  int* ln_ctr;                   // [2 * bands] arrival / departure counters (zero between launches), then the flag
+  unsigned long long* ln_stats;  // [bands][ntn][BM] per-tile row statistics {sum, M2} (scratch)
 };
 
 using mapa_idx::group_coords;
@@ -349,6 +358,16 @@ __device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const Epi
 // 256-row bf16 kernel (gemm_big.hip): variant 0 = 256x256 tile, 1 = 256x128 tile.  Returns false if it does not
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
+
+// The in-place residual linear (epi_mode 2: out_f32 = resid1 + gamma * (acc + bias)) with the LayerNorm of its output
+// rows fused (gemm_big.hip, LNF): the row statistics combine across a band's column tiles inside the launch (band
+// barrier through the ticket head of the workspace), then every tile normalises its own rows into a.ln_out (bf16).
+// variant: 14 (192x256 tiles) or 15 (192x192).  Returns false if the shape / epilogue / workspace does not qualify.
+// Workspace: the GEMM ticket head (its top LN_TICKET_WORDS words: per-band arrival / departure counters and the
+// timeout flag) + ln_stats_bytes of per-tile row statistics.
+constexpr int LN_TICKET_WORDS = 16384;
+int64_t ln_stats_bytes(int M, int N, int variant);
+bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_bytes, hipStream_t stream);
 
 // Stride-1 3x3 conv with its A operand read from an LDS halo window (conv_halo.hip); bn = 256 / 128 / 0 (auto).
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).

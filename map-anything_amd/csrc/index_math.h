@@ -26,20 +26,45 @@ MAPA_HD int xcd_remap(int b, int nblk) {
 
 // Linear tile index t -> (tile row, tile col), walked in groups of GM tile-rows so the ~32 tiles an XCD runs at
 // once form a GM x (32/GM) patch: its A row-blocks and W column-blocks are re-read from that XCD's L2.
-template <int GM>
-MAPA_HD void group_coords(int t, int ntm, int ntn, int& tm, int& tn) {
-  const int group = t / (GM * ntn);
-  const int first = group * GM;
-  const int rows = imin(GM, ntm - first);
-  const int in = t - group * GM * ntn;
+MAPA_HD void group_coords_rt(int t, int gm, int ntm, int ntn, int& tm, int& tn) {
+  const int group = t / (gm * ntn);
+  const int first = group * gm;
+  const int rows = imin(gm, ntm - first);
+  const int in = t - group * gm * ntn;
   tm = first + in % rows;
   tn = in / rows;
+}
+template <int GM>
+MAPA_HD void group_coords(int t, int ntm, int ntn, int& tm, int& tn) {
+  group_coords_rt(t, GM, ntm, ntn, tm, tn);
 }
 
 // Output tile of workgroup b of a data-parallel GEMM grid of ntm * ntn tiles.
 template <int GM>
 MAPA_HD void tile_coords(int b, int ntm, int ntn, int& tm, int& tn) {
   group_coords<GM>(xcd_remap(b, ntm * ntn), ntm, ntn, tm, tn);
+}
+// The same with the group height chosen at run time (mapa_gemm_tune MAPA_TUNE_TILE_GROUP; gm >= 1).
+MAPA_HD void tile_coords_rt(int b, int gm, int ntm, int ntn, int& tm, int& tn) {
+  group_coords_rt(xcd_remap(b, ntm * ntn), gm, ntm, ntn, tm, tn);
+}
+
+// ---- LayerNorm-fused residual GEMM (gemm_big.hip, LNF): the row statistics of a LayerNorm over N combine across the
+// ntn column tiles of a tile row ("band") inside the launch, so every band's tiles must run together.  The bands are
+// dealt to the 8 XCDs in contiguous ranges and each XCD walks its bands band-major (a band's ntn tiles consecutive in
+// that XCD's dispatch order): a band never straddles XCDs, its A rows are fetched into one L2, and a band whose tiles
+// wait for each other is always the oldest incomplete one on its XCD.  Grid = lnf_grid blocks; the blocks past an
+// XCD's last band (XCDs with one band fewer) are idle.
+MAPA_HD int lnf_grid(int ntm, int ntn) { return 8 * ((ntm + 7) / 8) * ntn; }
+MAPA_HD bool lnf_coords(int b, int ntm, int ntn, int& tm, int& tn) {
+  const int x = b % 8, j = b / 8;
+  const int q = ntm / 8, r = ntm % 8;
+  const int lo = x * q + imin(x, r), cnt = q + (x < r ? 1 : 0);
+  const int band = j / ntn;
+  if (band >= cnt) return false;
+  tm = lo + band;
+  tn = j - band * ntn;
+  return true;
 }
 
 // ---- stream-K (gemm_big.hip gemm_sk_kernel): data-parallel whole tiles first, then K-iteration ranges

@@ -46,7 +46,8 @@ class GemmDesc(ctypes.Structure):
         ("out_mode", ctypes.c_int), ("ps_s", ctypes.c_int), ("ps_h", ctypes.c_int), ("ps_w", ctypes.c_int),
         ("ps_cout", ctypes.c_int), ("workspace", ctypes.c_void_p), ("workspace_bytes", ctypes.c_int64),
         ("out_s3", ctypes.c_void_p), ("out_s3_relu", ctypes.c_void_p), ("a_split", ctypes.c_int),
-        ("conv_kblock", ctypes.c_int),
+        ("conv_kblock", ctypes.c_int), ("ln_w", ctypes.c_void_p), ("ln_b", ctypes.c_void_p), ("ln_eps", ctypes.c_float),
+        ("ln_out", ctypes.c_void_p), ("ln_ldo", ctypes.c_int64),
     ]
 
 
@@ -230,6 +231,7 @@ def _toc(tok, kind, flops=0.0):
 # order, written at exit, so tools/profile_summary.py can name each rocprofv3 dispatch the way bench.py does (the
 # split-precision head GEMMs share kernel symbols with the plain ones).
 _LAUNCH_LOG = [] if os.environ.get("MAPA_LAUNCH_LOG") else None
+_LAUNCH_SHAPES = os.environ.get("MAPA_LAUNCH_SHAPES", "0") == "1"  # log "kind:shape" (profile_summary.py shapes)
 if _LAUNCH_LOG is not None:
     import atexit
     import json as _json
@@ -272,13 +274,15 @@ def attention_workspace(d) -> torch.Tensor:
     return ws
 
 
-TUNE_CONV_HALO, TUNE_TAIL_STREAMK, TUNE_HALO_SPLIT = 0, 1, 2
+TUNE_CONV_HALO, TUNE_TAIL_STREAMK, TUNE_HALO_SPLIT, TUNE_TILE_GROUP, TUNE_LN_FUSE = 0, 1, 2, 3, 4
 
 
 def gemm_tune(key: int, value: int):
     """A-B hooks of the automatic kernel choice (include/mapa.h mapa_gemm_tune): TUNE_CONV_HALO (stride-1 head convs
     on the LDS halo-window kernel, default on), TUNE_TAIL_STREAMK (tail-only stream-K for nearly empty last waves),
-    TUNE_HALO_SPLIT (K part count of the flat-raster halo conv, 0 = automatic)."""
+    TUNE_HALO_SPLIT (K part count of the flat-raster halo conv, 0 = automatic), TUNE_TILE_GROUP (tile rows per group
+    in the 256-row GEMM kernels' tile order, 0 = the default 4), TUNE_LN_FUSE (LayerNorm fused into the residual
+    linears where it qualifies, default 1)."""
     check(lib().mapa_gemm_tune(key, value), "mapa_gemm_tune")
     _WS_NEED.clear()
 
@@ -291,7 +295,7 @@ def gemm_set_variant(variant: int = 0):
 
 def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_NONE, resid1=None, resid2=None,
          out_f32=None, out_lp=None, out_lp_relu=None, out_s3=None, out_s3_relu=None, ldo=None, conv=None,
-         pixshuf=None, head_out=None):
+         pixshuf=None, head_out=None, ln=None):
     """C = A W^T with fused epilogue (see include/mapa.h). conv=(C, IH, IW, OH, OW, stride); pixshuf=(s, h, w, cout).
     out_s3 / out_s3_relu: split-precision operand outputs (bf16 [rows][2*ldo], [hi | lo]).  A weight packed for split
     operands (W._mapa_split, engine._split_pack) marks A as a compact split operand (mapa_gemm_desc.a_split): K is
@@ -299,7 +303,9 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     channel-block-major K order (mapa_gemm_desc.conv_kblock).
     head_out=(w6, b6, pose_out, scale, views_per_scale, pts3d, pts3d_cam, rays, depth, conf, logits, mask): the conv
     is the regressor's conv2 and its hidden map goes straight into the dense head (mapa_regressor_head_out; no other
-    outputs; image i uses scale[i // views_per_scale])."""
+    outputs; image i uses scale[i // views_per_scale]).
+    ln=(w, b, eps, out): the LayerNorm of out_f32's rows into out (the GEMM's 16-bit dtype; mapa_gemm_desc.ln_*), fused
+    into the residual linear where the library can (include/mapa.h)."""
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype
@@ -333,7 +339,12 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     if pixshuf is not None:
         d.out_mode = OUT_PIXSHUF
         d.ps_s, d.ps_h, d.ps_w, d.ps_cout = pixshuf
-    key = (d.dtype, M, N, K, d.a_mode, d.a_split, d.conv_kblock) + (tuple(conv) if conv is not None else ())
+    if ln is not None:
+        lw, lb, leps, lout = ln
+        d.ln_w, d.ln_b, d.ln_eps, d.ln_out, d.ln_ldo = lw.data_ptr(), lb.data_ptr(), float(leps), lout.data_ptr(), \
+            lout.stride(0)
+    key = (d.dtype, M, N, K, d.a_mode, d.a_split, d.conv_kblock, ln is not None) + \
+        (tuple(conv) if conv is not None else ())
     need = _WS_NEED.get(key)
     if need is None:
         need = _WS_NEED[key] = int(lib().mapa_gemm_workspace_bytes(ctypes.byref(d)))
@@ -351,7 +362,8 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops
     kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if split_a else "")
     if _LAUNCH_LOG is not None:
-        _LAUNCH_LOG.append(kind)
+        _LAUNCH_LOG.append(f"{kind}:{M}x{N}x{K}" + (f":{conv[1]}x{conv[2]}s{conv[5]}" if conv is not None else "")
+                           if _LAUNCH_SHAPES else kind)
     _toc(tok, kind, 2.0 * M * N * K)
 
 
@@ -379,7 +391,7 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
         for i, (st, ln) in enumerate(kv_segments):
             d.kv_seg_start[i], d.kv_seg_len[i] = st, ln
     if _LAUNCH_LOG is not None:
-        _LAUNCH_LOG.append(kind)
+        _LAUNCH_LOG.append(f"{kind}:{batch}x{heads}x{seq_q}x{seq_kv}" if _LAUNCH_SHAPES else kind)
     tok = _tic()
     check(lib().mapa_attention(ctypes.byref(d), stream()), "mapa_attention")
     _toc(tok, kind, 4.0 * batch * heads * seq_q * seq_kv * 64)

@@ -386,10 +386,25 @@ class MapaEngine:
         return OH, OW
 
     # ------------------------------------------------------------------------------------ transformer block
+    def _norm1(self, x, xn, rows, dim, p, normed):
+        """norm1 of a block into xn for the rows the previous block's fc2 did not already normalise (normed)."""
+        if normed < rows:
+            self._ln(x[normed:], rows - normed, dim, p["n1w"], p["n1b"], y_lp=xn[normed:])
+
+    @staticmethod
+    def _lnf(w, b, out):
+        """The LayerNorm that follows a residual linear, requested from that GEMM (mapa_gemm_desc.ln_*): fused into
+        its epilogue where the library can (bf16 residual linears on the 192-row tiles), else run right after it by
+        the library with the same kernel as _ln."""
+        return dict(ln=(w, b, LN_EPS, out))
+
     def _block(self, x, xn, qkv, ao, hbuf, rows, dim, heads, p, *, attn_batch, attn_seq, gamma=True,
-               attn_kind="attention", attn_scale=None):
-        lp = self.lp
-        self._ln(x, rows, dim, p["n1w"], p["n1b"], y_lp=xn)
+               attn_kind="attention", attn_scale=None, normed=0, next_ln=None):
+        """SelfAttentionBlock / NestedTensorBlock (dinov2 layers/block.py:93-118, transformer_blocks.py:452-469) on the
+        fp32 residual stream x.  norm2 comes out of the attention projection's GEMM and, with next_ln = the next
+        block's (norm1 weight, bias), that block's norm1 out of fc2's (xn); normed = leading rows of xn already
+        holding this block's norm1.  Returns the rows of xn normalised for the next block."""
+        self._norm1(x, xn, rows, dim, p, normed)
         nat.gemm(xn, p["qkv"], rows, 3 * dim, dim, bias=p["qkv_b"], out_lp=qkv)
         rs = 3 * dim
         nat.attention(qkv, qkv[:, dim:], qkv[:, 2 * dim:], ao, batch=attn_batch, heads=heads, seq_q=attn_seq,
@@ -397,11 +412,11 @@ class MapaEngine:
                       v_bstride=attn_seq * rs, v_rstride=rs, o_bstride=attn_seq * dim, o_rstride=dim, kind=attn_kind,
                       scale=attn_scale)
         nat.gemm(ao, p["proj"], rows, dim, dim, bias=p["proj_b"], gamma=p.get("ls1") if gamma else None,
-                 resid1=x, out_f32=x)
-        self._ln(x, rows, dim, p["n2w"], p["n2b"], y_lp=xn)
+                 resid1=x, out_f32=x, **self._lnf(p["n2w"], p["n2b"], xn))
         nat.gemm(xn, p["fc1"], rows, 4 * dim, dim, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
         nat.gemm(hbuf, p["fc2"], rows, dim, 4 * dim, bias=p["fc2_b"], gamma=p.get("ls2") if gamma else None,
-                 resid1=x, out_f32=x)
+                 resid1=x, out_f32=x, **(self._lnf(*next_ln, xn) if next_ln is not None else {}))
+        return rows if next_ln is not None else 0
 
     # ------------------------------------------------------------------------------------------- encoder
     def encode(self, imgs, taps=None, geo: Optional[GeoInputs] = None, scenes: int = 1):
@@ -448,8 +463,11 @@ class MapaEngine:
         del pe_out, patches
         xn, qkv, ao = self._empty(R, ENC_DIM), self._empty(R, 3 * ENC_DIM), self._empty(R, ENC_DIM)
         hbuf = self._empty(R, 4 * ENC_DIM)
-        for p in w.enc:
-            self._block(x, xn, qkv, ao, hbuf, R, ENC_DIM, ENC_HEADS, p, attn_batch=VB, attn_seq=T + 1)
+        normed = 0
+        for i, p in enumerate(w.enc):
+            nxt = w.enc[i + 1] if i + 1 < len(w.enc) else None
+            normed = self._block(x, xn, qkv, ao, hbuf, R, ENC_DIM, ENC_HEADS, p, attn_batch=VB, attn_seq=T + 1,
+                                 normed=normed, next_ln=None if nxt is None else (nxt["n1w"], nxt["n1b"]))
         del xn, qkv, ao, hbuf
         enc = self._empty(VB * T, ENC_DIM, dtype=torch.float32)
         self._ln(x, VB * T, ENC_DIM, w.enc_nw, w.enc_nb, y_f32=enc, group=T, gstride=T + 1, off=1)
@@ -627,18 +645,23 @@ class MapaEngine:
             kv_full = self._empty(shard.world * shard.max_rows, 2 * D)
             q_loc = self._empty(L, D)
         inter = {}
+        normed = 0  # leading rows of yn already holding the current block's norm1 (fused into the last fc2)
         for d, p in enumerate(w.aat):
+            nxt = w.aat[d + 1] if d + 1 < len(w.aat) else None
+            nln = None if nxt is None else (nxt["n1w"], nxt["n1b"])
             if info.is_global(d):   # global attention over every view + the scale token
                 if shard is None and B == 1:
-                    self._block(y, yn, qkv, ao, hbuf, L, D, NH, p, attn_batch=1, attn_seq=L, gamma=False,
-                                attn_kind="attention_global", attn_scale=g_scale)
+                    normed = self._block(y, yn, qkv, ao, hbuf, L, D, NH, p, attn_batch=1, attn_seq=L, gamma=False,
+                                         attn_kind="attention_global", attn_scale=g_scale, normed=normed,
+                                         next_ln=nln)
                 elif shard is None:
-                    self._block_global_scenes(y, yn, qkv, ao, hbuf, L, p, B, V, T, g_scale)
+                    normed = self._block_global_scenes(y, yn, qkv, ao, hbuf, L, p, B, V, T, g_scale, normed, nln)
                 else:
-                    self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, g_scale)
+                    normed = self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, g_scale,
+                                                        normed, nln)
             else:                   # frame attention inside each view; the scale token bypasses the block
-                self._block(y, yn, qkv, ao, hbuf, VB * T, D, NH, p, attn_batch=VB, attn_seq=T,
-                            gamma=False, attn_scale=f_scale)
+                normed = self._block(y, yn, qkv, ao, hbuf, VB * T, D, NH, p, attn_batch=VB, attn_seq=T,
+                                     gamma=False, attn_scale=f_scale, normed=normed, next_ln=nln)
             if d in info.indices:  # IFR taps feed only the DPT (a head: fp32 in the reference, model.py:1774)
                 t_lp = self._hop(VB * T, D)
                 t_f = self._empty(VB * T, D, dtype=torch.float32) if taps is not None else None
@@ -670,13 +693,13 @@ class MapaEngine:
             self._ones_buf = o
         return o
 
-    def _block_global_scenes(self, y, yn, qkv, ao, hbuf, L, p, B, V, T, scale=None):
+    def _block_global_scenes(self, y, yn, qkv, ao, hbuf, L, p, B, V, T, scale=None, normed=0, next_ln=None):
         """Global SelfAttentionBlock of B batched scenes (rows [image][token] scene-major, then the B scale tokens):
         LayerNorm / GEMMs over all rows at once; per scene one attention of its token rows and one of its scale-token
         row, both over the scene's keys through the segment table (its V*T token rows + its scale-token row)."""
         C, NH = self.info.dim, self.info.heads
         rs = 3 * C
-        self._ln(y, L, C, p["n1w"], p["n1b"], y_lp=yn)
+        self._norm1(y, yn, L, C, p, normed)
         nat.gemm(yn, p["qkv"], L, rs, C, bias=p["qkv_b"], out_lp=qkv)
         k, v = qkv[:, C:], qkv[:, 2 * C:]
         kw = dict(batch=1, heads=NH, q_bstride=0, q_rstride=rs, k_bstride=0, k_rstride=rs, v_bstride=0, v_rstride=rs,
@@ -686,18 +709,20 @@ class MapaEngine:
             segs = [(r0, V * T), (tok, 1)]
             nat.attention(qkv[r0:], k, v, ao[r0:], seq_q=V * T, seq_kv=V * T + 1, kv_segments=segs, **kw)
             nat.attention(qkv[tok:], k, v, ao[tok:], seq_q=1, seq_kv=V * T + 1, kv_segments=segs, **kw)
-        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
-        self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)
+        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y, **self._lnf(p["n2w"], p["n2b"], yn))
         nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
-        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y)
+        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y,
+                 **(self._lnf(*next_ln, yn) if next_ln is not None else {}))
+        return L if next_ln is not None else 0
 
-    def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, scale=None):
+    def _block_global_sharded(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, scale=None, normed=0,
+                              next_ln=None):
         """Global SelfAttentionBlock on a view shard: Q for the local rows, K/V of all ranks (one all-gather).
         The all-gather runs on the communicator's stream while the local queries attend to this rank's own keys;
         the remote-key partial follows the gather and the two partials are merged through their LSEs
         (MAPA_KV_OVERLAP=0: gather first, one attention over every key)."""
         C, NH = self.info.dim, self.info.heads
-        self._ln(y, L, C, p["n1w"], p["n1b"], y_lp=yn)
+        self._norm1(y, yn, L, C, p, normed)
         nat.gemm(yn, p["qkv"][:C], L, C, C, bias=p["qkv_b"][:C], out_lp=q_loc)
         slot = kv_full[shard.rank * shard.max_rows:]
         nat.gemm(yn, p["qkv"][C:], L, 2 * C, C, bias=p["qkv_b"][C:], out_lp=slot, ldo=2 * C)
@@ -725,10 +750,11 @@ class MapaEngine:
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao_r, seq_kv=sum(sg[1] for sg in rest), kv_segments=rest,
                           lse=lse_r, kind="attention_global", **strides)
             nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, NH, C)
-        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y)
-        self._ln(y, L, C, p["n2w"], p["n2b"], y_lp=yn)
+        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y, **self._lnf(p["n2w"], p["n2b"], yn))
         nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
-        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y)
+        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y,
+                 **(self._lnf(*next_ln, yn) if next_ln is not None else {}))
+        return L if next_ln is not None else 0
 
     # ----------------------------------------------------------------------------------------------- DPT
     def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None, head=None):

@@ -492,6 +492,10 @@ class MapAnything:
                             static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
                     except Exception as e:  # noqa: BLE001 -- any capture failure: agree, then run eager
                         err = e
+                        if os.environ.get("MAPA_GRAPH_DEBUG"):
+                            import traceback
+                            traceback.print_exc()
+                            raise
                     if not self._comm.all_agree(err is None, imgs.device):
                         warnings.warn(f"sharded HIP-graph capture failed ({err or 'on another rank'}); "
                                       "running the sharded path eagerly")

@@ -119,6 +119,54 @@ def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
         assert ws.numel() > 0 and int(ws[: 4 * 65536].count_nonzero()) == 0
 
 
+def _ln_flag(nat):
+    """Band-barrier timeout flags of the GEMM workspaces (include/mapa.h: int word 65535 of the head)."""
+    ws = list(nat._WS.values()) + nat._WS_RETIRED
+    return sum(int(w.view(torch.int32)[65535].item()) for w in ws if w.numel() >= 262144)
+
+
+# (M, N, K, gamma): the path's residual linears at 8 views (enc proj / fc2 on 192x256 tiles, aat proj / fc2 on
+# 192x192), a one-band problem, a ragged last band, and B = 2 scenes (more tiles than CUs: fused only if the 192-row
+# tile is still the automatic choice, else the library's GEMM + LayerNorm)
+@pytest.mark.parametrize("M,N,K,gamma", [(10960, 1024, 1024, True), (10960, 1024, 4096, True), (10953, 768, 768, False),
+                                         (10953, 768, 3072, False), (150, 768, 768, False), (4001, 1024, 1024, True),
+                                         (21905, 768, 3072, False)])
+def test_gemm_layernorm_fused(nat, M, N, K, gamma):
+    """mapa_gemm with ln_out (the next sub-block's LayerNorm fused into the residual linear): the fp32 residual
+    stream bitwise equal to the plain GEMM's, the bf16 normalised rows within one bf16 rounding of the standalone
+    two-pass LayerNorm of that stream (mapa_layernorm) and of torch's fp32 LayerNorm, repeatable bit for bit, and no
+    band barrier timed out.  MAPA_TUNE_LN_FUSE=0 (GEMM, then LayerNorm) is the A side."""
+    A = _rand(M, K, seed=61).to(torch.bfloat16)
+    W = _rand(N, K, scale=K ** -0.5, seed=62).to(torch.bfloat16)
+    b = _rand(N, seed=63)
+    g = _rand(N, scale=0.1, seed=64) if gamma else None
+    x0 = _rand(M, N, seed=65) + 3.0 * _rand(1, N, seed=66)  # per-channel offsets, as the residual stream carries
+    lw, lb = 1.0 + 0.2 * _rand(N, seed=67), 0.1 * _rand(N, seed=68)
+
+    def run(fuse):
+        nat.gemm_tune(nat.TUNE_LN_FUSE, fuse)
+        x = x0.clone()
+        y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=x, out_f32=x, ln=(lw, lb, 1e-6, y))
+        torch.cuda.synchronize()
+        return x, y
+    try:
+        xs, ys = run(0)
+        xf, yf = run(1)
+        xf2, yf2 = run(1)
+    finally:
+        nat.gemm_tune(nat.TUNE_LN_FUSE, 1)
+    assert _ln_flag(nat) == 0
+    assert torch.equal(xf, xs) and torch.equal(xf2, xf) and torch.equal(yf2, yf)
+    assert not torch.isnan(yf.float()).any()
+    ref = F.layer_norm(xs, (N,), lw, lb, 1e-6)
+    ulp = ref.abs().clamp_min(1e-3) * 2.0 ** -7  # one bf16 rounding (8 significant bits)
+    for y in (ys, yf):
+        assert ((y.float() - ref).abs() <= ulp).all()
+    diff = (yf.float() != ys.float()).float().mean().item()
+    assert diff < 1e-3, diff  # statistics rounded differently flip at most a few bf16 roundings
+
+
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574])
 def test_conv3x3_big_variants(nat, variant):
     n, H, W, C, Co = 2, 37, 37, 256, 256

@@ -1,4 +1,4 @@
-# Round-3 profile set (run on the GPU box; summarised on the CPU by tools/profile_round.sh <round>):
+# Per-round profile set (run on the GPU box; summarised on the CPU by tools/profile_round.sh <round>):
 #   1. the driver's bench command under rocprofv3 --kernel-trace --stats (graph replay, the production path)
 #   2. the same bench eager (MAPA_HIP_GRAPHS=0) with a launch log -> per-kind trace (split GEMMs named apart)
 #   3. PMC passes, each its own run: FETCH_SIZE, WRITE_SIZE, SQ MFMA-busy (+ launch logs)
@@ -14,7 +14,7 @@ if [[ $PART == *1* ]]; then
 timeout -k 10 700 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_rocprof.json 2> gpurun_out/rocprof.err || { tail -20 gpurun_out/rocprof.err; exit 1; }
 export MAPA_HIP_GRAPHS=0
 S="--steps 2 --warmup 1 --no-kernel-timing"
-MAPA_LAUNCH_LOG=gpurun_out/prof_e/launch_log.json timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/prof_e -o run --output-format csv -- $B $S > gpurun_out/prof_e.log 2>&1 || { tail -20 gpurun_out/prof_e.log; exit 1; }
+MAPA_LAUNCH_SHAPES=1 MAPA_LAUNCH_LOG=gpurun_out/prof_e/launch_log.json timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/prof_e -o run --output-format csv -- $B $S > gpurun_out/prof_e.log 2>&1 || { tail -20 gpurun_out/prof_e.log; exit 1; }
 fi
 if [[ $PART == *2* ]]; then
 export MAPA_HIP_GRAPHS=0

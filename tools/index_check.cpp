@@ -4,7 +4,8 @@
 // of the MapAnything path (8 / 100 / 250-view encoder, transformer and head GEMMs, attention layouts up to the
 // 2 738 001-key configs[4] layer) plus randomised ones:
 //   * xcd_remap is a bijection of [0, nblk);
-//   * tile_coords<GM> visits every output tile of a grid exactly once, in range;
+//   * tile_coords<GM> visits every output tile of a grid exactly once, in range; the LayerNorm-fused grid
+//     (lnf_coords) too, with each band's tiles on one XCD at consecutive dispatch positions;
 //   * stream-K: every (tile, k) iteration is computed by exactly one block, the blocks touching a split tile are
 //     exactly sk_contributors' range, slab slots stay inside the g slab pairs of the workspace, the grid fits g;
 //   * attention: every task's K/V tile range [0, nkt) is covered exactly once by its chunks, chunks are non-empty,
@@ -54,6 +55,27 @@ static void check_tiles(int ntm, int ntn) {
     REQUIRE(!s, "GM %d grid %dx%d: tile (%d,%d) twice", GM, ntm, ntn, tm, tn);
     s = 1;
   }
+}
+
+// LayerNorm-fused grid: every tile exactly once; a band's ntn tiles on one XCD (block % 8) at consecutive positions
+// of that XCD's dispatch order (block / 8); the blocks past an XCD's bands are idle.
+static void check_lnf(int ntm, int ntn) {
+  std::vector<int> owner((size_t)ntm * ntn, -1);
+  const int grid = lnf_grid(ntm, ntn);
+  for (int b = 0; b < grid; ++b) {
+    int tm, tn;
+    if (!lnf_coords(b, ntm, ntn, tm, tn)) continue;
+    REQUIRE(tm >= 0 && tm < ntm && tn >= 0 && tn < ntn, "lnf %dx%d b %d -> (%d,%d)", ntm, ntn, b, tm, tn);
+    int& o = owner[(size_t)tm * ntn + tn];
+    REQUIRE(o < 0, "lnf %dx%d: tile (%d,%d) twice", ntm, ntn, tm, tn);
+    o = b;
+  }
+  for (int tm = 0; tm < ntm; ++tm)
+    for (int tn = 0; tn < ntn; ++tn) {
+      const int b = owner[(size_t)tm * ntn + tn], b0 = owner[(size_t)tm * ntn];
+      REQUIRE(b >= 0, "lnf %dx%d: tile (%d,%d) never visited", ntm, ntn, tm, tn);
+      REQUIRE(b % 8 == b0 % 8 && b / 8 == b0 / 8 + tn, "lnf %dx%d: band %d not consecutive on one XCD", ntm, ntn, tm);
+    }
 }
 
 static void check_streamk(int64_t tiles, int nk, int g, bool tail, bool dp, int per_env) {
@@ -206,7 +228,10 @@ int main() {
     for (int ntn = 1; ntn <= 40; ++ntn) {
       check_tiles<4>(ntm, ntn);
       check_tiles<8>(ntm, ntn);
+      check_lnf(ntm, ntn);
     }
+  for (int M : rows)
+    for (int ntn : {3, 4, 5, 6, 8}) check_lnf((M + 191) / 192, ntn);
 
   // stream-K: the head convs (M = views * pixels, K = 9 * 3C logical split columns / 32-deep steps) + random
   const int sk_g[] = {256, 512, 1024};

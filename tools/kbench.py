@@ -1,7 +1,8 @@
 """Kernel micro-benchmark: TFLOP/s of the hot GEMM / conv / attention shapes of the 8-view 518x518 workload
 (HIP-event timing, random data).  Usage: python tools/kbench.py [gemm|attn|conv|all] [reps]
 KB_VARIANTS=0,2580,2568 sweeps GEMM/conv kernel variants (0 = the automatic choice; include/mapa.h); KB_KBLOCK=0,32 runs
-the convs in the tap-major and the channel-block-major K order (interleaved)."""
+the convs in the tap-major and the channel-block-major K order (interleaved); KB_GM=2,4,8 sweeps the 256-row GEMM
+kernels' tile-group height (mapa_gemm_tune MAPA_TUNE_TILE_GROUP, interleaved with the variants)."""
 import os
 import sys
 
@@ -26,6 +27,7 @@ if os.environ.get("KB_SHAPES"):  # "M,N,K;M,N,K" ad-hoc GEMM shapes
              for m, n, k in (t.split(",") for t in os.environ["KB_SHAPES"].split(";"))]
 ONLY = os.environ.get("KB_ONLY")
 VARIANTS = [int(v) for v in os.environ.get("KB_VARIANTS", "0").split(",")]
+GMS = [int(v) for v in os.environ.get("KB_GM", "0").split(",")]
 if ONLY:
     GEMMS = [g for g in GEMMS if g[0] in ONLY.split(",")]
 CONVS = [("rn1.c@148", V, 148, 148, 256, 256), ("reg.c2@518", V, 518, 518, 128, 128),
@@ -84,9 +86,10 @@ def main():
             gam = torch.randn(N, device="cuda") * 0.1 if resid else None
             gelu = name.endswith("fc1") and not os.environ.get("KB_NO_RESID")  # the MLP's first linear: GELU epilogue
 
-            def run(var):
+            def run(var, gm=0):
                 def f():
                     nat.gemm_set_variant(var)
+                    nat.gemm_tune(nat.TUNE_TILE_GROUP, gm)
                     if resid:
                         nat.gemm(A, W, M, N, K, bias=b, gamma=gam, resid1=x, out_f32=x)
                     elif gelu:
@@ -94,13 +97,16 @@ def main():
                     else:
                         nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
                 return f
-            fns = [run(v) for v in VARIANTS]
+            combos = [(v, g) for v in VARIANTS for g in GMS]
+            fns = [run(v, g) for v, g in combos]
             if "torch" in sys.argv:
                 fns.append(lambda: torch.nn.functional.linear(A, W, b.to(dt)))
             mss = interleaved(fns, reps)
-            for var, ms in zip(VARIANTS, mss):
-                print(f"gemm {name:10s} v{var:<4d} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s",
+            for (var, gm), ms in zip(combos, mss):
+                tag = f" gm{gm}" if len(GMS) > 1 else ""
+                print(f"gemm {name:10s} v{var:<4d}{tag} M={M} N={N} K={K}: {ms*1e3:8.1f} us  {2*M*N*K/ms/1e9:7.1f} TF/s",
                       flush=True)
+            nat.gemm_tune(nat.TUNE_TILE_GROUP, 0)
             if "torch" in sys.argv:
                 print(f"gemm {name:10s} hipBLASLt via torch: {mss[-1]*1e3:8.1f} us  {2*M*N*K/mss[-1]/1e9:7.1f} TF/s",
                       flush=True)

@@ -5,6 +5,8 @@
   python tools/profile_summary.py mfma <kernel-regex> <pmc.csv>...           -> MFMA-pipe utilisation at the real clock
   python tools/profile_summary.py mfma_groups <pmc.csv> [launch_log.json]   -> the same per kernel group (bench run)
   python tools/profile_summary.py kinds <kernel_trace.csv> <launch_log.json> -> per bench.py kind (calls / avg / total)
+  python tools/profile_summary.py shapes <kernel_trace.csv> <launch_log.json> -> per kind and problem shape (a log
+                                                                               written with MAPA_LAUNCH_SHAPES=1)
   python tools/profile_summary.py headline <kernel_trace.csv> <bench.json>   -> groups over the headline infers only
 
 With a launch log (MAPA_LAUNCH_LOG, mapanything/_native.py) every GEMM / attention dispatch is named exactly as
@@ -44,9 +46,13 @@ def _is_gemm(name):
         "gemm_pp_kernel" in name or "conv_halo_kernel" in name
 
 
-def dispatch_kinds(names, log_path):
-    """names: kernel names of the dispatches in order -> the bench kind of each (None for other kernels)."""
+def dispatch_kinds(names, log_path, keep_shape=False):
+    """names: kernel names of the dispatches in order -> the bench kind of each (None for other kernels).  Log
+    entries written with MAPA_LAUNCH_SHAPES=1 carry the problem shape after a colon ("gemm:10960x3072x1024");
+    keep_shape keeps it, otherwise only the kind is returned."""
     log = json.load(open(log_path))
+    if not keep_shape:
+        log = [k.split(":")[0] for k in log]
     g_log = [k for k in log if k.startswith(("gemm", "conv3x3"))]
     a_log = [k for k in log if k.startswith("attention")]
     gi = ai = 0
@@ -65,10 +71,10 @@ def dispatch_kinds(names, log_path):
     return out
 
 
-def kinds(trace_csv, log_path):
+def kinds(trace_csv, log_path, keep_shape=False):
     rows = list(csv.DictReader(open(trace_csv)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ks = dispatch_kinds([r["Kernel_Name"] for r in rows], log_path)
+    ks = dispatch_kinds([r["Kernel_Name"] for r in rows], log_path, keep_shape)
     g = defaultdict(lambda: {"calls": 0, "total_ns": 0.0})
     for r, k in zip(rows, ks):
         k = k or group(r["Kernel_Name"])
@@ -231,5 +237,8 @@ if __name__ == "__main__":
         print(json.dumps(headline(a[2], a[3]), indent=1))
     elif a[1] == "kinds":
         print(json.dumps(kinds(a[2], a[3]), indent=1))
+    elif a[1] == "shapes":
+        per = kinds(a[2], a[3], keep_shape=True)
+        print(json.dumps(dict(sorted(per.items(), key=lambda kv: -kv[1]["total_ns"])), indent=1))
     else:
         print(json.dumps(traffic(a[2], a[3], *(a[4:6] if len(a) > 5 else (None, None))), indent=1))
