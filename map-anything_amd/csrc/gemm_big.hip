@@ -135,12 +135,14 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& p, f32x4 (&acc)[FM]
 // The in-place residual pattern of epi_mode 2 (out_f32 = resid1 + gamma * (acc + bias): the arithmetic of
 // epi_store_row8_mode<2>), then nn.LayerNorm over each output row, whose N columns are the band's ntn tiles
 // (dinov2 layers/block.py:93-118 norm1 / norm2, transformer_blocks.py:452-469):
-//  1. every lane keeps its 8-column row segments of the new residual in registers (FM/2 parts x 4 passes);
+//  1. every lane computes its 8-column row segments of the new residual and keeps them in registers (FM/2 parts x
+//     4 passes);
 //  2. per tile row: the sum over the tile's columns (8-lane butterfly, then the WN column waves' partials in LDS in
 //     wave order), the tile mean, then M2 = sum (v - mean_t)^2 the same way (two-pass inside the tile);
 //  3. {sum, M2} of every row published as one 8-byte write-through granule per tile (agent-scope relaxed store),
-//     every storing wave drains (vmcnt 0), then one arrival on the band's counter; one lane polls the counter until
-//     the band's ntn tiles arrived (bounded: past LN_SPIN_LIMIT polls it sets the flag word and proceeds);
+//     every storing wave drains (vmcnt 0: the residual loads and the granules only), then one arrival on the band's
+//     counter; the new residual rows are stored to out_f32 only now, so they drain while one lane polls the counter
+//     until the band's ntn tiles arrived (bounded: past LN_SPIN_LIMIT polls it sets the flag word and proceeds);
 //  4. per row, from the ntn granules read write-through in column order (the same value in every tile of the band):
 //     mean = sum / N, M2 = sum_t (M2_t + n_t (mean_t - mean)^2) (Chan's merge, exact up to rounding), rstd =
 //     rsqrt(M2 / N + eps);
@@ -204,11 +206,9 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
         }
         v0 += *reinterpret_cast<const f32x4*>(p.resid1 + off);
         v1 += *reinterpret_cast<const f32x4*>(p.resid1 + off + 4);
-        *reinterpret_cast<f32x4*>(p.out_f32 + off) = v0;
-        *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = v1;
       }
-      keep[part][pass][0] = v0;
-      keep[part][pass][1] = v1;
+      keep[part][pass][0] = v0;  // stored to out_f32 after the band's arrival (step 3): the publish drain must not
+      keep[part][pass][1] = v1;  // wait for the residual stream's stores
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -271,8 +271,20 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through granules
   __syncthreads();
+  if (tid == 0) __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the new residual stream (epi_mode 2's out_f32), issued now so its stores drain while the band gathers
+#pragma unroll
+  for (int part = 0; part < NP; ++part)
+#pragma unroll
+    for (int pass = 0; pass < 4; ++pass) {
+      const int m = bm + wm * TM + part * 32 + pass * 8 + (lane >> 3);
+      if (col_ok && m < p.M) {
+        const int64_t off = (int64_t)m * p.ldo + n0;
+        *reinterpret_cast<f32x4*>(p.out_f32 + off) = keep[part][pass][0];
+        *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = keep[part][pass][1];
+      }
+    }
   if (tid == 0) {
-    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     unsigned spins = 0;
     while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntn) {
       __builtin_amdgcn_s_sleep(2);

@@ -359,8 +359,10 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
               "mapa_regressor_head_out")
     else:
         check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
-    # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops
-    kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if split_a else "")
+    # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops; residual
+    # linears with their output LayerNorm (ln=) too ("gemm_ln": the GEMM flops over the fused launch's time)
+    kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if split_a else "") + \
+        ("_ln" if ln is not None else "")
     if _LAUNCH_LOG is not None:
         _LAUNCH_LOG.append(f"{kind}:{M}x{N}x{K}" + (f":{conv[1]}x{conv[2]}s{conv[5]}" if conv is not None else "")
                            if _LAUNCH_SHAPES else kind)

@@ -113,8 +113,9 @@ class MapAnything:
         # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
         self.hip_graphs = hip_graphs and os.environ.get("MAPA_HIP_GRAPHS", "1") != "0"
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
-        # sharded capture: off with MAPA_SHARD_GRAPHS=0, or on every rank once any rank's capture has failed
-        self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "1") != "0"
+        # sharded capture (RCCL collectives inside the HIP graph): opt-in with MAPA_SHARD_GRAPHS=1 until it has run on
+        # the hardware; off on every rank once any rank's capture has failed
+        self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "0") == "1"
         self._modules: Dict[str, Any] = {}
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)
@@ -298,11 +299,17 @@ class MapAnything:
         gather_outputs: None -> the returned list holds this rank's views' outputs and None for the others;
         "rank0" -> rank 0 returns every view's outputs, as the reference's infer does (model.py:2266-2282), the
         other ranks their own views'; "all" -> every rank returns every view's outputs."""
-        from ...parallel import DistComm
+        import torch.distributed as dist
+
+        from ...parallel import DistComm, RcclComm
 
         if gather_outputs not in (None, "rank0", "all"):
             raise ValueError(f"gather_outputs must be None, 'rank0' or 'all', got {gather_outputs!r}")
-        self._comm = comm if comm is not None else DistComm(group)
+        if comm is None:
+            # an RCCL group with sharded HIP graphs on: the collectives go to RCCL directly (capturable)
+            rccl = self._shard_graphs and dist.get_backend(group) == "nccl"
+            comm = RcclComm(group, self._device if self._device.type == "cuda" else None) if rccl else DistComm(group)
+        self._comm = comm
         self._gather = gather_outputs
         return self
 

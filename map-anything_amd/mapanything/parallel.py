@@ -122,9 +122,9 @@ class DistComm:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        # RCCL collectives are enqueued on the device and can be captured into a HIP graph (fork / join with the
-        # communicator's stream); gloo's run on the host
-        self.graph_safe = dist.get_backend(group) == "nccl"
+        # ProcessGroupNCCL's collectives cannot be captured into a HIP graph (its watchdog polls the captured work's
+        # events; rccl.py): the captured sharded forward uses RcclComm instead
+        self.graph_safe = False
 
     def _call(self, what, fn, *a, **k):
         """Run one collective; a backend error (gloo raises on a dead peer / timeout, RCCL's watchdog on a timed-out
@@ -184,6 +184,53 @@ class DistComm:
                 return None
             full = torch.cat(lst, 0)
         return torch.cat([full[r * mx:r * mx + c] for r, c in enumerate(counts)], 0)
+
+
+class RcclComm(DistComm):
+    """DistComm whose device-side collectives (the per-global-layer K/V all-gather, the scale-token broadcast) go to
+    RCCL directly on a communicator of its own (mapanything/rccl.py), so they can be captured with the kernels into
+    the sharded forward's HIP graph; the host-side ones (output gather, the capture agreement) stay on the process
+    group.  The overlapped all-gather runs on a side stream forked from and joined back into the caller's stream
+    (event record / wait: captured as graph edges).  An RCCL error raises CommError; a collective that never
+    completes is not timed out here (no watchdog over captured work) — MAPA_SHARD_GRAPHS=0 keeps the process group's
+    eager, watchdog-timed path."""
+
+    graph_safe = True
+
+    def __init__(self, group=None, device=None):
+        super().__init__(group)
+        from . import rccl
+
+        self._rccl_mod = rccl
+        try:
+            self._nccl = rccl.Communicator(group, device)
+        except Exception as e:  # noqa: BLE001 — init failures become CommError like the process group's
+            raise CommError(f"RCCL communicator init failed on rank {self.rank} of {self.world}: {e}") from e
+        self._side = torch.cuda.Stream(self._nccl.device)
+
+    def _rc(self, what, fn, *a):
+        try:
+            fn(*a)
+        except self._rccl_mod.RcclError as e:
+            raise CommError(f"{what} failed on rank {self.rank} of {self.world}: {e}") from e
+
+    def allgather_slots(self, full: torch.Tensor, rows_per_slot: int):
+        self._rc("K/V all-gather", self._nccl.all_gather_, full, rows_per_slot, torch.cuda.current_stream())
+
+    def allgather_slots_async(self, full: torch.Tensor, rows_per_slot: int):
+        cur = torch.cuda.current_stream()
+        side = self._side
+        side.wait_stream(cur)  # the K/V projection into this rank's slot is done
+        self._rc("K/V all-gather", self._nccl.all_gather_, full, rows_per_slot, side)
+
+        class _Handle:
+            def wait(self_inner):
+                cur.wait_stream(side)
+
+        return _Handle()
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        self._rc("scale-token broadcast", self._nccl.broadcast_, t, src, torch.cuda.current_stream())
 
 
 class ThreadComm:

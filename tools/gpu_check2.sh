@@ -16,7 +16,7 @@ step lnf_tests timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeo
 tail -3 gpurun_out/lnf_tests.log
 step nccl_dbg env MAPA_GRAPH_DEBUG=1 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 --master-port=29733 tests/nccl1_worker.py gpurun_out/nccl1.json
 grep -v "^\[rank0\]:\[W" gpurun_out/nccl_dbg.log | grep -B2 -A25 "Traceback" | head -60
-step gpu_tests timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread --deselect tests/test_gpu_distcomm.py::test_one_rank_rccl_sharded_graph
+step gpu_tests timeout -k 10 900 python -u -m pytest tests -m gpu -q -s --timeout 300 --timeout-method thread --deselect tests/test_gpu_distcomm.py::test_one_rank_rccl_sharded_graph
 grep -E "passed|failed|FAILED|Error" gpurun_out/gpu_tests.log | tail -12
 step smoke timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()"
 tail -1 gpurun_out/smoke.log

@@ -10,7 +10,7 @@
   python tools/profile_summary.py headline <kernel_trace.csv> <bench.json>   -> groups over the headline infers only
 
 With a launch log (MAPA_LAUNCH_LOG, mapanything/_native.py) every GEMM / attention dispatch is named exactly as
-bench.py names it ("gemm", "gemm_split", "conv3x3", "conv3x3_split", "attention", "attention_global"): the n-th
+bench.py names it ("gemm", "gemm_ln", "gemm_split", "conv3x3", "conv3x3_split", "attention", "attention_global"): the n-th
 GEMM-kernel dispatch of the trace is the n-th GEMM call of the log (one dispatch per mapa_gemm call), the n-th
 attn_fwd dispatch the n-th attention call.
 
