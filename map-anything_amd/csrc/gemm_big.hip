@@ -151,6 +151,7 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& p, f32x4 (&acc)[FM]
 // Equal to the standalone two-pass LayerNorm (norm.hip) up to the fp32 rounding of the statistics.  The launch needs
 // N % BN == 0 (every tile holds BN columns of a row) and the row-major in-place residual outputs (epi_mode 2).
 constexpr unsigned LN_SPIN_LIMIT = 1u << 22;
+constexpr int LN_MAX_NTN = 8;  // column tiles per band the merge holds in registers (launch_gemm_big_ln checks)
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
 
@@ -298,18 +299,23 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the granule loads below the poll
   // 4. merge the band's statistics (write-through loads, tiles in column order)
   if (tid < BM) {
+    // every granule of the row in flight at once (one fabric round trip), then merged in column order
+    unsigned long long gv[LN_MAX_NTN];
+#pragma unroll
+    for (int t = 0; t < LN_MAX_NTN; ++t)
+      gv[t] = t < ntn ? __hip_atomic_load(stats + t * BM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     float sum = 0.f;
-    for (int t = 0; t < ntn; ++t) {
-      const unsigned long long gv = __hip_atomic_load(stats + t * BM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sum += __uint_as_float((unsigned)gv);
-    }
+#pragma unroll
+    for (int t = 0; t < LN_MAX_NTN; ++t)
+      if (t < ntn) sum += __uint_as_float((unsigned)gv[t]);
     const float mean = sum / (float)p.N;
     float m2 = 0.f;
-    for (int t = 0; t < ntn; ++t) {
-      const unsigned long long gv = __hip_atomic_load(stats + t * BM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float d = __uint_as_float((unsigned)gv) * (1.f / BN) - mean;
-      m2 += __uint_as_float((unsigned)(gv >> 32)) + (float)BN * d * d;
-    }
+#pragma unroll
+    for (int t = 0; t < LN_MAX_NTN; ++t)
+      if (t < ntn) {
+        const float d = __uint_as_float((unsigned)gv[t]) * (1.f / BN) - mean;
+        m2 += __uint_as_float((unsigned)(gv[t] >> 32)) + (float)BN * d * d;
+      }
     rmean[tid] = mean;
     rrstd[tid] = rsqrtf(m2 / (float)p.N + p.ln_eps);
   }
@@ -1027,7 +1033,7 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
       a.out_s3_relu || a.act != MAPA_ACT_NONE || a.ldo % 8 != 0 || !a.vec_ok)
     return false;
   const int ntm = (a.M + 191) / 192, ntn = a.N / bn;
-  if (2 * ntm >= LN_TICKET_WORDS || !ws || ws_bytes < GEMM_TICKET_BYTES + ln_stats_bytes(a.M, a.N, variant))
+  if (ntn > LN_MAX_NTN || 2 * ntm >= LN_TICKET_WORDS || !ws || ws_bytes < GEMM_TICKET_BYTES + ln_stats_bytes(a.M, a.N, variant))
     return false;
   GemmArgs b = a;
   b.ln_ctr = reinterpret_cast<int*>(ws) + (GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS);

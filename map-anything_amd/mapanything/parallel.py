@@ -195,10 +195,9 @@ class RcclComm(DistComm):
     completes is not timed out here (no watchdog over captured work) — MAPA_SHARD_GRAPHS=0 keeps the process group's
     eager, watchdog-timed path."""
 
-    graph_safe = True
-
     def __init__(self, group=None, device=None):
         super().__init__(group)
+        self.graph_safe = True
         from . import rccl
 
         self._rccl_mod = rccl

@@ -5,6 +5,7 @@ Writes its result as JSON to argv[1]."""
 import json
 import os
 import sys
+import warnings
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "map-anything_amd"))
@@ -46,7 +47,9 @@ def main():
         model.hip_graphs = False
         eager = model.infer(views, **kw)
         model.hip_graphs = True
-        g1 = model.infer(views, **kw)  # captures the sharded forward (RCCL collectives inside the graph)
+        with warnings.catch_warnings(record=True) as caught:  # a failed capture warns and falls back to eager
+            warnings.simplefilter("always")
+            g1 = model.infer(views, **kw)  # captures the sharded forward (RCCL collectives inside the graph)
         g2 = model.infer(views, **kw)  # replays it
         torch.cuda.synchronize()
         res[prec] = {
@@ -55,6 +58,7 @@ def main():
             "replay_eq_eager": all(torch.equal(a[k], b[k]) for a, b in zip(g2, eager) for k in KEYS),
             "eager_eq_single": all(torch.equal(a[k], b[k]) for a, b in zip(eager, single) for k in KEYS),
             "err_vs_single": {k: max(rel(eager[v][k], single[v][k]) for v in range(V)) for k in KEYS},
+            "warnings": [str(w.message)[:500] for w in caught],
         }
     with open(out, "w") as f:
         json.dump(res, f)

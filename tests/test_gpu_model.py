@@ -30,7 +30,9 @@ from conftest import GOLDEN, rel_l2
 pytestmark = pytest.mark.gpu
 
 from tests_helpers import CASES, make_views
-BF16_FACTOR, BF16_FLOOR, SMALL_FACTOR, SCALE_FACTOR = 1.5, 1e-3, 2.0, 3.0
+# SCALE_FACTOR: the largest ratio to the spread max measured over every case on MI355X (round 4) is 1.61 (cfg1_224,
+# the same with bf16 or split heads: it comes from the bf16 transformer, not the heads); 2.0 = the per-view bound
+BF16_FACTOR, BF16_FLOOR, SMALL_FACTOR, SCALE_FACTOR = 1.5, 1e-3, 2.0, 2.0
 SMALL_KEYS = ("cam_trans", "cam_quats", "metric_scaling_factor", "camera_poses", "intrinsics")
 METRIC_KEYS = ("pts3d", "depth_along_ray", "cam_trans", "camera_poses")  # multiplied by metric_scaling_factor
 

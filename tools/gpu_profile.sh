@@ -6,7 +6,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof gpurun_out/prof_e gpurun_out/pmc_f gpurun_out/pmc_w gpurun_out/pmc_m
-B="python bench.py --no-cpu-baseline --no-fast-mode --strong-views 0"
+B="python bench.py --no-cpu-baseline --no-fast-mode --strong-views 0 --batch-scenes 0"
 # PART=1: steps 1-2, PART=2: steps 3-4 (each under gpurun's 20-minute limit); default both
 PART=${PART:-12}
 if [[ $PART == *1* ]]; then
