@@ -13,9 +13,10 @@ Differences that are by design:
     geometric encoders and the downstream heads fp32-exact as the reference runs them with autocast disabled
     (model.py:1377, 1774; split-precision bf16 GEMMs on MI355X); `use_amp=False` (or precision="fp32") runs the
     exact-fp32 MFMA path; `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
-  * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687) run scene by scene through the engine
-    (every stage of the path is per scene: global attention, the scale token and scale head, the camera
-    normalisation across views), and the per-view outputs are concatenated on the batch dimension as the reference
+  * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687): image-only scenes run as ONE engine
+    call (encoder, frame layers and heads over all B x V images, global attention, scale token and scale head per
+    scene, as the reference's batched forward, model.py:687-721); scenes with geometric inputs or on a view-sharded
+    model run scene by scene.  The per-view outputs are concatenated on the batch dimension as the reference
     returns them.
 """
 
@@ -113,9 +114,10 @@ class MapAnything:
         # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
         self.hip_graphs = hip_graphs and os.environ.get("MAPA_HIP_GRAPHS", "1") != "0"
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
-        # sharded capture (RCCL collectives inside the HIP graph): opt-in with MAPA_SHARD_GRAPHS=1 until it has run on
-        # the hardware; off on every rank once any rank's capture has failed
-        self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "0") == "1"
+        # sharded capture (the collectives through the direct RCCL communicator, parallel.RcclComm, inside the HIP
+        # graph): off with MAPA_SHARD_GRAPHS=0 (eager launches, collectives through the process group and its
+        # watchdog), or on every rank once any rank's capture has failed
+        self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "1") != "0"
         self._modules: Dict[str, Any] = {}
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)

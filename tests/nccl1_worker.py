@@ -27,7 +27,7 @@ def main():
     out = sys.argv[1]
     torch.cuda.set_device(0)
     os.environ["MAPA_FORCE_COLLECTIVES"] = "1"
-    os.environ["MAPA_SHARD_GRAPHS"] = "1"  # the sharded capture is opt-in
+    os.environ["MAPA_SHARD_GRAPHS"] = "1"  # the default; set in case the caller's environment turned it off
     from mapanything.models import MapAnything
     from mapanything.parallel import init_distributed
     from mapanything.utils import synthetic

@@ -11,7 +11,6 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "map-anything_amd"))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 os.environ["MAPA_FORCE_COLLECTIVES"] = "1"
-os.environ.setdefault("MAPA_SHARD_GRAPHS", "1")  # the sharded capture is opt-in
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
