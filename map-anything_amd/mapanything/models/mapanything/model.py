@@ -110,7 +110,7 @@ class MapAnything:
         self._comm = None
         self._gather = None
         self.training = False
-        # Replay the engine's ~2.7k launches per forward from a captured HIP graph (image-only, single device,
+        # Replay the engine's ~350 launches per forward from a captured HIP graph (image-only, single device,
         # all views in one dense-head pass): removes the host launch gaps.  MAPA_HIP_GRAPHS=0 disables.
         self.hip_graphs = hip_graphs and os.environ.get("MAPA_HIP_GRAPHS", "1") != "0"
         self._graphs: "OrderedDict[tuple, tuple]" = OrderedDict()
