@@ -139,20 +139,19 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& p, f32x4 (&acc)[FM]
 //     4 passes);
 //  2. per tile row: the sum over the tile's columns (8-lane butterfly, then the WN column waves' partials in LDS in
 //     wave order), the tile mean, then M2 = sum (v - mean_t)^2 the same way (two-pass inside the tile);
-//  3. {sum, M2} of every row published as one 8-byte write-through granule per tile (agent-scope relaxed store),
-//     every storing wave drains (vmcnt 0: the residual loads and the granules only), then one arrival on the band's
-//     counter; the new residual rows are stored to out_f32 only now, so they drain while one lane polls the counter
-//     until the band's ntn tiles arrived (bounded: past LN_SPIN_LIMIT polls it sets the flag word and proceeds);
-//  4. per row, from the ntn granules read write-through in column order (the same value in every tile of the band):
-//     mean = sum / N, M2 = sum_t (M2_t + n_t (mean_t - mean)^2) (Chan's merge, exact up to rounding), rstd =
-//     rsqrt(M2 / N + eps);
-//  5. the band's last departing block re-zeroes its two counters; every tile writes y = (v - mean) * rstd * w + b as
-//     bf16 for its own columns.
+//  3. {epoch, sum, M2, ~epoch} of every row published as one 16-byte write-through granule per tile (the data is
+//     its own flag: the guide's R2 hand-off, no drain, no arrival counter; epoch = the band's generation word + 1);
+//     the new residual rows are stored to out_f32 only now, so they drain while the band gathers;
+//  4. per row, the band's ntn granules polled with write-through loads until every one carries this launch's epoch
+//     (bounded: past LN_SPIN_LIMIT polls the flag word is set and the block proceeds), then merged in column order
+//     (the same value in every tile of the band): mean = sum / N, M2 = sum_t (M2_t + n_t (mean_t - mean)^2) (Chan's
+//     merge, exact up to rounding), rstd = rsqrt(M2 / N + eps);
+//  5. the band's last departing block re-arms the departure counter and bumps the generation word; every tile
+//     writes y = (v - mean) * rstd * w + b as bf16 for its own columns.
 // Equal to the standalone two-pass LayerNorm (norm.hip) up to the fp32 rounding of the statistics.  The launch needs
 // N % BN == 0 (every tile holds BN columns of a row) and the row-major in-place residual outputs (epi_mode 2).
 constexpr unsigned LN_SPIN_LIMIT = 1u << 22;
 constexpr int LN_MAX_NTN = 8;  // column tiles per band the merge holds in registers (launch_gemm_big_ln checks)
-typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) int gi32;
 
 template <int FM, int FN, int TM, int TN, int WN, int BM>
@@ -257,22 +256,21 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
       if ((lane & 7) == 0) red[wn * BM + wm * TM + part * 32 + pass * 8 + (lane >> 3)] = q;
     }
   __syncthreads();
-  // 3. publish {sum, M2} per row, arrive, wait for the band
-  gu64* stats = (gu64*)(p.ln_stats) + (int64_t)tm * ntn * BM;
-  gi32* arrive = (gi32*)(p.ln_ctr) + 2 * tm;
-  gi32* depart = arrive + 1;
+  // 3. publish {epoch, sum, M2, ~epoch} per row as one 16-byte write-through granule: the data is its own flag (no
+  // drain, no arrival counter); epoch = the band's generation word + 1, bumped by the band's last departing tile
+  gi32* gen = (gi32*)(p.ln_ctr) + 2 * tm;
+  gi32* depart = gen + 1;
   gi32* flag = (gi32*)(p.ln_ctr) + (LN_TICKET_WORDS - 1);
+  const unsigned epoch = (unsigned)__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.ln_stats + (int64_t)tm * ntn * BM * 4, 0, ntn * BM * 16,
+                                                     0x00020000);
   if (tid < BM) {
     float m2 = 0.f;
 #pragma unroll
     for (int w = 0; w < WN; ++w) m2 += red[w * BM + tid];
-    const unsigned long long gv =
-        (unsigned long long)__float_as_uint(tsum) | ((unsigned long long)__float_as_uint(m2) << 32);
-    __hip_atomic_store(stats + tn * BM + tid, gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32x4 gv = {epoch, __float_as_uint(tsum), __float_as_uint(m2), ~epoch};
+    __builtin_amdgcn_raw_buffer_store_b128(gv, srs, (tn * BM + tid) * 16, 0, 16);  // sc1
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its write-through granules
-  __syncthreads();
-  if (tid == 0) __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the new residual stream (epi_mode 2's out_f32), issued now so its stores drain while the band gathers
 #pragma unroll
   for (int part = 0; part < NP; ++part)
@@ -285,45 +283,46 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
         *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = keep[part][pass][1];
       }
     }
-  if (tid == 0) {
+  // 4. every row's ntn granules polled (write-through loads) until all carry this launch's epoch, then merged in
+  // column order (Chan): the same value in every tile of the band
+  if (tid < BM) {
+    u32x4 gv[LN_MAX_NTN];
     unsigned spins = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntn) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > LN_SPIN_LIMIT) {  // a band tile never arrived: flag it, do not hang the device
+    for (;;) {
+#pragma unroll
+      for (int t = 0; t < LN_MAX_NTN; ++t)
+        gv[t] = t < ntn ? __builtin_amdgcn_raw_buffer_load_b128(srs, (t * BM + tid) * 16, 0, 16) : u32x4{epoch, 0u, 0u, ~epoch};
+      bool ok = true;
+#pragma unroll
+      for (int t = 0; t < LN_MAX_NTN; ++t) ok = ok && gv[t][0] == epoch && gv[t][3] == ~epoch;
+      if (ok) break;
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory");  // re-issue the granule loads every pass
+      if (++spins > LN_SPIN_LIMIT) {  // a band tile never published: flag it, do not hang the device
         __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // no instruction: keeps the granule loads below the poll
-  // 4. merge the band's statistics (write-through loads, tiles in column order)
-  if (tid < BM) {
-    // every granule of the row in flight at once (one fabric round trip), then merged in column order
-    unsigned long long gv[LN_MAX_NTN];
-#pragma unroll
-    for (int t = 0; t < LN_MAX_NTN; ++t)
-      gv[t] = t < ntn ? __hip_atomic_load(stats + t * BM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     float sum = 0.f;
 #pragma unroll
     for (int t = 0; t < LN_MAX_NTN; ++t)
-      if (t < ntn) sum += __uint_as_float((unsigned)gv[t]);
+      if (t < ntn) sum += __uint_as_float(gv[t][1]);
     const float mean = sum / (float)p.N;
     float m2 = 0.f;
 #pragma unroll
     for (int t = 0; t < LN_MAX_NTN; ++t)
       if (t < ntn) {
-        const float d = __uint_as_float((unsigned)gv[t]) * (1.f / BN) - mean;
-        m2 += __uint_as_float((unsigned)(gv[t] >> 32)) + (float)BN * d * d;
+        const float d = __uint_as_float(gv[t][1]) * (1.f / BN) - mean;
+        m2 += __uint_as_float(gv[t][2]) + (float)BN * d * d;
       }
     rmean[tid] = mean;
     rrstd[tid] = rsqrtf(m2 / (float)p.N + p.ln_eps);
   }
   __syncthreads();
-  if (tid == 0) {  // every tile of the band is past its poll: the last one out re-arms the counters
+  if (tid == 0) {  // every tile of the band holds its granules: the last one out bumps the band's generation
     if (__hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ntn - 1) {
-      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(gen, (int)epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // 5. normalise this tile's columns
@@ -1022,7 +1021,7 @@ static int ln_bn(int variant) { return variant == 14 ? 256 : variant == 15 ? 192
 int64_t ln_stats_bytes(int M, int N, int variant) {
   const int bn = ln_bn(variant);
   if (!bn || N % bn) return -1;
-  return (int64_t)((M + 191) / 192) * (N / bn) * 192 * 8;
+  return (int64_t)((M + 191) / 192) * (N / bn) * 192 * 16;  // one 16-B granule per row and column tile
 }
 
 bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
@@ -1037,7 +1036,7 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
     return false;
   GemmArgs b = a;
   b.ln_ctr = reinterpret_cast<int*>(ws) + (GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS);
-  b.ln_stats = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + GEMM_TICKET_BYTES);
+  b.ln_stats = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + GEMM_TICKET_BYTES);
   void (*k)(GemmArgs) = variant == 14 ? gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, false, true>
                                       : gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, false, true>;
   hipLaunchKernelGGL(k, dim3(mapa_idx::lnf_grid(ntm, ntn)), dim3(BTHREADS), 0, stream, b);

@@ -41,8 +41,8 @@ struct GemmArgs {
   float ln_eps;
   void* ln_out;
   int64_t ln_ldo;
-  int* ln_ctr;                   // [2 * bands] arrival / departure counters (zero between launches), then the flag
-  unsigned long long* ln_stats;  // [bands][ntn][BM] per-tile row statistics {sum, M2} (scratch)
+  int* ln_ctr;                   // [bands] {generation, departure counter} words, then the flag (zeroed once)
+  unsigned* ln_stats;            // [bands][ntn][BM] 16-B granules {epoch, sum, M2, ~epoch} (scratch)
 };
 
 using mapa_idx::group_coords;

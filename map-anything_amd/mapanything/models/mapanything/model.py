@@ -507,8 +507,12 @@ class MapAnything:
                             raise
                     if not self._comm.all_agree(err is None, imgs.device):
                         warnings.warn(f"sharded HIP-graph capture failed ({err or 'on another rank'}); "
-                                      "running the sharded path eagerly")
+                                      "running the sharded path eagerly on the process group")
                         self._shard_graphs = False
+                        from ...parallel import DistComm, RcclComm
+
+                        if isinstance(self._comm, RcclComm):  # an aborted capture may leave its RCCL state unusable
+                            self._comm = DistComm(self._comm.group)
                         return eng.run(imgs, shard=plan, comm=self._comm, pe_idx=pe_idx, scenes=scenes)
                 # the side stream is kept with the graph: its handle keys the per-stream workspaces the graph
                 # captured (_native._WS/_AWS), so it must not be destroyed and its handle reused while the graph lives
