@@ -151,7 +151,8 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *   MAPA_TUNE_TILE_GROUP (default 0 = 4): the 256-row data-parallel GEMM kernels walk each XCD's tile range in
  *     groups of this many tile rows (all tile columns of a group before the next group).
  *   MAPA_TUNE_LN_FUSE (default 1, or the environment's MAPA_LN_FUSE): ln_out requests run fused into the residual
- *     linear where it qualifies; 0 = always as a separate mapa_layernorm launch (A/B). */
+ *     linear where its automatic tile choice is the 192-row kernel; 2 = on the fused kernel whatever the tile choice;
+ *     0 = always as a separate mapa_layernorm launch (A/B). */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,
        MAPA_TUNE_LN_FUSE = 4 };
 int mapa_gemm_tune(int key, int value);

@@ -332,9 +332,12 @@ static int g_ln_fuse = -1;    // mapa_gemm_tune(MAPA_TUNE_LN_FUSE, .) / env MAPA
 
 // The residual linears whose automatic tile choice is the 192-row data-parallel kernel (the path's proj / fc2 at
 // 8 views) fuse a requested output LayerNorm (launch_gemm_big_ln); everything else runs it as its own launch.
+// g_ln_fuse 2 (A/B): every qualifying bf16 residual linear on the fused kernel whatever its automatic tile choice
+// (the batched-scene shapes: more tiles than CUs, band progress from in-order dispatch, index_math.h lnf_coords).
 static int pick_ln_fused(const mapa_gemm_desc* d, int variant, int sk) {
-  if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? (atoi(getenv("MAPA_LN_FUSE")) != 0) : 1;
+  if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? atoi(getenv("MAPA_LN_FUSE")) : 1;
   if (!d->ln_out || !g_ln_fuse || d->dtype != MAPA_BF16 || d->a_mode != MAPA_A_DENSE || d->a_split || sk) return 0;
+  if (g_ln_fuse == 2) return d->N % 256 == 0 ? 14 : d->N % 192 == 0 ? 15 : 0;
   return variant == 2574 ? 14 : variant == 2587 ? 15 : 0;
 }
 static int pick_flat(const GemmArgs& a) {
@@ -541,7 +544,7 @@ extern "C" int mapa_gemm_tune(int key, int value) {
   if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 || value == 3 ? value : value ? 1 : 0;
   else if (key == MAPA_TUNE_HALO_SPLIT) g_halo_split = value;
   else if (key == MAPA_TUNE_TILE_GROUP) g_tile_gm = value ? value : 4;
-  else if (key == MAPA_TUNE_LN_FUSE) g_ln_fuse = value ? 1 : 0;
+  else if (key == MAPA_TUNE_LN_FUSE) g_ln_fuse = value == 2 ? 2 : value ? 1 : 0;
   else g_tail_sk = value ? 1 : 0;
   return 0;
 }
