@@ -8,6 +8,7 @@
   python tools/profile_summary.py shapes <kernel_trace.csv> <launch_log.json> -> per kind and problem shape (a log
                                                                                written with MAPA_LAUNCH_SHAPES=1)
   python tools/profile_summary.py headline <kernel_trace.csv> <bench.json>   -> groups over the headline infers only
+  python tools/profile_summary.py agree <kernel_kinds_eager.json> <bench.json> -> bench vs rocprof for the roofline class
 
 With a launch log (MAPA_LAUNCH_LOG, mapanything/_native.py) every GEMM / attention dispatch is named exactly as
 bench.py names it ("gemm", "gemm_ln", "gemm_split", "conv3x3", "conv3x3_split", "attention", "attention_global"): the n-th
@@ -225,6 +226,16 @@ def mfma_groups(path, log_path=None):
             for k, v in acc.items() if v["sq_busy"] > 0}
 
 
+def agree(kinds_json, bench):
+    """The bench line's dominant kernel class: its HIP-event average launch vs rocprofv3's average for the same class
+    in the eager per-kind trace (launch-log-named dispatches, so split / LayerNorm-fused GEMMs are told apart)."""
+    b = json.load(open(bench))
+    r = b["roofline"]
+    k = json.load(open(kinds_json)).get(r["kernel"], {})
+    return {"kernel": r["kernel"], "bench_avg_launch_us": r["avg_launch_us"], "rocprof_eager_avg_us": k.get("avg_us"),
+            "ratio": (r["avg_launch_us"] / k["avg_us"]) if k.get("avg_us") else None, "rocprof_calls": k.get("calls")}
+
+
 if __name__ == "__main__":
     a = sys.argv
     if a[1] == "mfma_groups":
@@ -237,6 +248,8 @@ if __name__ == "__main__":
         print(json.dumps(headline(a[2], a[3]), indent=1))
     elif a[1] == "kinds":
         print(json.dumps(kinds(a[2], a[3]), indent=1))
+    elif a[1] == "agree":
+        print(json.dumps(agree(a[2], a[3]), indent=1))
     elif a[1] == "shapes":
         per = kinds(a[2], a[3], keep_shape=True)
         print(json.dumps(dict(sorted(per.items(), key=lambda kv: -kv[1]["total_ns"])), indent=1))
