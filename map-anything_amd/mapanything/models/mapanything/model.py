@@ -308,9 +308,22 @@ class MapAnything:
         if gather_outputs not in (None, "rank0", "all"):
             raise ValueError(f"gather_outputs must be None, 'rank0' or 'all', got {gather_outputs!r}")
         if comm is None:
-            # an RCCL group with sharded HIP graphs on: the collectives go to RCCL directly (capturable)
-            rccl = self._shard_graphs and dist.get_backend(group) == "nccl"
-            comm = RcclComm(group, self._device if self._device.type == "cuda" else None) if rccl else DistComm(group)
+            comm = DistComm(group)
+            if self._shard_graphs and dist.get_backend(group) == "nccl":
+                # an RCCL group with sharded HIP graphs on: the collectives go to RCCL directly (capturable); every
+                # rank keeps the process-group communicator instead if any rank's RCCL communicator fails
+                dev = self._device if self._device.type == "cuda" else torch.device("cuda", torch.cuda.current_device())
+                rc, err = None, None
+                try:
+                    rc = RcclComm(group, dev)
+                except Exception as e:  # noqa: BLE001 -- agreed on below
+                    err = e
+                if comm.all_agree(rc is not None, dev):
+                    comm = rc
+                else:
+                    warnings.warn(f"direct RCCL communicator unavailable ({err or 'on another rank'}); the sharded "
+                                  "path runs eagerly on the process group")
+                    self._shard_graphs = False
         self._comm = comm
         self._gather = gather_outputs
         return self

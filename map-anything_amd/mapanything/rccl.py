@@ -73,10 +73,14 @@ class Communicator:
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         uid = UniqueId()
-        if self.rank == 0:
-            check(L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-        obj = [ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid))]  # rank 0's bytes reach every rank
+        obj = [None]
+        if self.rank == 0:  # rank 0 always reaches the broadcast: an error travels to every rank as a string
+            rc = L.ncclGetUniqueId(ctypes.byref(uid))
+            obj = [ctypes.string_at(ctypes.addressof(uid), ctypes.sizeof(uid)) if rc == 0
+                   else f"ncclGetUniqueId: {L.ncclGetErrorString(rc).decode()} (ncclResult {rc})"]
         dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if isinstance(obj[0], str):
+            raise RcclError(obj[0])
         ctypes.memmove(ctypes.addressof(uid), obj[0], ctypes.sizeof(uid))
         self.device = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         self._comm = ctypes.c_void_p()
