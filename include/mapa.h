@@ -75,10 +75,13 @@ typedef struct {
   int out_mode; /* MAPA_OUT_ROWMAJOR or MAPA_OUT_PIXSHUF (n = (ky*s+kx)*cout + co, m = img*h*w + y*w + x) */
   int ps_s, ps_h, ps_w, ps_cout;
   /* Optional scratch for the stream-K schedule (bf16 shapes whose tile count divides badly over the CUs) and for
-   * the split-K flat-raster halo conv (the 19^2 / 37^2 convs): device memory, ZERO-FILLED before its first use, used
-   * by one stream at a time.  Only its head (the 256 KiB of ticket words) is returned to zero when each call
-   * completes; the rest holds fp32 partial-sum slabs (scratch data) afterwards.  Size:
-   * mapa_gemm_workspace_bytes.  NULL / too small -> a data-parallel schedule (same results to rounding). */
+   * the split-K flat-raster halo conv (the 19^2 / 37^2 convs) and for the LayerNorm-fused residual linears (ln_out):
+   * device memory, ZERO-FILLED before its first use, used by one stream at a time, never written by the caller
+   * afterwards.  Its 256 KiB head holds the ticket words (returned to zero when each call completes) and, in its top
+   * 64 KiB, the LayerNorm bands' generation words (they count up from call to call) and the barrier-timeout flag
+   * (int word 65535); the rest holds fp32 partial-sum slabs / row-statistics granules (scratch data) afterwards.
+   * Size: mapa_gemm_workspace_bytes.  NULL / too small -> a data-parallel schedule, or the GEMM followed by
+   * mapa_layernorm (same results to rounding). */
   void* workspace;
   int64_t workspace_bytes;
   /* Split-precision operand outputs (dtype BF16 only; NULL = off): row r of out_s3 is 2*ld bf16 wide (ld = ldo, or

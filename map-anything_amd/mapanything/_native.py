@@ -247,10 +247,10 @@ _WS_RETIRED = []  # grown-out GEMM workspaces, kept alive for graphs captured ag
 
 
 def gemm_workspace(nbytes: int) -> torch.Tensor:
-    """Zero-filled GEMM scratch (stream-K tickets + partial-sum slabs) for the current device and stream.
-
-    mapa_gemm leaves it zeroed after every call; one buffer per stream because concurrent calls must not share it.
-    Grown (re-allocated zeroed, stream-ordered) when a larger problem needs more."""
+    """Zero-filled GEMM scratch (stream-K / split-K tickets and slabs, the LayerNorm-fused linears' band generation
+    words and statistics granules) for the current device and stream — include/mapa.h's workspace contract: zeroed
+    once, then owned by mapa_gemm.  One buffer per stream because concurrent calls must not share it.  Grown
+    (re-allocated zeroed, stream-ordered) when a larger problem needs more."""
     key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:

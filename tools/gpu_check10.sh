@@ -1,5 +1,6 @@
 # Round-4 GPU session 9: LayerNorm fused for any tile choice (MAPA_LN_FUSE=2, the batched-scene shapes) — kernel
-# tests, the batched-scene model test under mode 2, and a B = 1 / B = 2 bench A/B of modes 1 and 2 (two rounds)
+# tests, the batched-scene model test under mode 2, the full GPU suite + smoke at the final head, and a B = 1 / B = 2
+# bench A/B of modes 1 and 2 (two rounds)
 set -o pipefail
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
@@ -15,6 +16,10 @@ step lnf timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-met
 tail -3 gpurun_out/lnf.log
 step batched env MAPA_LN_FUSE=2 timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_model.py -k "batched or graph"
 grep -E "passed|failed" gpurun_out/batched.log | tail -3
+step gpu_tests timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+grep -E "passed|failed|FAILED" gpurun_out/gpu_tests.log | tail -8
+step smoke timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+tail -1 gpurun_out/smoke.log
 B="python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --no-fast-mode --strong-views 0"
 for i in 1 2; do
   for f in 1 2; do
