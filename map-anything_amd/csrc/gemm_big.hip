@@ -262,7 +262,10 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
   gi32* depart = gen + 1;
   gi32* flag = (gi32*)(p.ln_ctr) + (LN_TICKET_WORDS - 1);
   const unsigned epoch = (unsigned)__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-  const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.ln_stats + (int64_t)tm * ntn * BM * 4, 0, ntn * BM * 16,
+  // band tm's granules at a fixed stride of LN_MAX_NTN column tiles whatever this shape's ntn: a slot is only ever
+  // written by band tm, with epochs from tm's own monotonic generation word, so no stale granule of another shape
+  // (another ntn) can carry this launch's epoch
+  const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.ln_stats + (int64_t)tm * LN_MAX_NTN * BM * 4, 0, ntn * BM * 16,
                                                      0x00020000);
   if (tid < BM) {
     float m2 = 0.f;
@@ -1021,7 +1024,7 @@ static int ln_bn(int variant) { return variant == 14 ? 256 : variant == 15 ? 192
 int64_t ln_stats_bytes(int M, int N, int variant) {
   const int bn = ln_bn(variant);
   if (!bn || N % bn) return -1;
-  return (int64_t)((M + 191) / 192) * (N / bn) * 192 * 16;  // one 16-B granule per row and column tile
+  return (int64_t)((M + 191) / 192) * LN_MAX_NTN * 192 * 16;  // 16-B granules, LN_MAX_NTN column-tile slots per band
 }
 
 bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
