@@ -106,7 +106,7 @@ typedef struct {
    * (fp32 [N]) and ln_eps and stored to ln_out in the GEMM's 16-bit dtype (fp32 for MAPA_F32), row stride ln_ldo —
    * the next sub-block's nn.LayerNorm fused into the residual linear (dinov2 layers/block.py:93-118,
    * transformer_blocks.py:452-469).  Needs out_f32, row-major.  For bf16 residual linears (out_f32 = resid1 +
-   * gamma * (acc + bias), nothing else) whose tiles are the 192-row data-parallel kernel, and with a workspace of
+   * gamma * (acc + bias), nothing else; N a multiple of 192 or 256) and with a workspace of
    * mapa_gemm_workspace_bytes, the statistics combine across the row's column tiles inside the launch (two-pass per
    * tile, Chan's merge across tiles: the standalone result up to fp32 rounding of mean / variance); otherwise the
    * GEMM is followed by mapa_layernorm on the same stream.  A band barrier that does not complete within its bounded
@@ -153,9 +153,9 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *   MAPA_TUNE_HALO_SPLIT (default 0 = automatic): the K part count of the flat-raster halo conv (1..64).
  *   MAPA_TUNE_TILE_GROUP (default 0 = 4): the 256-row data-parallel GEMM kernels walk each XCD's tile range in
  *     groups of this many tile rows (all tile columns of a group before the next group).
- *   MAPA_TUNE_LN_FUSE (default 1, or the environment's MAPA_LN_FUSE): ln_out requests run fused into the residual
- *     linear where its automatic tile choice is the 192-row kernel; 2 = on the fused kernel whatever the tile choice;
- *     0 = always as a separate mapa_layernorm launch (A/B). */
+ *   MAPA_TUNE_LN_FUSE (default 2, or the environment's MAPA_LN_FUSE): 2 = ln_out requests run on the LayerNorm-fused
+ *     kernel whatever the automatic tile choice of the shape; 1 = only where that choice is the 192-row kernel; 0 =
+ *     always as a separate mapa_layernorm launch (A/B). */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,
        MAPA_TUNE_LN_FUSE = 4 };
 int mapa_gemm_tune(int key, int value);

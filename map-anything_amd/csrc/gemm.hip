@@ -332,10 +332,12 @@ static int g_ln_fuse = -1;    // mapa_gemm_tune(MAPA_TUNE_LN_FUSE, .) / env MAPA
 
 // The residual linears whose automatic tile choice is the 192-row data-parallel kernel (the path's proj / fc2 at
 // 8 views) fuse a requested output LayerNorm (launch_gemm_big_ln); everything else runs it as its own launch.
-// g_ln_fuse 2 (A/B): every qualifying bf16 residual linear on the fused kernel whatever its automatic tile choice
-// (the batched-scene shapes: more tiles than CUs, band progress from in-order dispatch, index_math.h lnf_coords).
+// g_ln_fuse 2 (default): every qualifying bf16 residual linear on the fused kernel whatever its automatic tile choice
+// (the batched-scene shapes too: more tiles than CUs, band progress from in-order dispatch, index_math.h lnf_coords;
+// B = 2 x 8 views 254.4 / 256.9 vs 251.4 / 250.8 views/s in mode 1, the B = 1 launches identical); 1 = only where the
+// automatic choice is the 192-row kernel; 0 = GEMM, then mapa_layernorm.
 static int pick_ln_fused(const mapa_gemm_desc* d, int variant, int sk) {
-  if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? atoi(getenv("MAPA_LN_FUSE")) : 1;
+  if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? atoi(getenv("MAPA_LN_FUSE")) : 2;
   if (!d->ln_out || !g_ln_fuse || d->dtype != MAPA_BF16 || d->a_mode != MAPA_A_DENSE || d->a_split || sk) return 0;
   if (g_ln_fuse == 2) return d->N % 256 == 0 ? 14 : d->N % 192 == 0 ? 15 : 0;
   return variant == 2574 ? 14 : variant == 2587 ? 15 : 0;

@@ -282,7 +282,7 @@ def gemm_tune(key: int, value: int):
     on the LDS halo-window kernel, default on), TUNE_TAIL_STREAMK (tail-only stream-K for nearly empty last waves),
     TUNE_HALO_SPLIT (K part count of the flat-raster halo conv, 0 = automatic), TUNE_TILE_GROUP (tile rows per group
     in the 256-row GEMM kernels' tile order, 0 = the default 4), TUNE_LN_FUSE (LayerNorm fused into the residual
-    linears where it qualifies, default 1)."""
+    linears: 2 = default, whatever the tile choice; 1 = where it is the 192-row kernel; 0 = off)."""
     check(lib().mapa_gemm_tune(key, value), "mapa_gemm_tune")
     _WS_NEED.clear()
 
