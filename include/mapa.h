@@ -42,6 +42,24 @@ int mapa_device_check(int device);
  * HIP_LAUNCH_BLOCKING is set) — SURVEY.md §5's race-detection / serialize row; no reference counterpart. */
 int mapa_stream_check(mapa_stream_t stream, const char* what);
 
+/* Device-side fault channel (round 5).  Kernels that can detect a failed assumption at run time set a bit of the
+ * library's sticky per-device fault word instead of hanging or failing silently; today one: MAPA_FAULT_LN_BARRIER, a
+ * LayerNorm-fused GEMM band barrier (mapa_gemm_desc.ln_out) that did not complete within its bounded wait — that
+ * launch's LayerNorm rows are invalid.
+ *   mapa_fault_slot_create: 64 bytes of coherent, device-mapped pinned host memory (the one allocation the library
+ *     makes; free with mapa_fault_slot_destroy); *host for the CPU, *dev for mapa_fault_publish.
+ *   mapa_fault_publish: enqueue on `stream` a one-lane kernel that writes dev_slot[0] = 1 | (fault word << 1) once
+ *     every earlier launch on the stream has completed (graph-capturable).  The host zeroes slot[0], enqueues the
+ *     work and the publish, and polls slot[0] != 0 — no stream synchronisation, so the GPU keeps running the work
+ *     queued after the publish (MapAnything.infer publishes after the transformer and checks before returning).
+ *   mapa_fault_status: synchronous read of the fault word (and reset to 0 when `reset`); -1 on a HIP error.
+ *   mapa_stream_check also reports and clears it. */
+enum { MAPA_FAULT_LN_BARRIER = 1 };
+int mapa_fault_slot_create(uint32_t** host, uint32_t** dev);
+int mapa_fault_slot_destroy(uint32_t* host);
+int mapa_fault_publish(uint32_t* dev_slot, mapa_stream_t stream);
+int mapa_fault_status(int reset);
+
 /* ---------------------------------------------------------------------------------------------------------
  * GEMM / implicit-GEMM convolution: C[M,N] = A[M,K] * W[N,K]^T, fused epilogue
  *   v = acc + bias[n % bias_mod]; v = act(v); v *= gamma[n]; v += resid1[o] + resid2[o];
@@ -78,8 +96,11 @@ typedef struct {
    * the split-K flat-raster halo conv (the 19^2 / 37^2 convs) and for the LayerNorm-fused residual linears (ln_out):
    * device memory, ZERO-FILLED before its first use, used by one stream at a time, never written by the caller
    * afterwards.  Its 256 KiB head holds the ticket words (returned to zero when each call completes) and, in its top
-   * 64 KiB, the LayerNorm bands' generation words (they count up from call to call) and the barrier-timeout flag
-   * (int word 65535); the rest holds fp32 partial-sum slabs / row-statistics granules (scratch data) afterwards.
+   * 64 KiB, the LayerNorm bands' generation words (they count up from call to call); the rest holds fp32 partial-sum
+   * slabs / row-statistics granules (scratch data) afterwards.  LayerNorm-fused calls (ln_out) should get a
+   * workspace of their own, not shared with stream-K / split-K calls: their granule slots are then written only by
+   * their own band with that band's monotonic epoch tags (with a shared workspace, slab data left in a slot is
+   * rejected by the {epoch, ~epoch} tags alone).  The Python binding keeps one of each per stream.
    * Size: mapa_gemm_workspace_bytes.  NULL / too small -> a data-parallel schedule, or the GEMM followed by
    * mapa_layernorm (same results to rounding). */
   void* workspace;
@@ -109,8 +130,10 @@ typedef struct {
    * gamma * (acc + bias), nothing else; N a multiple of 192 or 256) and with a workspace of
    * mapa_gemm_workspace_bytes, the statistics combine across the row's column tiles inside the launch (two-pass per
    * tile, Chan's merge across tiles: the standalone result up to fp32 rounding of mean / variance); otherwise the
-   * GEMM is followed by mapa_layernorm on the same stream.  A band barrier that does not complete within its bounded
-   * wait sets int word 65535 of the workspace (the last word of its 256 KiB head) to 1 instead of hanging. */
+   * GEMM is followed by mapa_layernorm on the same stream.  The fused kernel never has more workgroups in flight
+   * than the device holds at once (larger problems run as several launches of whole bands), so its band barrier
+   * does not depend on dispatch order; a barrier that still does not complete within its bounded wait sets
+   * MAPA_FAULT_LN_BARRIER in the fault word (mapa_fault_publish / mapa_fault_status) instead of hanging. */
   const float* ln_w;
   const float* ln_b;
   float ln_eps;
@@ -155,9 +178,12 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *     groups of this many tile rows (all tile columns of a group before the next group).
  *   MAPA_TUNE_LN_FUSE (default 2, or the environment's MAPA_LN_FUSE): 2 = ln_out requests run on the LayerNorm-fused
  *     kernel whatever the automatic tile choice of the shape; 1 = only where that choice is the 192-row kernel; 0 =
- *     always as a separate mapa_layernorm launch (A/B). */
+ *     always as a separate mapa_layernorm launch (A/B).
+ *   MAPA_TUNE_LN_SPIN (default 0 = 2^22): polls of the fused LayerNorm's band barrier before it gives up.
+ *   MAPA_TUNE_LN_TEST_SKIP (test hook, default 0): the next `value` LayerNorm-fused launches each have one tile
+ *     (band 0, column tile 0) skip its statistics publish, so band 0 times out and raises MAPA_FAULT_LN_BARRIER. */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,
-       MAPA_TUNE_LN_FUSE = 4 };
+       MAPA_TUNE_LN_FUSE = 4, MAPA_TUNE_LN_SPIN = 5, MAPA_TUNE_LN_TEST_SKIP = 6 };
 int mapa_gemm_tune(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------------------

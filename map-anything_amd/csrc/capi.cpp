@@ -43,11 +43,19 @@ extern "C" int mapa_device_check(int device) {
 // whatever synchronises next.  Launch errors are already reported (and cleared) by each entry point's own
 // hipGetLastError (MAPA_CHECK_LAUNCH), so this only synchronises and PEEKS: a sticky error left by an unrelated
 // earlier call is reported as such but not cleared, so the caller still sees the real error state.
+// It also reads (and clears) the library's sticky fault word: a LayerNorm band barrier that gave up is reported here
+// as the failure of the launch being checked.
 extern "C" int mapa_stream_check(hipStream_t stream, const char* what) {
   const hipError_t s = hipStreamSynchronize(stream);
   const hipError_t e = s != hipSuccess ? s : hipPeekAtLastError();
   if (e != hipSuccess)
     return mapa_set_error("%s: device error after launch: %s (hipError %d)", what ? what : "launch",
                           hipGetErrorString(e), (int)e);
+  const int f = mapa_fault_status(1);
+  if (f < 0) return 1;  // message already set
+  if (f & MAPA_FAULT_LN_BARRIER)
+    return mapa_set_error("%s: a LayerNorm-fused GEMM band barrier timed out (its LayerNorm rows are invalid)",
+                          what ? what : "launch");
+  if (f) return mapa_set_error("%s: device fault word 0x%x", what ? what : "launch", (unsigned)f);
   return 0;
 }

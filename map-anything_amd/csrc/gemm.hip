@@ -333,9 +333,9 @@ static int g_ln_fuse = -1;    // mapa_gemm_tune(MAPA_TUNE_LN_FUSE, .) / env MAPA
 // The residual linears whose automatic tile choice is the 192-row data-parallel kernel (the path's proj / fc2 at
 // 8 views) fuse a requested output LayerNorm (launch_gemm_big_ln); everything else runs it as its own launch.
 // g_ln_fuse 2 (default): every qualifying bf16 residual linear on the fused kernel whatever its automatic tile choice
-// (the batched-scene shapes too: more tiles than CUs, band progress from in-order dispatch, index_math.h lnf_coords;
-// B = 2 x 8 views 254.4 / 256.9 vs 251.4 / 250.8 views/s in mode 1, the B = 1 launches identical); 1 = only where the
-// automatic choice is the 192-row kernel; 0 = GEMM, then mapa_layernorm.
+// (the batched-scene shapes too: more bands than the device holds at once run as several launches of co-resident
+// bands, launch_gemm_big_ln; B = 2 x 8 views 254.4 / 256.9 vs 251.4 / 250.8 views/s in mode 1, the B = 1 launches
+// identical); 1 = only where the automatic choice is the 192-row kernel; 0 = GEMM, then mapa_layernorm.
 static int pick_ln_fused(const mapa_gemm_desc* d, int variant, int sk) {
   if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? atoi(getenv("MAPA_LN_FUSE")) : 2;
   if (!d->ln_out || !g_ln_fuse || d->dtype != MAPA_BF16 || d->a_mode != MAPA_A_DENSE || d->a_split || sk) return 0;
@@ -539,8 +539,19 @@ extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6,
 
 extern "C" int mapa_gemm_tune(int key, int value) {
   MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK || key == MAPA_TUNE_HALO_SPLIT ||
-                     key == MAPA_TUNE_TILE_GROUP || key == MAPA_TUNE_LN_FUSE,
+                     key == MAPA_TUNE_TILE_GROUP || key == MAPA_TUNE_LN_FUSE || key == MAPA_TUNE_LN_SPIN ||
+                     key == MAPA_TUNE_LN_TEST_SKIP,
                  "mapa_gemm_tune: unknown key %d", key);
+  MAPA_CHECK_ARG((key != MAPA_TUNE_LN_SPIN && key != MAPA_TUNE_LN_TEST_SKIP) || value >= 0,
+                 "mapa_gemm_tune: negative value %d", value);
+  if (key == MAPA_TUNE_LN_SPIN) {
+    ln_set_spin((unsigned)value);
+    return 0;
+  }
+  if (key == MAPA_TUNE_LN_TEST_SKIP) {
+    ln_arm_test_skip(value);
+    return 0;
+  }
   MAPA_CHECK_ARG(key != MAPA_TUNE_HALO_SPLIT || (value >= 0 && value <= 64), "mapa_gemm_tune: split %d", value);
   MAPA_CHECK_ARG(key != MAPA_TUNE_TILE_GROUP || (value >= 0 && value <= 1024), "mapa_gemm_tune: group %d", value);
   if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 || value == 3 ? value : value ? 1 : 0;

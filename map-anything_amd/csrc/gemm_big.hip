@@ -11,6 +11,8 @@
 //    applied on the per-lane SOURCE address -> conflict-free ds_read_b128 fragment reads).
 //  * K tile t+1 is DMA'd into the other stage while tile t is multiplied; one barrier per K tile.
 //  * Epilogue: each wave stages 32 x 64 fp32 of its accumulators through LDS and stores 16-B row segments.
+#include <string.h>
+
 #include <algorithm>
 #include <type_traits>
 
@@ -143,16 +145,25 @@ __device__ __forceinline__ void big_epilogue(const GemmArgs& p, f32x4 (&acc)[FM]
 //     its own flag: the guide's R2 hand-off, no drain, no arrival counter; epoch = the band's generation word + 1);
 //     the new residual rows are stored to out_f32 only now, so they drain while the band gathers;
 //  4. per row, the band's ntn granules polled with write-through loads until every one carries this launch's epoch
-//     (bounded: past LN_SPIN_LIMIT polls the flag word is set and the block proceeds), then merged in column order
+//     (bounded: past p.ln_spin polls the library's fault word gets MAPA_FAULT_LN_BARRIER and the block proceeds —
+//     the host raises on it, mapa_fault_publish / mapa_fault_status), then merged in column order
 //     (the same value in every tile of the band): mean = sum / N, M2 = sum_t (M2_t + n_t (mean_t - mean)^2) (Chan's
 //     merge, exact up to rounding), rstd = rsqrt(M2 / N + eps);
 //  5. the band's last departing block re-arms the departure counter and bumps the generation word; every tile
 //     writes y = (v - mean) * rstd * w + b as bf16 for its own columns.
 // Equal to the standalone two-pass LayerNorm (norm.hip) up to the fp32 rounding of the statistics.  The launch needs
 // N % BN == 0 (every tile holds BN columns of a row) and the row-major in-place residual outputs (epi_mode 2).
-constexpr unsigned LN_SPIN_LIMIT = 1u << 22;
+// Progress: launch_gemm_big_ln never launches more workgroups than the device holds at once (occupancy x CUs), so
+// every tile a waiting tile needs is resident or waits only for a slot held by another kernel — nothing assumes an
+// order of dispatch.  The granule hand-off assumes a 16-byte aligned dwordx4 store reaches L2 as one piece (the
+// guide's R2 hand-off); a torn granule would fail the {epoch, ~epoch} check and be re-polled, not merged.
+constexpr unsigned LN_SPIN_DEFAULT = 1u << 22;  // ~1 us per poll round: seconds before a band gives up
 constexpr int LN_MAX_NTN = 8;  // column tiles per band the merge holds in registers (launch_gemm_big_ln checks)
 typedef __attribute__((address_space(1))) int gi32;
+
+// Sticky fault bits of the library (MAPA_FAULT_* in mapa.h), set by device code, read by mapa_fault_publish (into a
+// host-visible slot, stream-ordered) and mapa_fault_status (synchronously).  Written with vector atomics only.
+__device__ unsigned g_mapa_fault;
 
 template <int FM, int FN, int TM, int TN, int WN, int BM>
 __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[FM][FN], char* lds, int tm, int tn,
@@ -260,14 +271,13 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
   // drain, no arrival counter); epoch = the band's generation word + 1, bumped by the band's last departing tile
   gi32* gen = (gi32*)(p.ln_ctr) + 2 * tm;
   gi32* depart = gen + 1;
-  gi32* flag = (gi32*)(p.ln_ctr) + (LN_TICKET_WORDS - 1);
   const unsigned epoch = (unsigned)__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   // band tm's granules at a fixed stride of LN_MAX_NTN column tiles whatever this shape's ntn: a slot is only ever
   // written by band tm, with epochs from tm's own monotonic generation word, so no stale granule of another shape
   // (another ntn) can carry this launch's epoch
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.ln_stats + (int64_t)tm * LN_MAX_NTN * BM * 4, 0, ntn * BM * 16,
                                                      0x00020000);
-  if (tid < BM) {
+  if (tid < BM && !(p.ln_skip && tm == 0 && tn == 0)) {  // (ln_skip: the test hook's missing tile)
     float m2 = 0.f;
 #pragma unroll
     for (int w = 0; w < WN; ++w) m2 += red[w * BM + tid];
@@ -301,8 +311,9 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
       if (ok) break;
       __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");  // re-issue the granule loads every pass
-      if (++spins > LN_SPIN_LIMIT) {  // a band tile never published: flag it, do not hang the device
-        __hip_atomic_store(flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > p.ln_spin) {  // a band tile never published: raise the fault word, do not hang the device
+        __hip_atomic_fetch_or(&g_mapa_fault, (unsigned)MAPA_FAULT_LN_BARRIER, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -367,7 +378,9 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BM - 1) / BM;
   int tm, tn;
   if constexpr (LNF) {
-    if (!mapa_idx::lnf_coords(blockIdx.x, ntm, ntn, tm, tn)) return;  // idle block of an XCD with one band fewer
+    // this launch's bands [ln_band0, ln_band0 + ln_nbands); idle block of an XCD with one band fewer
+    if (!mapa_idx::lnf_coords(blockIdx.x, p.ln_nbands, ntn, tm, tn)) return;
+    tm += p.ln_band0;
   } else {
     mapa_idx::tile_coords_rt(blockIdx.x, p.tile_gm, ntm, ntn, tm, tn);
   }
@@ -1027,6 +1040,26 @@ int64_t ln_stats_bytes(int M, int N, int variant) {
   return (int64_t)((M + 191) / 192) * LN_MAX_NTN * 192 * 16;  // 16-B granules, LN_MAX_NTN column-tile slots per band
 }
 
+static unsigned g_ln_spin = LN_SPIN_DEFAULT;  // mapa_gemm_tune(MAPA_TUNE_LN_SPIN, .)
+static int g_ln_skip = 0;                      // mapa_gemm_tune(MAPA_TUNE_LN_TEST_SKIP, .): launches left to sabotage
+void ln_set_spin(unsigned spins) { g_ln_spin = spins ? spins : LN_SPIN_DEFAULT; }
+void ln_arm_test_skip(int n) { g_ln_skip = n; }
+
+static int device_cus();
+
+// Workgroups of an LNF kernel the device holds at once (occupancy per CU x CUs), per variant.
+static int lnf_slots(int variant, void (*k)(GemmArgs)) {
+  static int slots[2] = {0, 0};
+  int& s = slots[variant == 14 ? 0 : 1];
+  if (!s) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, BTHREADS, 0) != hipSuccess || per_cu <= 0)
+      per_cu = 1;
+    s = per_cu * device_cus();
+  }
+  return s;
+}
+
 bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_bytes, hipStream_t stream) {
   const int bn = ln_bn(variant);
   if (!bn || a.N % bn || a.lp_f16 || !a.ln_out || !a.ln_w || !a.ln_b || a.ln_ldo % 8 != 0) return false;
@@ -1037,18 +1070,51 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
   const int ntm = (a.M + 191) / 192, ntn = a.N / bn;
   if (ntn > LN_MAX_NTN || 2 * ntm >= LN_TICKET_WORDS || !ws || ws_bytes < GEMM_TICKET_BYTES + ln_stats_bytes(a.M, a.N, variant))
     return false;
+  void (*k)(GemmArgs) = variant == 14 ? gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, false, true>
+                                      : gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, false, true>;
+  // Co-residency by construction: every launch holds at most `slots` workgroups (lnf_grid rounds the bands up to a
+  // multiple of the 8 XCDs), so a band's tiles never wait on a tile that cannot be dispatched until they finish.
+  // Larger problems (batched scenes, the 100-view job) run as several launches of balanced band ranges.
+  const int slots = lnf_slots(variant, k);
+  const int nb_max = 8 * (slots / (8 * ntn));
+  if (nb_max <= 0) return false;
+  const int launches = (ntm + nb_max - 1) / nb_max;
+  const int nb = (ntm + launches - 1) / launches;
   GemmArgs b = a;
   b.ln_ctr = reinterpret_cast<int*>(ws) + (GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS);
   b.ln_stats = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + GEMM_TICKET_BYTES);
-  void (*k)(GemmArgs) = variant == 14 ? gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, false, true>
-                                      : gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, false, true>;
-  hipLaunchKernelGGL(k, dim3(mapa_idx::lnf_grid(ntm, ntn)), dim3(BTHREADS), 0, stream, b);
+  b.ln_spin = g_ln_spin;
+  b.ln_skip = 0;
+  if (g_ln_skip > 0) {
+    b.ln_skip = 1;
+    --g_ln_skip;
+  }
+  for (int b0 = 0; b0 < ntm; b0 += nb) {
+    b.ln_band0 = b0;
+    b.ln_nbands = nb < ntm - b0 ? nb : ntm - b0;
+    const int grid = mapa_idx::lnf_grid(b.ln_nbands, ntn);
+    if (grid > slots) {  // cannot happen with nb <= nb_max; checked so a change to lnf_grid cannot break progress
+      mapa_set_error("mapa_gemm: LayerNorm-fused launch of %d workgroups exceeds the %d co-resident slots", grid,
+                     slots);
+      return false;
+    }
+    hipLaunchKernelGGL(k, dim3(grid), dim3(BTHREADS), 0, stream, b);
+    b.ln_skip = 0;
+  }
   return true;
+}
+
+// The library's fault word (g_mapa_fault): stream-ordered publish into a host-visible slot, synchronous read / reset.
+__global__ void fault_publish_kernel(unsigned* slot) {
+  if (threadIdx.x == 0) {
+    const unsigned f = __hip_atomic_load(&g_mapa_fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(slot, 1u | (f << 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Stream-K variants: 0 = 256x128 / 64-B rows / 3 stages / setprio / 2 per CU, 1 = 256x256 / 64-B rows / 3 stages
 // / setprio / 1 per CU.  Workspace: [tickets: 64 Ki words][slabs: G * 2 * 256 * BN * 4].
-static int sk_cus() {
+static int device_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1057,6 +1123,7 @@ static int sk_cus() {
   }
   return cus;
 }
+static int sk_cus() { return device_cus(); }
 
 static void sk_shape(int variant, int& bn, int& per_cu) {
   bn = variant == 1 ? 256 : 128;
@@ -1110,3 +1177,53 @@ bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, in
 }
 
 }  // namespace mapa_gemm_impl
+
+extern "C" int mapa_fault_slot_create(uint32_t** host, uint32_t** dev) {
+  MAPA_CHECK_ARG(host && dev, "mapa_fault_slot_create: null output");
+  void* h = nullptr;
+  hipError_t e = hipHostMalloc(&h, 64, hipHostMallocCoherent | hipHostMallocMapped);
+  if (e != hipSuccess) return mapa_set_error("mapa_fault_slot_create: hipHostMalloc: %s", hipGetErrorString(e));
+  void* d = nullptr;
+  e = hipHostGetDevicePointer(&d, h, 0);
+  if (e != hipSuccess) {
+    (void)hipHostFree(h);
+    return mapa_set_error("mapa_fault_slot_create: hipHostGetDevicePointer: %s", hipGetErrorString(e));
+  }
+  memset(h, 0, 64);
+  *host = static_cast<uint32_t*>(h);
+  *dev = static_cast<uint32_t*>(d);
+  return 0;
+}
+
+extern "C" int mapa_fault_slot_destroy(uint32_t* host) {
+  if (!host) return 0;
+  const hipError_t e = hipHostFree(host);
+  return e == hipSuccess ? 0 : mapa_set_error("mapa_fault_slot_destroy: %s", hipGetErrorString(e));
+}
+
+extern "C" int mapa_fault_publish(uint32_t* dev_slot, hipStream_t stream) {
+  MAPA_CHECK_ARG(dev_slot != nullptr, "mapa_fault_publish: null slot");
+  hipLaunchKernelGGL(mapa_gemm_impl::fault_publish_kernel, dim3(1), dim3(64), 0, stream,
+                     reinterpret_cast<unsigned*>(dev_slot));
+  MAPA_CHECK_LAUNCH("mapa_fault_publish");
+  return 0;
+}
+
+extern "C" int mapa_fault_status(int reset) {
+  unsigned v = 0;
+  hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(mapa_gemm_impl::g_mapa_fault), sizeof(v), 0,
+                                     hipMemcpyDeviceToHost);
+  if (e != hipSuccess) {
+    mapa_set_error("mapa_fault_status: %s", hipGetErrorString(e));
+    return -1;
+  }
+  if (reset && v) {
+    const unsigned zero = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(mapa_gemm_impl::g_mapa_fault), &zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      mapa_set_error("mapa_fault_status: reset: %s", hipGetErrorString(e));
+      return -1;
+    }
+  }
+  return (int)v;
+}

@@ -41,8 +41,11 @@ struct GemmArgs {
   float ln_eps;
   void* ln_out;
   int64_t ln_ldo;
-  int* ln_ctr;                   // [bands] {generation, departure counter} words, then the flag (zeroed once)
-  unsigned* ln_stats;            // [bands][ntn][BM] 16-B granules {epoch, sum, M2, ~epoch} (scratch)
+  int* ln_ctr;                   // [bands] {generation, departure counter} words (zeroed once)
+  unsigned* ln_stats;            // [bands][LN_MAX_NTN][BM] 16-B granules {epoch, sum, M2, ~epoch} (scratch)
+  int ln_band0, ln_nbands;       // this launch's bands [ln_band0, ln_band0 + ln_nbands) (co-resident by construction)
+  unsigned ln_spin;              // bounded wait: polls before the band barrier gives up and raises the fault word
+  int ln_skip;                   // test hook: tile (band 0, column 0) skips its publish (mapa_gemm_tune LN_TEST_SKIP)
 };
 
 using mapa_idx::group_coords;
@@ -361,13 +364,18 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
 
 // The in-place residual linear (epi_mode 2: out_f32 = resid1 + gamma * (acc + bias)) with the LayerNorm of its output
 // rows fused (gemm_big.hip, LNF): the row statistics combine across a band's column tiles inside the launch (band
-// barrier through the ticket head of the workspace), then every tile normalises its own rows into a.ln_out (bf16).
+// barrier through the workspace), then every tile normalises its own rows into a.ln_out (bf16).
 // variant: 14 (192x256 tiles) or 15 (192x192).  Returns false if the shape / epilogue / workspace does not qualify.
-// Workspace: the GEMM ticket head (its top LN_TICKET_WORDS words: per-band arrival / departure counters and the
-// timeout flag) + ln_stats_bytes of per-tile row statistics.
+// Workspace: the GEMM ticket head (its top LN_TICKET_WORDS words: per-band generation / departure counters) +
+// ln_stats_bytes of per-tile row statistics.  Problems with more bands than the device holds at once run as several
+// launches of co-resident bands (the barrier's progress never depends on dispatch order).  A band that does not
+// complete within its bounded wait sets MAPA_FAULT_LN_BARRIER in the library's fault word (mapa_fault_status).
 constexpr int LN_TICKET_WORDS = 16384;
 int64_t ln_stats_bytes(int M, int N, int variant);
 bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_bytes, hipStream_t stream);
+// Tuning / test state of the LayerNorm-fused launches (mapa_gemm_tune MAPA_TUNE_LN_SPIN / MAPA_TUNE_LN_TEST_SKIP).
+void ln_set_spin(unsigned spins);
+void ln_arm_test_skip(int n);
 
 // Stride-1 3x3 conv with its A operand read from an LDS halo window (conv_halo.hip); bn = 256 / 128 / 0 (auto).
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).

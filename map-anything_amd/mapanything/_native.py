@@ -30,8 +30,10 @@ EXPORTED = (
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
     "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
     "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_tune",
-    "mapa_regressor_head_out", "mapa_stream_check",
+    "mapa_regressor_head_out", "mapa_stream_check", "mapa_fault_slot_create", "mapa_fault_slot_destroy",
+    "mapa_fault_publish", "mapa_fault_status",
 )
+FAULT_LN_BARRIER = 1  # include/mapa.h MAPA_FAULT_LN_BARRIER
 
 
 class GemmDesc(ctypes.Structure):
@@ -125,6 +127,11 @@ def load_library(path: Optional[str] = None):
     L.mapa_normalize_image.argtypes = [vp, i, i, i, vp, vp, vp, vp]
     L.mapa_rope2d.argtypes = [vp, i, i, i, i, i, i64, i64, i64, vp, f, f, vp]
     L.mapa_stream_check.argtypes = [vp, ctypes.c_char_p]
+    pu32 = ctypes.POINTER(ctypes.c_uint32)
+    L.mapa_fault_slot_create.argtypes = [ctypes.POINTER(pu32), ctypes.POINTER(pu32)]
+    L.mapa_fault_slot_destroy.argtypes = [pu32]
+    L.mapa_fault_publish.argtypes = [pu32, vp]
+    L.mapa_fault_status.argtypes = [i]
     _lib = L
     return L
 
@@ -184,6 +191,96 @@ def dt_code(dtype: torch.dtype) -> int:
     if dtype == torch.float16:
         return F16
     raise NativeError(f"unsupported dtype {dtype}")
+
+
+# ------------------------------------------------------------------------------------------- fault channel
+def _fault_message(bits: int) -> str:
+    if bits & FAULT_LN_BARRIER:
+        return ("a LayerNorm-fused GEMM band barrier timed out on the device (include/mapa.h MAPA_FAULT_LN_BARRIER): "
+                "the normalised rows of that launch are invalid, so this call's outputs were discarded")
+    return f"device fault word 0x{bits:x}"
+
+
+def fault_status(reset: bool = True) -> int:
+    """Synchronous read of the library's sticky device fault word (mapa_fault_status), reset when `reset`."""
+    v = int(lib().mapa_fault_status(1 if reset else 0))
+    if v < 0:
+        raise NativeError(lib().mapa_last_error().decode())
+    return v
+
+
+def check_faults():
+    """Raise NativeError if a kernel set the device fault word since the last check (synchronises the device)."""
+    v = fault_status(reset=True)
+    if v:
+        raise NativeError(_fault_message(v))
+
+
+class FaultTimeout(NativeError):
+    """The device did not reach a fault publish within the caller's bound (a hung kernel or collective)."""
+
+
+class FaultSlot:
+    """A host-visible slot the device writes its fault word into, stream-ordered (mapa_fault_publish): the host
+    arms it (slot = 0), enqueues work + publish(), and wait() polls the slot — without synchronising the stream, so
+    the kernels queued after the publish keep the GPU busy while the host checks.  One slot per captured graph (its
+    publish node is baked into the graph with this slot's address) and one per eager caller."""
+
+    def __init__(self):
+        L = lib()
+        h, d = ctypes.POINTER(ctypes.c_uint32)(), ctypes.POINTER(ctypes.c_uint32)()
+        if L.mapa_fault_slot_create(ctypes.byref(h), ctypes.byref(d)) != 0:
+            raise NativeError(L.mapa_last_error().decode())
+        self._h, self._d = h, d
+        self._word = ctypes.c_uint32.from_address(ctypes.addressof(h.contents))
+        self.armed = False
+
+    def arm(self):
+        self._word.value = 0
+        self.armed = True
+
+    def publish(self):
+        """Enqueue the publish on the current stream (also inside a graph capture)."""
+        check(lib().mapa_fault_publish(self._d, stream()), "mapa_fault_publish")
+
+    def wait(self, timeout_s: float = 600.0, poll=None):
+        """Poll until the armed publish has run; raise NativeError if it carried a fault (the device word is reset).
+        The poll sleeps ~50 us between reads, calls `poll()` (e.g. a communicator's asynchronous-error check) every
+        ~10 ms, and raises FaultTimeout past timeout_s, or NativeError if the stream drains without the publish."""
+        import time
+
+        if not self.armed:
+            return
+        self.armed = False
+        t0, s = time.monotonic(), torch.cuda.current_stream()
+        t_poll = t0
+        while True:
+            v = self._word.value
+            if v:
+                break
+            if s.query():  # the stream is idle: the publish ran (re-read once) or never was enqueued
+                v = self._word.value
+                if not v:
+                    raise NativeError("fault publish slot armed but never written (the publish was not enqueued)")
+                break
+            now = time.monotonic()
+            if now - t0 > timeout_s:
+                raise FaultTimeout(f"fault publish not reached within {timeout_s:.0f} s")
+            if poll is not None and now - t_poll > 0.01:
+                poll()
+                t_poll = now
+            time.sleep(5e-5)
+        bits = v >> 1
+        if bits:
+            fault_status(reset=True)
+            raise NativeError(_fault_message(bits))
+
+    def __del__(self):
+        try:
+            if _lib is not None and getattr(self, "_h", None):
+                _lib.mapa_fault_slot_destroy(self._h)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
 
 
 # --------------------------------------------------------------------------------------- kernel timing
@@ -246,12 +343,13 @@ _AWS = {}
 _WS_RETIRED = []  # grown-out GEMM workspaces, kept alive for graphs captured against them
 
 
-def gemm_workspace(nbytes: int) -> torch.Tensor:
-    """Zero-filled GEMM scratch (stream-K / split-K tickets and slabs, the LayerNorm-fused linears' band generation
-    words and statistics granules) for the current device and stream — include/mapa.h's workspace contract: zeroed
-    once, then owned by mapa_gemm.  One buffer per stream because concurrent calls must not share it.  Grown
-    (re-allocated zeroed, stream-ordered) when a larger problem needs more."""
-    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream)
+def gemm_workspace(nbytes: int, ln: bool = False) -> torch.Tensor:
+    """Zero-filled GEMM scratch (stream-K / split-K tickets and slabs; with ln=True the LayerNorm-fused linears' band
+    generation words and statistics granules, in a buffer of their own) for the current device and stream —
+    include/mapa.h's workspace contract: zeroed once, then owned by mapa_gemm.  One buffer per stream (and kind)
+    because concurrent calls must not share it.  Grown (re-allocated zeroed, stream-ordered) when a larger problem
+    needs more."""
+    key = (torch.cuda.current_device(), torch.cuda.current_stream().cuda_stream, bool(ln))
     ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         if ws is not None:
@@ -275,6 +373,7 @@ def attention_workspace(d) -> torch.Tensor:
 
 
 TUNE_CONV_HALO, TUNE_TAIL_STREAMK, TUNE_HALO_SPLIT, TUNE_TILE_GROUP, TUNE_LN_FUSE = 0, 1, 2, 3, 4
+TUNE_LN_SPIN, TUNE_LN_TEST_SKIP = 5, 6
 
 
 def gemm_tune(key: int, value: int):
@@ -282,7 +381,9 @@ def gemm_tune(key: int, value: int):
     on the LDS halo-window kernel, default on), TUNE_TAIL_STREAMK (tail-only stream-K for nearly empty last waves),
     TUNE_HALO_SPLIT (K part count of the flat-raster halo conv, 0 = automatic), TUNE_TILE_GROUP (tile rows per group
     in the 256-row GEMM kernels' tile order, 0 = the default 4), TUNE_LN_FUSE (LayerNorm fused into the residual
-    linears: 2 = default, whatever the tile choice; 1 = where it is the 192-row kernel; 0 = off)."""
+    linears: 2 = default, whatever the tile choice; 1 = where it is the 192-row kernel; 0 = off), TUNE_LN_SPIN (polls
+    of the fused LayerNorm's band barrier before it gives up, 0 = default), TUNE_LN_TEST_SKIP (test hook: the next n
+    fused launches drop one tile's statistics, so a band times out and the fault word is raised)."""
     check(lib().mapa_gemm_tune(key, value), "mapa_gemm_tune")
     _WS_NEED.clear()
 
@@ -349,7 +450,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     if need is None:
         need = _WS_NEED[key] = int(lib().mapa_gemm_workspace_bytes(ctypes.byref(d)))
     if need:
-        ws = gemm_workspace(need)
+        ws = gemm_workspace(need, ln=ln is not None)
         d.workspace, d.workspace_bytes = ws.data_ptr(), ws.numel()
     tok = _tic()
     if head_out is not None:

@@ -33,7 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from ... import _native as nat
-from ...parallel import force_collectives
+from ...parallel import force_collectives, force_overlap
 from .spec import RELEASED_INFO, InfoSharingSpec
 
 ENC_DIM, ENC_HEADS, PATCH, KPAD = 1024, 16, 14, 640
@@ -729,18 +729,25 @@ class MapaEngine:
         strides = dict(batch=1, heads=NH, seq_q=L, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C,
                        v_bstride=0, v_rstride=2 * C, o_bstride=0, o_rstride=C, scale=scale)
         overlap = hasattr(comm, "allgather_slots_async") and os.environ.get("MAPA_KV_OVERLAP", "1") != "0"
+        # MAPA_FORCE_OVERLAP=1 on a one-rank shard: the overlapped multi-rank branch with the second half of this
+        # rank's own keys standing in for the remote ones (parallel.force_overlap)
+        split_own = shard.world == 1 and overlap and force_overlap()
         if shard.world == 1 and not force_collectives():  # a one-rank group: every key is local
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
                           kv_segments=shard.kv_segments(), kind="attention_global", **strides)
-        elif not overlap or shard.world == 1:  # gather first (forced collectives on one rank: nothing remote)
+        elif not overlap or (shard.world == 1 and not split_own):  # gather first (forced collectives, one rank)
             comm.allgather_slots(kv_full, shard.max_rows)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=shard.total_kv,
                           kv_segments=shard.kv_segments(), kind="attention_global", **strides)
         else:
             handle = comm.allgather_slots_async(kv_full, shard.max_rows)
             segs = shard.kv_segments()
-            own = segs[shard.rank]
-            rest = [sg for r, sg in enumerate(segs) if r != shard.rank]
+            if split_own:
+                st, n = segs[0]
+                own, rest = (st, n // 2), [(st + n // 2, n - n // 2)]
+            else:
+                own = segs[shard.rank]
+                rest = [sg for r, sg in enumerate(segs) if r != shard.rank]
             lse_l = self._empty(NH, L, dtype=torch.float32)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=own[1], kv_segments=[own], lse=lse_l,
                           kind="attention_global", **strides)
@@ -959,14 +966,16 @@ class MapaEngine:
     @torch.no_grad()
     def run(self, imgs: torch.Tensor, taps: Optional[dict] = None, shard=None, comm=None,
             geo: Optional[GeoInputs] = None, dpt_chunk: Optional[int] = None,
-            pe_idx: Optional[torch.Tensor] = None, scenes: int = 1) -> Dict[str, torch.Tensor]:
+            pe_idx: Optional[torch.Tensor] = None, scenes: int = 1, fault=None) -> Dict[str, torch.Tensor]:
         """imgs: (V, 3, H, W) fp32 DINOv2-normalised on this device (B = 1 per view).  Returns the raw
         per-pixel / per-view outputs of MapAnything.forward, view-major.  With `shard`/`comm`, imgs are this
         rank's views only (parallel.ShardPlan.local_views) and the outputs are those views'.  `geo` carries the
         optional geometric inputs of these views (GeoInputs).  dpt_chunk: run the dense head over at most that many
         views at a time (memory_efficient_inference, model.py:1479-1516); None = all views at once.
         scenes = B > 1: imgs are B scenes of V views, scene-major ((B*V, 3, H, W), image b*V + v), run as one batch
-        (the reference's batched forward, model.py:687-721): outputs scene-major, metric_scaling_factor (B, 1)."""
+        (the reference's batched forward, model.py:687-721): outputs scene-major, metric_scaling_factor (B, 1).
+        fault: an armed _native.FaultSlot — the device fault word is published into it right after the transformer
+        (the last LayerNorm-fused launch), so the caller can check it while the heads still run."""
         if imgs.dim() != 4 or imgs.shape[1] != 3:
             raise AssertionError("images must be (V, 3, H, W)")
         VB, _, H, W = imgs.shape
@@ -995,6 +1004,8 @@ class MapaEngine:
                     first = self.head_rows(fused_f32[:VB * T])
             inter, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx,
                                           fused_f32=fused_f32, scenes=B)
+            if fault is not None:
+                fault.publish()
             if len(inter) == 3:
                 first, l11, l17 = inter
             else:

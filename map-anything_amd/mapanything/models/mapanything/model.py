@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from ... import _native as nat
-from ...parallel import force_collectives
+from ...parallel import comm_timeout, force_collectives, force_overlap
 from ...utils.inference import (postprocess_outputs, preprocess_input_views_for_inference,
                                 validate_input_views_for_inference)
 from .spec import InfoSharingSpec, aliases, canonical_spec, full_spec
@@ -324,6 +324,13 @@ class MapAnything:
                     warnings.warn(f"direct RCCL communicator unavailable ({err or 'on another rank'}); the sharded "
                                   "path runs eagerly on the process group")
                     self._shard_graphs = False
+        old = getattr(self, "_comm", None)
+        if old is not None and old is not comm:
+            # graphs captured against the previous communicator hold its RCCL handle: drop them, then release it
+            for k in [k for k in self._graphs if k[-1] is not None]:
+                del self._graphs[k]
+            if hasattr(old, "close"):
+                old.close()
         self._comm = comm
         self._gather = gather_outputs
         return self
@@ -432,6 +439,7 @@ class MapAnything:
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference),
                                scenes=B)
+        self._await_faults(plan)
         return self._finish(raw, plan, len(views), with_post=False, scenes=B)
 
     # entries a view may carry and still run in a batched-scene engine call (image-only, no geometric inputs)
@@ -481,9 +489,9 @@ class MapAnything:
         if (not self.hip_graphs or not shard_ok or geo is not None or dpt_chunk is not None
                 or nat._timing is not None or nat.SERIALIZE or imgs.device.type != "cuda"):
             return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx,
-                           scenes=scenes)
+                           scenes=scenes, fault=self._arm_fault())
         pkey = None if plan is None else (plan.world, plan.rank, tuple(plan.counts), force_collectives(),
-                                          os.environ.get("MAPA_KV_OVERLAP", "1"))
+                                          force_overlap(), os.environ.get("MAPA_KV_OVERLAP", "1"))
         key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index, scenes, pkey)
         comm = self._comm if plan is not None else None
         with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
@@ -494,16 +502,20 @@ class MapAnything:
                 side = torch.cuda.Stream(imgs.device)
                 side.wait_stream(torch.cuda.current_stream(imgs.device))
                 with torch.cuda.stream(side):  # eager warm-up: lazy packing, pos-embed caches
-                    eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
+                    eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes,
+                            fault=self._arm_fault())
+                    self._await_local_fault()
                 torch.cuda.current_stream(imgs.device).wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
+                gslot = nat.FaultSlot()  # the graph's own publish slot (its address is baked into the graph)
                 # captured on the warm-up stream: the per-stream GEMM / attention workspaces made in the warm-up
                 # are the ones the graph uses (no allocation or zero-fill inside the capture).  With a shard the
                 # capture is thread-local: the communicator's watchdog thread keeps querying its events meanwhile
                 mode = "global" if plan is None else "thread_local"
                 if plan is None:
                     with torch.cuda.graph(graph, stream=side, capture_error_mode=mode):
-                        static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
+                        static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes,
+                                             fault=gslot)
                 else:
                     # every rank captures the same collectives in the same order, so a capture that fails on one
                     # rank fails on all; the ranks still agree (one eager all-reduce) before any replays, and fall
@@ -511,7 +523,8 @@ class MapAnything:
                     err = None
                     try:
                         with torch.cuda.graph(graph, stream=side, capture_error_mode=mode):
-                            static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes)
+                            static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes,
+                                                 fault=gslot)
                     except Exception as e:  # noqa: BLE001 -- any capture failure: agree, then run eager
                         err = e
                         if os.environ.get("MAPA_GRAPH_DEBUG"):
@@ -525,22 +538,86 @@ class MapAnything:
                         from ...parallel import DistComm, RcclComm
 
                         if isinstance(self._comm, RcclComm):  # an aborted capture may leave its RCCL state unusable
-                            self._comm = DistComm(self._comm.group)
-                        return eng.run(imgs, shard=plan, comm=self._comm, pe_idx=pe_idx, scenes=scenes)
+                            old, self._comm = self._comm, DistComm(self._comm.group)
+                            old.close(abort=True)
+                        return eng.run(imgs, shard=plan, comm=self._comm, pe_idx=pe_idx, scenes=scenes,
+                                       fault=self._arm_fault())
                 # the side stream is kept with the graph: its handle keys the per-stream workspaces the graph
                 # captured (_native._WS/_AWS), so it must not be destroyed and its handle reused while the graph lives
-                entry = (graph, static_in, static_out, static_pe, side)
+                entry = (graph, static_in, static_out, static_pe, side, gslot)
                 self._graphs[key] = entry
                 while len(self._graphs) > self._MAX_GRAPHS:
                     self._graphs.popitem(last=False)
             else:
                 self._graphs.move_to_end(key)
-            graph, static_in, static_out, static_pe, _side = entry
+            graph, static_in, static_out, static_pe, _side, gslot = entry
             static_in.copy_(imgs)
             if static_pe is not None:
                 static_pe.copy_(pe_idx)
+            gslot.arm()
+            self._fault_state().pending = gslot
             graph.replay()
         return {k: v.clone() for k, v in static_out.items()}
+
+    # ----------------------------------------------------------------------------------- device fault channel
+    def _fault_state(self):
+        """Per-thread fault-channel state (the in-thread sharding tests drive one model from several rank threads):
+        .eager = this thread's slot for eager runs, .pending = the slot this thread's current call waits on."""
+        st = self.__dict__.get("_fault_tls")
+        if st is None:
+            import threading
+
+            st = self.__dict__.setdefault("_fault_tls", threading.local())
+        if not hasattr(st, "pending"):
+            st.eager, st.pending = None, None
+        return st
+
+    def _arm_fault(self):
+        """This thread's eager fault slot, armed; the run publishes the device fault word into it after the
+        transformer (engine.run), and the caller checks it before returning (_await_faults)."""
+        st = self._fault_state()
+        if st.eager is None:
+            st.eager = nat.FaultSlot()
+        st.eager.arm()
+        st.pending = st.eager
+        return st.eager
+
+    def _await_local_fault(self):
+        st = self._fault_state()
+        slot, st.pending = st.pending, None
+        if slot is not None:
+            slot.wait()
+
+    def _await_faults(self, plan):
+        """Wait for this call's fault publish (the GPU is past the transformer then and still has the heads queued,
+        so the wait costs no GPU time) and raise NativeError if a kernel set the device fault word — a LayerNorm-
+        fused band barrier that timed out (include/mapa.h fault channel): the outputs are then never returned.  A
+        sharded model that gathers outputs agrees first, so every rank raises together instead of one rank leaving
+        the others in the gather."""
+        err = None
+        st = self._fault_state()
+        slot, st.pending = st.pending, None
+        if slot is not None:
+            comm = self._comm if plan is not None else None
+            try:
+                if comm is None:
+                    slot.wait()
+                else:  # sharded: a hung collective never lets the forward reach its publish
+                    slot.wait(timeout_s=comm_timeout().total_seconds(), poll=getattr(comm, "check_async", None))
+            except nat.FaultTimeout as e:
+                from ...parallel import CommError
+
+                if hasattr(comm, "abort"):
+                    comm.abort()  # RCCL's kernels stop on the abort flag; the stream can drain
+                raise CommError(f"sharded forward on rank {plan.rank} did not complete: {e} (RCCL communicator "
+                                "aborted)") from e
+            except nat.NativeError as e:
+                err = e
+        if plan is not None and self._gather is not None and plan.world > 1:
+            if not self._comm.all_agree(err is None, self._device):
+                raise err or nat.NativeError("a device fault on another rank (include/mapa.h fault channel)")
+        elif err is not None:
+            raise err
 
     @torch.inference_mode()
     def infer(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False, use_amp: bool = True,
@@ -595,6 +672,7 @@ class MapAnything:
                                    edge_depth_threshold=edge_depth_threshold,
                                    apply_confidence_mask=apply_confidence_mask,
                                    confidence_percentile=confidence_percentile)
+        self._await_faults(plan)
         return self._finish(post, plan, len(views), with_post=True, scenes=B)
 
     def _dpt_chunk(self, memory_efficient: bool):

@@ -73,6 +73,7 @@ class DINOv2Encoder(_EngineModule):
         eng = self._eng()
         with torch.cuda.device(eng.device):
             enc = eng.encoder_features(img)
+            nat.check_faults()  # the LayerNorm-fused residual linears' band barriers (include/mapa.h fault channel)
         return ViTEncoderOutput(features=_chw(enc, B, H // PATCH, W // PATCH))
 
 
@@ -118,6 +119,7 @@ class MultiViewAlternatingAttentionTransformerIFR(_EngineModule):
                 for j, d in enumerate(idx):
                     inter[j][b] = taps[f"aat_l{d}"].reshape(V, h, w, D)
                     inter_tok[j][b] = taps[f"aat_l{d}_token"]
+            nat.check_faults()
 
         def pack(per_b, toks):
             views = [torch.stack([per_b[b][v] for b in range(B)], 0).permute(0, 3, 1, 2).contiguous()

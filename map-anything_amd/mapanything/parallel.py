@@ -29,8 +29,17 @@ import torch
 def force_collectives() -> bool:
     """Debug switch MAPA_FORCE_COLLECTIVES=1: a one-rank shard still runs the K/V all-gather (gather-first form) and
     the scale-token broadcast through its communicator, so the collective path — RCCL under HIP-graph capture
-    included — runs on a single GPU."""
-    return os.environ.get("MAPA_FORCE_COLLECTIVES", "0") == "1"
+    included — runs on a single GPU.  Implied by MAPA_FORCE_OVERLAP=1."""
+    return os.environ.get("MAPA_FORCE_COLLECTIVES", "0") == "1" or force_overlap()
+
+
+def force_overlap() -> bool:
+    """Debug switch MAPA_FORCE_OVERLAP=1: a one-rank shard runs the OVERLAPPED global layer of the multi-rank path —
+    the asynchronous all-gather on the communicator's side stream, attention of the local queries over the first
+    half of its own keys (treated as "local") with LSE, the join, attention over the second half (treated as
+    "remote"), and the LSE merge — so the N > 1 production branch (RCCL fork / join under HIP-graph capture
+    included) executes on a single GPU (engine._block_global_sharded)."""
+    return os.environ.get("MAPA_FORCE_OVERLAP", "0") == "1"
 
 
 class CommError(RuntimeError):
@@ -159,6 +168,12 @@ class DistComm:
         """In place: every rank's t = rank src's t."""
         self._call("scale-token broadcast", self.dist.broadcast, t, src, group=self.group)
 
+    def close(self, abort: bool = False):
+        """Nothing to release: the process group belongs to the caller."""
+
+    def check_async(self):
+        """Device-side collectives of this communicator have no asynchronous error state of their own."""
+
     def all_agree(self, ok: bool, device) -> bool:
         """True on every rank iff ok on every rank (an eager MIN all-reduce of one int, never captured)."""
         flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
@@ -191,9 +206,12 @@ class RcclComm(DistComm):
     RCCL directly on a communicator of its own (mapanything/rccl.py), so they can be captured with the kernels into
     the sharded forward's HIP graph; the host-side ones (output gather, the capture agreement) stay on the process
     group.  The overlapped all-gather runs on a side stream forked from and joined back into the caller's stream
-    (event record / wait: captured as graph edges).  An RCCL error raises CommError; a collective that never
-    completes is not timed out here (no watchdog over captured work) — MAPA_SHARD_GRAPHS=0 keeps the process group's
-    eager, watchdog-timed path."""
+    (event record / wait: captured as graph edges).  The communicator is created non-blocking and its init polled
+    against comm_timeout() (rccl.Communicator: a peer that fails inside its init makes this rank raise CommError
+    instead of hanging); an RCCL error raises CommError.  Captured collectives have no watchdog of their own: the
+    model's per-call fault wait (MapAnything._await_faults, bounded by comm_timeout()) polls check_async() and, if
+    the forward does not reach its fault publish in time, aborts the communicator (abort() stops RCCL's kernels)
+    and raises CommError."""
 
     def __init__(self, group=None, device=None):
         super().__init__(group)
@@ -212,6 +230,16 @@ class RcclComm(DistComm):
             fn(*a)
         except self._rccl_mod.RcclError as e:
             raise CommError(f"{what} failed on rank {self.rank} of {self.world}: {e}") from e
+
+    def check_async(self):
+        self._rc("RCCL", self._nccl.check_async)
+
+    def abort(self):
+        self._nccl.abort()
+
+    def close(self, abort: bool = False):
+        """Release the RCCL communicator (ncclCommFinalize + ncclCommDestroy, or ncclCommAbort after an error)."""
+        self._nccl.close(abort=abort)
 
     def allgather_slots(self, full: torch.Tensor, rows_per_slot: int):
         self._rc("K/V all-gather", self._nccl.all_gather_, full, rows_per_slot, torch.cuda.current_stream())

@@ -48,9 +48,12 @@ def test_two_process_view_sharding_over_distcomm(tmp_path):
 
 def test_one_rank_rccl_sharded_graph(tmp_path):
     """A real one-rank RCCL process group (tests/nccl1_worker.py, MAPA_FORCE_COLLECTIVES=1): the sharded forward with
-    its K/V all-gathers and scale-token broadcast through RCCL, eager and HIP-graph captured / replayed, in fp32 and
-    in the bf16 recipe.  Graph-replayed == eager bitwise; sharded == unsharded (fp32 within 2e-5: the sharded global
-    layers project Q and K/V in two GEMMs and attend through the segment table)."""
+    its K/V all-gathers and scale-token broadcast through RCCL (the direct, non-blocking-initialised communicator),
+    eager and HIP-graph captured / replayed, in fp32 and in the bf16 recipe — in the gather-first form and, with
+    MAPA_FORCE_OVERLAP=1, in the overlapped form every N > 1 global layer takes (side-stream all-gather forked and
+    joined inside the capture, local / remote attention, LSE merge).  Graph-replayed == eager bitwise; sharded ==
+    unsharded (fp32 within 2e-5: the sharded global layers project Q and K/V in two GEMMs, attend through the segment
+    table, and in the overlapped form merge two partials)."""
     out = str(tmp_path / "nccl1.json")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
@@ -59,8 +62,11 @@ def test_one_rank_rccl_sharded_graph(tmp_path):
     assert r.returncode == 0, _rank_errors(r)
     res = json.load(open(out))
     print("\n[one-rank RCCL sharded forward]", json.dumps(res, indent=1))
-    for prec in ("fp32", "bf16"):
-        d = res[prec]
-        assert d["sharded_graph_keys"] == 1, d
-        assert d["graph_eq_eager"] and d["replay_eq_eager"], d
-    assert all(e < 2e-5 for e in res["fp32"]["err_vs_single"].values()), res["fp32"]
+    for mode in ("gather", "overlap"):
+        for prec in ("fp32", "bf16"):
+            d = res[f"{mode}_{prec}"]
+            assert d["direct_rccl"] and d["sharded_graph_keys"] == 1, d
+            assert d["graph_eq_eager"] and d["replay_eq_eager"], d
+            assert d["replay_python_merges"] == 0, d  # the replay launches nothing from Python
+            assert d["eager_merges"] == (12 if mode == "overlap" else 0), d  # one merge per global layer
+        assert all(e < 2e-5 for e in res[f"{mode}_fp32"]["err_vs_single"].values()), res[f"{mode}_fp32"]

@@ -120,9 +120,9 @@ def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
 
 
 def _ln_flag(nat):
-    """Band-barrier timeout flags of the GEMM workspaces (include/mapa.h: int word 65535 of the head)."""
-    ws = list(nat._WS.values()) + nat._WS_RETIRED
-    return sum(int(w.view(torch.int32)[65535].item()) for w in ws if w.numel() >= 262144)
+    """The library's device fault word (include/mapa.h fault channel): MAPA_FAULT_LN_BARRIER if a band barrier of a
+    LayerNorm-fused launch gave up."""
+    return nat.fault_status(reset=False)
 
 
 # (M, N, K, gamma): the path's residual linears at 8 views (enc proj / fc2 on 192x256 tiles, aat proj / fc2 on
@@ -130,7 +130,8 @@ def _ln_flag(nat):
 # tile is still the automatic choice, else the library's GEMM + LayerNorm)
 @pytest.mark.parametrize("M,N,K,gamma", [(10960, 1024, 1024, True), (10960, 1024, 4096, True), (10953, 768, 768, False),
                                          (10953, 768, 3072, False), (150, 768, 768, False), (4001, 1024, 1024, True),
-                                         (21905, 768, 3072, False)])
+                                         (21905, 768, 3072, False), (80001, 1024, 1024, True),
+                                         (136901, 768, 768, False)])
 def test_gemm_layernorm_fused(nat, M, N, K, gamma):
     """mapa_gemm with ln_out (the next sub-block's LayerNorm fused into the residual linear): the fp32 residual
     stream bitwise equal to the plain GEMM's, the bf16 normalised rows within one bf16 rounding of the standalone
@@ -169,6 +170,59 @@ def test_gemm_layernorm_fused(nat, M, N, K, gamma):
         diff = (y.float() != ys.float()).float().mean().item()
         assert diff < 1e-3, diff  # statistics rounded differently flip at most a few bf16 roundings
     assert rel_l2(xa.cpu(), xs.cpu()) < 1e-6  # another tile kernel for the residual when the choice differed
+
+
+def test_gemm_layernorm_barrier_timeout_is_reported(nat):
+    """A band that never completes (the test hook drops tile (0, 0)'s statistics publish; MAPA_TUNE_LN_SPIN shortens
+    the bounded wait) must not hang and must not pass silently: the fault word carries MAPA_FAULT_LN_BARRIER, a
+    FaultSlot published after the launch raises, check_faults raises and resets, and the next call is clean — its
+    residual stream still bitwise the plain GEMM's, its LayerNorm rows identical to an undisturbed fused run."""
+    M, N, K = 10953, 768, 768
+    A = _rand(M, K, seed=81).to(torch.bfloat16)
+    W = _rand(N, K, scale=K ** -0.5, seed=82).to(torch.bfloat16)
+    b, x0 = _rand(N, seed=83), _rand(M, N, seed=84)
+    lw, lb = 1.0 + 0.2 * _rand(N, seed=85), 0.1 * _rand(N, seed=86)
+
+    def run():
+        x = x0.clone()
+        y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
+        nat.gemm(A, W, M, N, K, bias=b, resid1=x, out_f32=x, ln=(lw, lb, 1e-6, y))
+        return x, y
+
+    assert nat.fault_status(reset=True) == 0
+    x_ok, y_ok = run()
+    slot = nat.FaultSlot()
+    nat.gemm_tune(nat.TUNE_LN_SPIN, 4096)
+    nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 1)
+    try:
+        slot.arm()
+        x_bad, y_bad = run()
+        slot.publish()
+        with pytest.raises(nat.NativeError, match="LayerNorm"):
+            slot.wait(timeout_s=60)
+    finally:
+        nat.gemm_tune(nat.TUNE_LN_SPIN, 0)
+        nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 0)
+    assert nat.fault_status(reset=False) == 0  # the slot's raise reset the word
+    # the synchronous form reports it too
+    nat.gemm_tune(nat.TUNE_LN_SPIN, 4096)
+    nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 1)
+    try:
+        run()
+        torch.cuda.synchronize()
+    finally:
+        nat.gemm_tune(nat.TUNE_LN_SPIN, 0)
+        nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 0)
+    assert nat.fault_status(reset=False) & nat.FAULT_LN_BARRIER
+    with pytest.raises(nat.NativeError, match="LayerNorm"):
+        nat.check_faults()
+    assert nat.fault_status(reset=False) == 0
+    assert torch.equal(x_bad, x_ok)  # the residual stream never depends on the barrier
+    assert torch.equal(y_bad[192:], y_ok[192:])  # only band 0's normalised rows are invalid
+    x2, y2 = run()
+    torch.cuda.synchronize()
+    assert nat.fault_status(reset=False) == 0
+    assert torch.equal(x2, x_ok) and torch.equal(y2, y_ok)
 
 
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574])

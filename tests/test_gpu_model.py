@@ -538,6 +538,39 @@ def test_serialize_debug_mode_runs_and_matches(model):
         assert torch.equal(a[k], b[k]), k
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_infer_raises_on_layernorm_barrier_timeout(model, graphs):
+    """include/mapa.h fault channel end to end: one LayerNorm-fused launch loses a tile's statistics (test hook), its
+    band barrier gives up after the (shortened) bounded wait, and infer() raises NativeError instead of returning
+    outputs — eager, and through the HIP-graph path (the hook fires in the graph's eager warm-up).  The word is reset:
+    the next infer is clean and bit-identical to one before the fault."""
+    from mapanything import _native as nat
+
+    views = _views(CASES["cfg1_224"])
+    kw = dict(use_amp=True, apply_mask=False)
+    model.hip_graphs = graphs
+    try:
+        model._graphs.clear()
+        before = model.infer(views, **kw)
+        model._graphs.clear()
+        nat.gemm_tune(nat.TUNE_LN_SPIN, 4096)
+        nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 1)
+        try:
+            with pytest.raises(nat.NativeError, match="LayerNorm"):
+                model.infer(views, **kw)
+        finally:
+            nat.gemm_tune(nat.TUNE_LN_SPIN, 0)
+            nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 0)
+        assert nat.fault_status(reset=False) == 0
+        after = model.infer(views, **kw)
+    finally:
+        model.hip_graphs = True
+        model._graphs.clear()
+    for a, b in zip(before, after):
+        for k in ("pts3d", "conf", "cam_quats", "metric_scaling_factor"):
+            assert torch.equal(a[k], b[k]), k
+
+
 FP16_CASES = ["cfg1_224", "mm_224", "v2_518", "cfg2_518"]
 
 

@@ -175,3 +175,87 @@ def test_scale_token_broadcast_and_output_gather_gloo(world):
         assert r["all"] == (every, every_mask)
         assert r["rank0"][0] == (every if rank == 0 else own)
         assert r[None][0] == own
+
+
+class _FakeRccl:
+    """Stands in for librccl.so in rccl.Communicator (the init protocol only): the last rank fails inside its own
+    ncclCommInitRankConfig; the others see their non-blocking init stay in progress (peers that never arrive) or,
+    with mode "async_error", turn into an asynchronous error after a few polls."""
+
+    def __init__(self, rank, world, mode):
+        self.rank, self.world, self.mode = rank, world, mode
+        self.aborted, self.polls, self.blocking = 0, 0, None
+
+    def ncclGetUniqueId(self, uid):
+        return 0
+
+    def ncclCommInitRankConfig(self, pcomm, nranks, uid, rank, cfg):
+        self.blocking = cfg._obj.blocking
+        pcomm._obj.value = 0x1234  # the communicator object exists before the connection set-up
+        if rank == self.world - 1:
+            return 2  # ncclSystemError inside this rank's init
+        return 7  # ncclInProgress
+
+    def ncclCommGetAsyncError(self, comm, pst):
+        self.polls += 1
+        pst._obj.value = 3 if (self.mode == "async_error" and self.polls > 5) else 7
+        return 0
+
+    def ncclCommAbort(self, comm):
+        self.aborted += 1
+        return 0
+
+    def ncclGetErrorString(self, rc):
+        return {2: b"unhandled system error", 3: b"internal error", 7: b"in progress"}.get(rc, b"?")
+
+
+def _rccl_init_worker(rank, world, port, mode, q):
+    """rccl.Communicator's non-blocking init with a peer failing inside its init: every rank raises RcclError within
+    the timeout (the waiting ranks abort their half-built communicator), then the ranks agree to fall back — the
+    sequence MapAnything.enable_view_sharding runs before it keeps the process-group communicator."""
+    import time
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mapanything import rccl
+
+        fake = _FakeRccl(rank, world, mode)
+        t0 = time.monotonic()
+        err = None
+        try:
+            rccl.Communicator(None, None, lib_=fake, timeout_s=2.0)
+        except rccl.RcclError as e:
+            err = e
+        dt = time.monotonic() - t0
+        agreed = DistComm().all_agree(err is None, "cpu")
+        q.put((rank, type(err).__name__ if err else None, str(err), dt, fake.aborted, fake.blocking, agreed))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["timeout", "async_error"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_rccl_init_failure_raises_on_every_rank_within_timeout(world, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_init_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, kind, msg, dt, aborted, blocking, agreed in res:
+        assert blocking == 0, "the communicator must be created non-blocking"
+        assert kind is not None, f"rank {rank} did not raise"
+        assert not agreed, "every rank must agree to fall back"
+        assert dt < 10.0, (rank, dt)
+        if rank == world - 1:
+            assert kind == "RcclError" and "system error" in msg and aborted == 1
+        elif mode == "timeout":
+            assert kind == "RcclTimeout" and dt >= 2.0 and aborted == 1, (rank, kind, dt, aborted)
+        else:
+            assert kind == "RcclError" and "internal error" in msg and aborted == 1, (rank, kind, msg)
