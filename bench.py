@@ -68,6 +68,10 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--geometric", action="store_true",
                     help="cfg4 inputs: + intrinsics, 90%%-sparse depth_z, is_metric_scale on every view")
+    ap.add_argument("--cfg4-views", type=int, default=32,
+                    help="N=1: also time configs[3] (this many views, images + intrinsics + 90%%-sparse depth, "
+                         "metric) as the nested multimodal_cfg4 object; 0 = skip")
+    ap.add_argument("--cfg4-steps", type=int, default=5)
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", PROFILE_ROUND, "pmc_traffic.json"),
                     help="HBM bytes per launch from rocprofv3 FETCH_SIZE/WRITE_SIZE passes (tools/profile_summary.py)")
     ap.add_argument("--mfma-pmc-json", default=os.path.join(REPO, "profiles", PROFILE_ROUND, "pmc_mfma.json"),
@@ -137,6 +141,7 @@ def main():
         step()
     torch.cuda.synchronize()
     eng = model.engine()
+    shard_check = shard_graph_self_check(model, step, dist, dev) if world > 1 else None
 
     def timed(k):
         return timed_fn(step, k)
@@ -207,6 +212,10 @@ def main():
                    "vs_single_scene": (B * V_total * args.steps / bdt) / value}
         del b_views
         torch.cuda.empty_cache()
+
+    cfg4 = None
+    if world == 1 and args.cfg4_views and not args.geometric and not args.total_views:
+        cfg4 = bench_cfg4(model, amp, dev, H, W, args, timed_fn)
 
     strong = None
     if args.strong_views and not args.total_views and not args.geometric and args.strong_views >= world:
@@ -301,15 +310,83 @@ def main():
             "cross_view_attention": xattn,
             "cpu_baseline": cpu,
             "batched_scenes": batched,
+            "multimodal_cfg4": cfg4,
             "fast_mode_bf16_heads": fast,
             "strong_scaling": strong,
             # one GPU, or a view shard over RCCL (kernels and collectives captured together; MAPA_SHARD_GRAPHS=0 or a
-            # failed capture on any rank: eager)
-            "hip_graphs": bool(model.hip_graphs and not args.geometric and (world == 1 or model._shard_graphs)),
+            # failed capture on any rank: eager, with the reason)
+            "hip_graphs": bool(model.hip_graphs and (world == 1 or model._shard_graphs)),
+            "hip_graph_fallback": None if world == 1 else model.shard_graph_fallback,
+            "shard_graph_check": shard_check,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_cfg4(model, amp, dev, H, W, args, timed_fn):
+    """configs[3]: 32 views 518x518, images + intrinsics + 90 %-sparse depth_z + is_metric_scale on every view, one
+    infer per step on one GPU (the geometric encoders fp32-exact as split-precision GEMMs; HIP-graph replayed with
+    the ray / depth / camera inputs refreshed into the graph's static buffers), plus its own per-kernel times from
+    an eager timing pass of 2 steps."""
+    from mapanything.utils import synthetic
+
+    V = args.cfg4_views
+    imgs = synthetic.synthetic_images(V, H, W, seed=5)
+    Ks = synthetic.synthetic_intrinsics(V, H, W, seed=5)
+    Ds = synthetic.synthetic_sparse_depth(V, H, W, seed=5)
+    views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"], "intrinsics": torch.from_numpy(K).to(dev),
+              "depth_z": torch.from_numpy(D).to(dev), "is_metric_scale": torch.ones(1, dtype=torch.bool)}
+             for i, K, D in zip(imgs, Ks, Ds)]
+    del imgs, Ks, Ds
+
+    def step():
+        return model.infer(views, **amp)
+
+    step()  # warm-up: geometric weights packed, graph captured
+    graphs = sum(1 for k in model._graphs if k[5] is not None)
+    step()
+    dt = timed_fn(step, args.cfg4_steps)
+    per_kernel = None
+    if not args.no_kernel_timing:
+        eng = model.engine()
+        eng.enable_kernel_timing()
+        timed_fn(step, 2)
+        kt = eng.collect_kernel_timing()
+        per_kernel = {k: {"ms_per_step": v["ms"] / 2,
+                          "tflops": (v["flops"] / (v["ms"] * 1e-3) / 1e12) if v["flops"] else None}
+                      for k, v in kt.items()}
+    out = {"views": V, "value": V * args.cfg4_steps / dt, "unit": "views/s", "ms_per_step": dt / args.cfg4_steps * 1e3,
+           "steps": args.cfg4_steps, "warmup": 2, "hip_graphs": graphs > 0,
+           "workload": f"{V}-view {H}x{W} images + intrinsics + 90%-sparse depth_z + is_metric_scale, "
+                       "MapAnything.infer on 1 GPU (configs[3])",
+           "per_kernel": per_kernel}
+    del views
+    torch.cuda.empty_cache()
+    return out
+
+
+def shard_graph_self_check(model, step, dist, dev):
+    """N > 1: the first graph replay of the sharded forward against one eager sharded forward of the same views,
+    bitwise, on every rank (the warm-up captured the graph; a replay and an eager run issue the same kernels and
+    collectives in the same order).  Returns what every rank saw (MIN over ranks) and the collective path taken."""
+    from mapanything.parallel import RcclComm
+
+    graphs = sum(1 for k in model._graphs if k[-1] is not None)
+    was = model.hip_graphs
+    model.hip_graphs = False
+    eager = step()
+    model.hip_graphs = was
+    replay = step()
+    torch.cuda.synchronize()
+    keys = [k for k in ("pts3d", "conf", "depth_along_ray", "ray_directions", "cam_quats", "cam_trans",
+                        "metric_scaling_factor", "mask") if replay and replay[0] is not None and k in replay[0]]
+    same = all(torch.equal(a[k], b[k]) for a, b in zip(replay, eager) if a is not None for k in keys)
+    flags = torch.tensor([1 if same else 0, graphs], dtype=torch.int32, device=dev)
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    return {"graph_eq_eager_all_ranks": bool(flags[0].item()), "sharded_graphs_min_over_ranks": int(flags[1].item()),
+            "communicator": "direct RCCL (captured)" if isinstance(model._comm, RcclComm) else "process group (eager)",
+            "keys": keys}
 
 
 def _free_port() -> int:

@@ -66,9 +66,39 @@ class GeoInputs:
     cam_mask: List[bool] = field(default_factory=list)       # (V,)
     pose_metric: List[bool] = field(default_factory=list)    # (V,) is_metric_scale & use_pose_scale
     local_start: int = 0
+    # B > 1 batched scenes (no shard): every list / tensor above holds the B scenes' views scene-major (image b*V + v);
+    # the camera translations are normalised per scene (pose inputs over each scene's V views, model.py:792-896)
+    scenes: int = 1
 
     def empty(self) -> bool:
         return not self.ray_views and not self.depth_views and not any(self.cam_mask)
+
+    def signature(self) -> tuple:
+        """The host-side structure (which views carry which input, the metric flags): the HIP-graph key of a
+        geometric forward — the tensors are refreshed into the graph's static copies before every replay."""
+        shp = lambda t: None if t is None else tuple(t.shape)  # noqa: E731
+        return (tuple(self.ray_views), tuple(self.depth_views), tuple(self.depth_metric), tuple(self.cam_mask),
+                tuple(self.pose_metric), self.local_start, self.scenes, shp(self.rays), shp(self.depth),
+                shp(self.cam_quats), shp(self.cam_trans))
+
+    def tensors(self):
+        return ("rays", "depth", "cam_quats", "cam_trans")
+
+    def static_copy(self) -> "GeoInputs":
+        """The same inputs in fresh buffers (a captured graph's static inputs)."""
+        import copy
+
+        g = copy.copy(self)
+        for k in self.tensors():
+            t = getattr(self, k)
+            setattr(g, k, None if t is None else t.clone())
+        return g
+
+    def refresh_into(self, static: "GeoInputs"):
+        for k in self.tensors():
+            t = getattr(self, k)
+            if t is not None:
+                getattr(static, k).copy_(t)
 
 
 KBLOCK = 32  # channel block of the head convs' K order (include/mapa.h conv_kblock)
@@ -369,6 +399,20 @@ class MapaEngine:
     def _empty(self, *shape, dtype=None):
         return torch.empty(shape, dtype=dtype or self.lp, device=self.device)
 
+    def _const(self, vals, dtype):
+        """A small device tensor of host-built values (view indices, per-view masks / scales), cached by value: an
+        eager run fills the cache, so a HIP-graph capture of the same structure never copies host memory."""
+        key = (tuple(vals) if not isinstance(vals[0], (list, tuple)) else tuple(map(tuple, vals)), dtype)
+        cache = self.__dict__.setdefault("_consts", {})
+        t = cache.get(key)
+        if t is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise nat.NativeError("geometric-input constants must be built by an eager run before capture")
+            t = torch.tensor(vals, dtype=dtype).to(self.device)
+            torch.cuda.current_stream(self.device).synchronize()  # shared lazily built state (see geometric())
+            cache[key] = t
+        return t
+
     def _ln(self, x, rows, dim, w, b, *, y_f32=None, y_lp=None, y_s3=None, group=0, gstride=0, off=0, ldx=None):
         nat.layernorm(x, rows, dim, w, b, eps=LN_EPS, ldx=ldx, y_f32=y_f32, y_lp=y_lp, y_s3=y_s3, group=group,
                       group_stride=gstride, row_off=off)
@@ -496,12 +540,16 @@ class MapaEngine:
                 vecs.append(self._global_rep(log_nf.view(VB, 1), VB, 1, g["depth_scale_encoder"]))
                 scales.append(sc)
         if any(geo.cam_mask):
-            V = len(geo.cam_mask)
-            mask = torch.tensor([1 if m else 0 for m in geo.cam_mask], dtype=torch.uint8).to(dev, non_blocking=True)
-            q = self._empty(V, 4, dtype=f32)
-            t = self._empty(V, 3, dtype=f32)
-            lnf = self._empty(V, dtype=f32)
-            nat.pose_inputs(geo.cam_quats.contiguous(), geo.cam_trans.contiguous(), mask, V, q, t, lnf)
+            NV = len(geo.cam_mask)  # all views (of every scene)
+            V = NV // geo.scenes
+            mask = self._const([1 if m else 0 for m in geo.cam_mask], torch.uint8)
+            q = self._empty(NV, 4, dtype=f32)
+            t = self._empty(NV, 3, dtype=f32)
+            lnf = self._empty(NV, dtype=f32)
+            cq, ct = geo.cam_quats.contiguous(), geo.cam_trans.contiguous()
+            for b in range(geo.scenes):  # camera inputs in each scene's view-0 frame, translations normalised per scene
+                sl = slice(b * V, (b + 1) * V)
+                nat.pose_inputs(cq[sl], ct[sl], mask[sl], V, q[sl], t[sl], lnf[sl])
             s0 = geo.local_start
             cm = [1.0 if geo.cam_mask[s0 + v] else 0.0 for v in range(VB)]
             pm = [cm[v] if geo.pose_metric[s0 + v] else 0.0 for v in range(VB)]
@@ -514,7 +562,7 @@ class MapaEngine:
                 scales.append(pm)
         if vecs:
             vb = torch.stack(vecs, 0).contiguous()
-            sb = torch.tensor(scales, dtype=f32).to(dev, non_blocking=True)
+            sb = self._const(scales, f32)
             nat.add_view_vectors(enc, T, ENC_DIM, VB, vb, sb, len(vecs))
 
     def _dense_into(self, enc, data, views, VB, H, W, C, g, view_div=None):
@@ -524,7 +572,7 @@ class MapaEngine:
         T = hp * wp
         n = len(views)
         if n != VB:
-            idx = torch.tensor(views, dtype=torch.long).to(self.device, non_blocking=True)
+            idx = self._const(list(views), torch.long)
             data = data.index_select(0, idx)
             if view_div is not None:
                 view_div = view_div.index_select(0, idx)
@@ -983,8 +1031,9 @@ class MapaEngine:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
         B = scenes
-        if B > 1 and (shard is not None or geo is not None or taps is not None or VB % B):
-            raise ValueError("batched scenes run image-only, unsharded, without taps, with VB a multiple of B")
+        if B > 1 and (shard is not None or (geo is not None and geo.scenes != B) or taps is not None or VB % B):
+            raise ValueError("batched scenes run unsharded, without taps, with VB a multiple of B and geometric "
+                             "inputs batched the same way (GeoInputs.scenes)")
         with torch.cuda.device(self.device):
             fused_lp, fused_f32, (hp, wp) = self.encode(imgs, taps, geo, scenes=B)
             T = hp * wp

@@ -118,6 +118,8 @@ class MapAnything:
         # graph): off with MAPA_SHARD_GRAPHS=0 (eager launches, collectives through the process group and its
         # watchdog), or on every rank once any rank's capture has failed
         self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "1") != "0"
+        # why the sharded path runs eagerly (None while sharded graphs are on); bench.py reports it
+        self.shard_graph_fallback: Optional[str] = None if self._shard_graphs else "MAPA_SHARD_GRAPHS=0"
         self._modules: Dict[str, Any] = {}
         if pretrained_checkpoint_path is not None:
             self.load_checkpoint(pretrained_checkpoint_path)
@@ -324,6 +326,7 @@ class MapAnything:
                     warnings.warn(f"direct RCCL communicator unavailable ({err or 'on another rank'}); the sharded "
                                   "path runs eagerly on the process group")
                     self._shard_graphs = False
+                    self.shard_graph_fallback = f"direct RCCL communicator unavailable: {err or 'on another rank'}"
         old = getattr(self, "_comm", None)
         if old is not None and old is not comm:
             # graphs captured against the previous communicator hold its RCCL handle: drop them, then release it
@@ -421,6 +424,39 @@ class MapAnything:
                                      else torch.zeros(1, 3, device=dev, dtype=f32) for v in range(V)], 0)
         return None if g.empty() else g
 
+    def _geo_inputs_scenes(self, views, B, metrics, **use):
+        """GeoInputs of B batched scenes (unsharded): each scene's inputs as _geo_inputs builds them (its own metric
+        flags, its own camera normalisation frame), concatenated scene-major (image b*V + v) with GeoInputs.scenes =
+        B; scenes without an input kind get the reference's zero / identity fill and a cleared mask.  metrics[b]:
+        scene b's per-view is_metric_scale flags (read on the host before the inputs moved to the device)."""
+        from .engine import GeoInputs
+
+        per = [self._geo_inputs(self._scene_views(views, b, B), None, metrics[b], **use) for b in range(B)]
+        if all(g is None for g in per):
+            return None
+        V = len(views)
+        H, W = views[0]["img"].shape[-2:]
+        dev, f32 = self._device, torch.float32
+        g = GeoInputs(local_start=0, scenes=B)
+        if any(p is not None and p.ray_views for p in per):
+            g.rays = torch.cat([p.rays if p is not None and p.ray_views else torch.zeros(V, H, W, 3, device=dev, dtype=f32)
+                                for p in per], 0).contiguous()
+            g.ray_views = [b * V + i for b, p in enumerate(per) if p is not None for i in p.ray_views]
+        if any(p is not None and p.depth_views for p in per):
+            g.depth = torch.cat([p.depth if p is not None and p.depth_views else torch.zeros(V, H, W, device=dev, dtype=f32)
+                                 for p in per], 0).contiguous()
+            g.depth_views = [b * V + i for b, p in enumerate(per) if p is not None for i in p.depth_views]
+            g.depth_metric = [bool(p is not None and p.depth_views and p.depth_metric[i]) for p in per for i in range(V)]
+        if any(p is not None and any(p.cam_mask) for p in per):
+            ident_q = torch.tensor([[0.0, 0.0, 0.0, 1.0]], device=dev, dtype=f32).expand(V, 4)
+            has = [p is not None and any(p.cam_mask) for p in per]
+            g.cam_quats = torch.cat([p.cam_quats if h else ident_q for p, h in zip(per, has)], 0).contiguous()
+            g.cam_trans = torch.cat([p.cam_trans if h else torch.zeros(V, 3, device=dev, dtype=f32)
+                                     for p, h in zip(per, has)], 0).contiguous()
+            g.cam_mask = [bool(h and p.cam_mask[i]) for p, h in zip(per, has) for i in range(V)]
+            g.pose_metric = [bool(h and p.pose_metric[i]) for p, h in zip(per, has) for i in range(V)]
+        return None if g.empty() else g
+
     def forward(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False,
                 precision: Optional[str] = None) -> List[Dict[str, torch.Tensor]]:
         """Raw per-view outputs of model.py:1657-2152 (pts3d, pts3d_cam, ray_directions, depth_along_ray,
@@ -435,21 +471,25 @@ class MapAnything:
         if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
         local, plan = self._local_views(views)
-        geo = self._geo_inputs(views, plan, self._metric_flags(views)) if B == 1 else None
+        geo = self._geo_inputs(views, plan, self._metric_flags(views)) if B == 1 else \
+            self._geo_inputs_scenes(views, B, [self._metric_flags(self._scene_views(views, b, B)) for b in range(B)])
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference),
                                scenes=B)
         self._await_faults(plan)
         return self._finish(raw, plan, len(views), with_post=False, scenes=B)
 
-    # entries a view may carry and still run in a batched-scene engine call (image-only, no geometric inputs)
-    _IMAGE_ONLY_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label"))
+    # entries a view may carry and still run in a batched-scene engine call: images and every geometric input
+    # (raw as infer() takes them, and preprocessed as forward() takes them)
+    _BATCHABLE_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label",
+                                 "intrinsics", "ray_directions", "depth_z", "camera_poses", "ray_directions_cam",
+                                 "depth_along_ray", "camera_pose_quats", "camera_pose_trans"))
 
     def _batchable(self, views) -> bool:
-        """B > 1 scenes run as ONE engine call (encoder / frame layers / heads over all B x V images, the global
-        layers per scene; the reference's batched forward, model.py:687-721) when the views carry images only and
-        the model is not view-sharded; otherwise scene by scene."""
-        return self._comm is None and all(set(v.keys()) <= self._IMAGE_ONLY_KEYS for v in views)
+        """B > 1 scenes run as ONE engine call (encoder, geometric encoders, frame layers and heads over all B x V
+        images; the global layers and the camera-translation normalisation per scene; the reference's batched
+        forward, model.py:687-721) unless the model is view-sharded; then scene by scene."""
+        return self._comm is None and all(set(v.keys()) <= self._BATCHABLE_KEYS for v in views)
 
     @staticmethod
     def _scene_major(imgs, B: int):
@@ -477,32 +517,35 @@ class MapAnything:
         return torch.cat([torch.zeros(1, dtype=torch.int64), rest.to(torch.int64)]).to(self._device)
 
     def _run_engine(self, eng, imgs, plan, geo, dpt_chunk, scenes: int = 1):
-        """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: no geometric inputs, no
+        """MapaEngine.run, replayed from a captured HIP graph when the call is graph-safe: no
         chunked dense head, no per-launch kernel timing, not in the serialize debug mode (every launch checked,
         nat.SERIALIZE), and either one device or a view shard whose communicator enqueues its collectives on the
         device (DistComm over RCCL: the K/V all-gathers and the scale-token broadcast are captured with the
         kernels, forking to and joining from the communicator's stream).  The graph is keyed on the image batch
-        shape, precision and shard plan; inputs are copied into its static buffer and outputs cloned out of it, so
-        results never alias a later call's."""
+        shape, precision, shard plan and the geometric inputs' structure (GeoInputs.signature: which views carry
+        rays / depth / poses, the metric flags); images, view-PE rows and geometric tensors are copied into its
+        static buffers and outputs cloned out of it, so results never alias a later call's."""
         pe_idx = self._view_pe_rows(plan.num_views if plan is not None else imgs.shape[0] // scenes)
         shard_ok = plan is None or (self._shard_graphs and getattr(self._comm, "graph_safe", False))
-        if (not self.hip_graphs or not shard_ok or geo is not None or dpt_chunk is not None
+        if (not self.hip_graphs or not shard_ok or dpt_chunk is not None
                 or nat._timing is not None or nat.SERIALIZE or imgs.device.type != "cuda"):
             return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, dpt_chunk=dpt_chunk, pe_idx=pe_idx,
                            scenes=scenes, fault=self._arm_fault())
         pkey = None if plan is None else (plan.world, plan.rank, tuple(plan.counts), force_collectives(),
                                           force_overlap(), os.environ.get("MAPA_KV_OVERLAP", "1"))
-        key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index, scenes, pkey)
+        key = (eng.precision, eng.heads, tuple(imgs.shape), imgs.device.index, scenes,
+               None if geo is None else geo.signature(), pkey)
         comm = self._comm if plan is not None else None
         with torch.inference_mode():  # static buffers are inference tensors whichever mode the first call ran in
             entry = self._graphs.get(key)
             if entry is None:
                 static_in = imgs.clone()
                 static_pe = None if pe_idx is None else pe_idx.clone()  # refreshed before every replay
+                static_geo = None if geo is None else geo.static_copy()  # geometric inputs: likewise
                 side = torch.cuda.Stream(imgs.device)
                 side.wait_stream(torch.cuda.current_stream(imgs.device))
                 with torch.cuda.stream(side):  # eager warm-up: lazy packing, pos-embed caches
-                    eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes,
+                    eng.run(static_in, shard=plan, comm=comm, geo=static_geo, pe_idx=static_pe, scenes=scenes,
                             fault=self._arm_fault())
                     self._await_local_fault()
                 torch.cuda.current_stream(imgs.device).wait_stream(side)
@@ -514,8 +557,8 @@ class MapAnything:
                 mode = "global" if plan is None else "thread_local"
                 if plan is None:
                     with torch.cuda.graph(graph, stream=side, capture_error_mode=mode):
-                        static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes,
-                                             fault=gslot)
+                        static_out = eng.run(static_in, shard=plan, comm=comm, geo=static_geo, pe_idx=static_pe,
+                                             scenes=scenes, fault=gslot)
                 else:
                     # every rank captures the same collectives in the same order, so a capture that fails on one
                     # rank fails on all; the ranks still agree (one eager all-reduce) before any replays, and fall
@@ -523,8 +566,8 @@ class MapAnything:
                     err = None
                     try:
                         with torch.cuda.graph(graph, stream=side, capture_error_mode=mode):
-                            static_out = eng.run(static_in, shard=plan, comm=comm, pe_idx=static_pe, scenes=scenes,
-                                                 fault=gslot)
+                            static_out = eng.run(static_in, shard=plan, comm=comm, geo=static_geo, pe_idx=static_pe,
+                                                 scenes=scenes, fault=gslot)
                     except Exception as e:  # noqa: BLE001 -- any capture failure: agree, then run eager
                         err = e
                         if os.environ.get("MAPA_GRAPH_DEBUG"):
@@ -535,25 +578,28 @@ class MapAnything:
                         warnings.warn(f"sharded HIP-graph capture failed ({err or 'on another rank'}); "
                                       "running the sharded path eagerly on the process group")
                         self._shard_graphs = False
+                        self.shard_graph_fallback = f"sharded HIP-graph capture failed: {err or 'on another rank'}"
                         from ...parallel import DistComm, RcclComm
 
                         if isinstance(self._comm, RcclComm):  # an aborted capture may leave its RCCL state unusable
                             old, self._comm = self._comm, DistComm(self._comm.group)
                             old.close(abort=True)
-                        return eng.run(imgs, shard=plan, comm=self._comm, pe_idx=pe_idx, scenes=scenes,
+                        return eng.run(imgs, shard=plan, comm=self._comm, geo=geo, pe_idx=pe_idx, scenes=scenes,
                                        fault=self._arm_fault())
                 # the side stream is kept with the graph: its handle keys the per-stream workspaces the graph
                 # captured (_native._WS/_AWS), so it must not be destroyed and its handle reused while the graph lives
-                entry = (graph, static_in, static_out, static_pe, side, gslot)
+                entry = (graph, static_in, static_out, static_pe, side, gslot, static_geo)
                 self._graphs[key] = entry
                 while len(self._graphs) > self._MAX_GRAPHS:
                     self._graphs.popitem(last=False)
             else:
                 self._graphs.move_to_end(key)
-            graph, static_in, static_out, static_pe, _side, gslot = entry
+            graph, static_in, static_out, static_pe, _side, gslot, static_geo = entry
             static_in.copy_(imgs)
             if static_pe is not None:
                 static_pe.copy_(pe_idx)
+            if static_geo is not None:
+                geo.refresh_into(static_geo)
             gslot.arm()
             self._fault_state().pending = gslot
             graph.replay()
@@ -648,7 +694,9 @@ class MapAnything:
                       ignore_depth_scale_inputs=ignore_depth_scale_inputs,
                       ignore_pose_scale_inputs=ignore_pose_scale_inputs)
             return self._merge_scenes([self.infer(self._scene_views(validated, b, B), **kw) for b in range(B)])
-        metric = self._metric_flags(validated)   # host-side flags read before the H2D copies
+        # host-side flags read before the H2D copies (per scene when B > 1)
+        metric = self._metric_flags(validated) if B == 1 else \
+            [self._metric_flags(self._scene_views(validated, b, B)) for b in range(B)]
         for v in validated:
             for k in list(v.keys()):
                 if k in ("instance", "idx", "true_shape", "data_norm_type"):
@@ -660,10 +708,13 @@ class MapAnything:
                                  for x in v[k])
         processed = preprocess_input_views_for_inference(validated)
         local, plan = self._local_views(processed)
-        geo = self._geo_inputs(processed, plan, metric, use_calibration=not ignore_calibration_inputs,
-                               use_depth=not ignore_depth_inputs, use_pose=not ignore_pose_inputs,
-                               use_depth_scale=not ignore_depth_scale_inputs,
-                               use_pose_scale=not ignore_pose_scale_inputs)
+        use = dict(use_calibration=not ignore_calibration_inputs, use_depth=not ignore_depth_inputs,
+                   use_pose=not ignore_pose_inputs, use_depth_scale=not ignore_depth_scale_inputs,
+                   use_pose_scale=not ignore_pose_scale_inputs)
+        if B == 1:
+            geo = self._geo_inputs(processed, plan, metric, **use)
+        else:
+            geo = self._geo_inputs_scenes(processed, B, metric, **use)
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         eng = self.engine(precision)
         raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)

@@ -274,6 +274,63 @@ def test_batched_scenes_match_scene_by_scene(model, precision):
             assert torch.equal(batched[v][k], again[v][k]) and torch.equal(batched[v][k], eager[v][k]), (v, k)
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_batched_geometric_scenes_match_scene_by_scene(model, precision):
+    """B = 2 scenes x 3 views with mixed geometric inputs (b2_224's inputs: intrinsics everywhere, depth on views 0
+    and 2, poses on views 0 and 1, different metric flags per scene) as ONE engine call — the dense geometric
+    encoders over every image that has the input, the camera inputs normalised per scene — against each scene run
+    alone (fp32 2e-5, bf16 twice the b2 spread), and the graph-replayed batched call == its eager run bitwise."""
+    views = _views(CASES["b2_224"])
+    kw = dict(use_amp=precision == "bf16", apply_mask=False)
+    assert model._batchable(views)
+    model._graphs.clear()
+    batched = model.infer(views, **kw)
+    assert any(k[4] == 2 and k[5] is not None for k in model._graphs), "batched geometric call graph-captured"
+    again = model.infer(views, **kw)  # graph replay
+    model.hip_graphs = False
+    try:
+        eager = model.infer(views, **kw)
+        per = [model.infer(model._scene_views(views, b, 2), **kw) for b in range(2)]
+    finally:
+        model.hip_graphs = True
+    spread = _spread("b2_224")
+    for v in range(3):
+        for k in ("pts3d", "conf", "depth_along_ray", "ray_directions", "cam_quats", "cam_trans", "intrinsics",
+                  "metric_scaling_factor"):
+            tol = 2e-5 if precision == "fp32" else 2 * spread["out_" + k]
+            ref = torch.cat([per[b][v][k] for b in range(2)], 0)
+            e = rel_l2(batched[v][k].float().cpu().numpy(), ref.float().cpu().numpy())
+            print(f"  view {v} {k:22s} {e:.3e} (bound {tol:.1e})")
+            assert e < tol, (v, k, e, tol)
+            assert torch.equal(batched[v][k], again[v][k]) and torch.equal(batched[v][k], eager[v][k]), (v, k)
+
+
+@pytest.mark.parametrize("name", ["mm_224", "mixed_224", "cfg4_518"])
+def test_geometric_hip_graph_replay_matches_eager(model, name):
+    """The geometric path is graph-captured (static ray / depth / camera buffers refreshed before every replay, the
+    graph keyed on which views carry which input): a replay with NEW inputs of the same structure == the eager
+    run of those inputs, bitwise (bf16 recipe)."""
+    case = dict(CASES[name])
+    kw = dict(use_amp=True, apply_mask=False)
+    model._graphs.clear()
+    first = model.infer(_views(case), **kw)  # captures
+    assert any(k[5] is not None for k in model._graphs), "geometric call graph-captured"
+    case["seed"] = case["seed"] + 100
+    views2 = _views(case)
+    replay = model.infer(views2, **kw)
+    model.hip_graphs = False
+    try:
+        eager = model.infer(views2, **kw)
+    finally:
+        model.hip_graphs = True
+    model._graphs.clear()
+    assert not torch.equal(first[0]["pts3d"], replay[0]["pts3d"])
+    for a, b in zip(replay, eager):
+        assert set(a) == set(b) and {"pts3d", "intrinsics", "metric_scaling_factor"} <= set(a)
+        for k in a:
+            assert torch.equal(a[k], b[k]), k
+
+
 def test_fp32_geometric_fused_tap(model, golden):
     """Encoder + ray / depth / depth-scale / camera features + fusion LayerNorm against the reference tap."""
     from mapanything.utils.inference import (preprocess_input_views_for_inference,
@@ -418,7 +475,7 @@ def test_hip_graph_replay_matches_eager(model, precision):
     assert model.hip_graphs
     g_a = model._run_engine(eng, imgs_a, None, None, None)
     g_b = model._run_engine(eng, imgs_b, None, None, None)  # replay of the graph captured by the first call
-    assert (precision, eng.heads, tuple(imgs_a.shape), imgs_a.device.index, 1, None) in model._graphs
+    assert (precision, eng.heads, tuple(imgs_a.shape), imgs_a.device.index, 1, None, None) in model._graphs
     for k in eager_a:
         assert torch.equal(g_a[k], eager_a[k]), k
         assert torch.equal(g_b[k], eager_b[k]), k
