@@ -20,6 +20,8 @@
 //    buffers).  Counted vmcnt over the groups still in flight + raw s_barrier (no drain in the loop).
 //  * The 9 taps of a slice are unrolled: vmcnt depths, tap shifts and window staging are compile-time, and every A
 //    fragment read is one of 8 per-slice base addresses + an immediate (no per-read VALU, few SALU per step).
+#include <type_traits>
+
 #include "gemm_internal.h"
 
 namespace mapa_gemm_impl {
@@ -121,27 +123,52 @@ __device__ __forceinline__ int win_chunk(int pos, int wp) { return (((pos & 1) <
 
 // DMA of K tile kt's W tile into ring slot `slot` (a device function, not a lambda in the kernel: with a lambda the
 // host pass drops the kernel's launch stub)
+// (buffer loads from the tile's W rows: the per-lane part of the address is a 32-bit offset, the K offset rides in
+// soffset — no 64-bit per-lane pointers live across the K loop)
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
 template <int BN, int BH>
-__device__ __forceinline__ void stage_w(char* wring, int slot, int wave, const char* const* w_src, int64_t koff) {
+__device__ __forceinline__ void stage_w(char* wring, int slot, int wave, __amdgpu_buffer_rsrc_t wr, const int* w_off,
+                                        int koff) {
   using C = HCfg<BN, BH>;
   char* dst = wring + slot * C::WT + wave * 1024;
 #pragma unroll
-  for (int i = 0; i < C::NWG; ++i) __builtin_amdgcn_global_load_lds(w_src[i] + koff, dst + i * 8192, 16, 0, 0);
+  for (int i = 0; i < C::NWG; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(wr, (lds_ptr_t)(dst + i * 8192), 16, w_off[i], koff, 0, 0);
 }
-// DMA of the input window of 32-channel slice `slice` into window buffer slice & 1 (dummy: the zero page into that
-// buffer — the uniform group past the last slice, which nothing reads)
-template <int BN, int BH>
-__device__ __forceinline__ void stage_win(const GemmArgs& p, char* wins, int slice, int wave, const int64_t* wsrc,
-                                          const bool* wok, bool dummy = false) {
+// DMA of the input window of the 32 physical channels starting at `ch` into window buffer `buf` (dummy: the zero
+// page into that buffer — the uniform group past the last slice, which nothing reads)
+// wsrc[r]: element offset of this thread's piece r from abase (-1: outside the map, the zero page)
+template <bool WIDE> struct WinOff { typedef int type; };
+template <> struct WinOff<true> { typedef int64_t type; };
+template <int BN, int BH, typename OffT>
+__device__ __forceinline__ void stage_win_t(const char* abase, char* wins, int buf, int64_t ch, int wave,
+                                            const OffT* wsrc, bool dummy) {
   using C = HCfg<BN, BH>;
   const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
-  const char* abase = reinterpret_cast<const char*>(p.A);
-  const int64_t ch = dummy ? 0 : split_col(p, slice * 32);
-  char* wd = wins + (slice & 1) * C::WBYTES + wave * 1024;
+  if (dummy) ch = 0;
+  char* wd = wins + buf * C::WBYTES + wave * 1024;
 #pragma unroll
   for (int r = 0; r < C::WROUNDS; ++r)
-    __builtin_amdgcn_global_load_lds(wok[r] && !dummy ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16,
+    __builtin_amdgcn_global_load_lds(wsrc[r] >= 0 && !dummy ? abase + (wsrc[r] + ch) * 2 : zero, wd + r * (HT * 16), 16,
                                      0, 0);
+}
+// 2-D blocks: the window lies in one image; a buffer descriptor over that image, a 32-bit byte offset per piece
+// (pieces outside the map carry an offset past the descriptor's range: the buffer load returns zeros) and the
+// channel offset in soffset
+template <int BN, int BH>
+__device__ __forceinline__ void stage_win(__amdgpu_buffer_rsrc_t ir, char* wins, int buf, int64_t ch, int wave,
+                                          const int* wsrc, bool dummy) {
+  using C = HCfg<BN, BH>;
+  char* wd = wins + buf * C::WBYTES + wave * 1024;
+  const int so = dummy ? 0 : (int)ch * 2;
+#pragma unroll
+  for (int r = 0; r < C::WROUNDS; ++r)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ir, (lds_ptr_t)(wd + r * (HT * 16)), 16, wsrc[r], so, 0, 0);
+}
+template <int BN, int BH>
+__device__ __forceinline__ void stage_win(const char* abase, char* wins, int buf, int64_t ch, int wave,
+                                          const int64_t* wsrc, bool dummy) {
+  stage_win_t<BN, BH, int64_t>(abase, wins, buf, ch, wave, wsrc, dummy);
 }
 
 template <int BN, bool HO = false, int BH = 16, bool FLAT = false>
@@ -175,8 +202,12 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   const int s_hi = FLAT ? (int)((int64_t)(kp + 1) * nslice / sp.nsplit) : nslice;
 
   // ---- window staging geometry (this thread's WROUNDS pieces; pixel offsets are slice-invariant)
-  int64_t wsrc[C::WROUNDS];
-  bool wok[C::WROUNDS];
+  // FLAT windows span images (offsets from A); a 2-D block's window lies in one image: 32-bit offsets from its base
+  typename WinOff<FLAT>::type wsrc[C::WROUNDS];
+  const char* abase = reinterpret_cast<const char*>(p.A) +
+                      (FLAT ? 0 : (int64_t)img * p.cv_IH * p.cv_IW * p.cv_Cp * 2);
+  const int img_bytes = FLAT ? 0 : p.cv_IH * p.cv_IW * p.cv_Cp * 2;  // < 2^31 (launch_conv_halo checks)
+  const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc((void*)abase, 0, img_bytes, 0x00020000);
 #pragma unroll
   for (int r = 0; r < C::WROUNDS; ++r) {
     const int q = r * HT + tid;
@@ -184,23 +215,25 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
     const int cs = win_chunk(cl, wp);  // LDS position cl holds channel chunk cs
     if constexpr (FLAT) {
       int im, iy, ix;  // window position wp = raster position fb*256 - Wp - 1 + wp
-      wok[r] = wp < 256 + 2 * Wp + 2 &&
-               mapa_idx::flat_pixel(fb * 256 - Wp - 1 + wp, Wp, Hp, p.cv_OH, p.cv_OW, imgs, im, iy, ix);
-      wsrc[r] = wok[r] ? ((int64_t)(im * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
+      const bool ok = wp < 256 + 2 * Wp + 2 &&
+                      mapa_idx::flat_pixel(fb * 256 - Wp - 1 + wp, Wp, Hp, p.cv_OH, p.cv_OW, imgs, im, iy, ix);
+      wsrc[r] = ok ? ((int64_t)(im * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : -1;
     } else {
       const int wy = wp / WE, wx = wp - wy * WE;
       const int iy = by * BH - 1 + wy, ix = bx * BW - 1 + wx;
-      wok[r] = q < C::WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
-      wsrc[r] = wok[r] ? ((int64_t)(img * p.cv_IH + iy) * p.cv_IW + ix) * p.cv_Cp + cs * 8 : 0;
+      const bool ok = q < C::WPIECES && iy >= 0 && iy < p.cv_IH && ix >= 0 && ix < p.cv_IW;
+      wsrc[r] = ok ? ((iy * p.cv_IW + ix) * p.cv_Cp + cs * 8) * 2 : 0x7ff00000;  // bytes in the image; past it: 0
     }
   }
   // ---- W staging geometry: instruction i of this wave covers ring rows (i*8 + wave)*16 + [0, 16)
-  const char* w_src[C::NWG];
+  int w_src[C::NWG];  // byte offsets from the tile's first W row
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<const char*>(p.W) + (int64_t)bn * p.ldw * 2), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int i = 0; i < C::NWG; ++i) {
     const int r = (i * 8 + wave) * 16 + (lane >> 2);
     const int sc = (lane & 3) ^ swz64(r);
-    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)(bn + r) * p.ldw + sc * 8) * 2;
+    w_src[i] = (r * (int)p.ldw + sc * 8) * 2;
   }
   f32x4 acc[C::FM][C::FN];
 #pragma unroll
@@ -220,43 +253,87 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
   // c mod 8 only -> a_off[c % 8] + c*64, an immediate offset for every (tap, row) pair.  FLAT: the tap shift
   // dy*Wp + dx is a runtime value, so each tap gets one address (+ i*1024 per block row i: 16 positions on)
 
-  // K loop: slices of 32 channels, the 9 taps of a slice unrolled, so the tap shift, the vmcnt depth of every step
-  // and which steps stage a window are compile-time constants.  K tile kt = slice*9 + tap lives in ring slot
-  // (kt - 9 s_lo) % S (`so`); the DMA group issued at step kt is W tile kt+S-1 (+ the next slice's window when kt+S-1
-  // starts it).  Every step issues exactly one group, also past the end (the last slice re-stages the last W tile
-  // and its own window into slots / the buffer nobody reads any more), so the counted waits hold in every slice with
-  // no last-slice branch: a peeled last slice spilled VGPRs, and scratch traffic inside a counted-vmcnt region breaks
-  // the count (a spill store can retire before an older LDS-DMA).
+  // K loop over A-slices (the 32 physical channels one window holds), the K steps of a slice unrolled, so the tap
+  // shift, the vmcnt depth of every step and which steps stage a window are compile-time constants.  Each step
+  // consumes one W tile from ring slot `so`; the DMA group issued at step q is W step q+S-1 (+ the next A-slice's
+  // window when q+S-1 starts it).  Every step issues exactly one group, also past the end (the last slice re-stages
+  // the last W tile and a dummy window into slots / the buffer nobody reads any more), so the counted waits hold in
+  // every slice with no last-slice branch: a peeled last slice spilled VGPRs, and scratch traffic inside a
+  // counted-vmcnt region breaks the count (a spill store can retire before an older LDS-DMA).
+  //  * plain operands (and the flat-raster split-K parts): A-slice = logical slice s, 9 steps (one per tap), W step
+  //    q at K column (s_lo*9 + q)*32;
+  //  * split-precision operands (the fp32-exact heads: logical K blocks [hi | hi | lo] against W [hi | lo | hi]): the
+  //    NH hi slices first, each window staged ONCE for both of its logical slices — 18 steps, (tap, w_hi) then (tap,
+  //    w_lo), the A fragments read at the first and reused at the second (a third fewer window DMAs and a quarter
+  //    fewer LDS fragment reads than visiting the hi slice twice) — then the NH lo slices, 9 steps each.  Same MFMAs
+  //    per output, accumulated in another order.
+  const bool paired = !FLAT && p.sp_half != 0x7fffffff;
+  const int NH = paired ? p.sp_half / 32 : 0;
+  const int n_aslice = paired ? 2 * NH : s_hi - s_lo;
   const int64_t kfirst = (int64_t)s_lo * 9 * 64;
   const int64_t klast = ((int64_t)s_hi * 9 - 1) * 64;
-  stage_w<BN, BH>(wring, 0, wave, w_src, kfirst);  // group 0: the first W tile + the first slice's window
-  stage_win<BN, BH>(p, wins, s_lo, wave, wsrc, wok);
+  // W source offsets (bytes), branch-free inside the unrolled bodies: step r of A-slice a stages from
+  // base(a) + (r & 1) * odd(a) + (r >> 1) * pair(a) — a paired hi slice: base a*576, odd = the w_lo block (NH*576),
+  // pair = 64 (one tap); a 9-step slice: base (its logical slice)*576, odd 64, pair 128 (r * 64); past the last
+  // slice: the last W tile again (dummy groups).
+  const int hop = NH * 576;
+  const int kfirst32 = s_lo * 576, klast32 = (s_hi * 9 - 1) * 64;  // K byte offsets fit 32 bits (K <= 9 * 2^12)
+  // the W step sequence of A-slice a: {base, odd, pair} as above (a >= n_aslice: the dummy groups past the end)
+  auto wbase = [&](int a) __attribute__((always_inline)) -> int {
+    return a >= n_aslice ? klast32 : a < NH ? a * 576 : paired ? (a + NH) * 576 : kfirst32 + a * 576;
+  };
+  // physical channel of A-slice a (its window)
+  auto aslice_ch = [&](int a) __attribute__((always_inline)) -> int64_t {
+    return paired ? (int64_t)a * 32 : (int64_t)split_col(p, (s_lo + a) * 32);
+  };
+  {
+    const int b0 = wbase(0);
+    const int odd0 = NH > 0 ? hop : 64, pair0 = NH > 0 ? 64 : 128;
+    stage_w<BN, BH>(wring, 0, wave, wr, w_src, b0);  // group 0: the first W tile + the first A-slice's window
+    if constexpr (FLAT) stage_win<BN, BH>(abase, wins, 0, aslice_ch(0), wave, wsrc, false);
+    else stage_win<BN, BH>(ir, wins, 0, aslice_ch(0), wave, wsrc, false);
 #pragma unroll
-  for (int s0 = 1; s0 < C::S - 1; ++s0) stage_w<BN, BH>(wring, s0, wave, w_src, kfirst + (int64_t)s0 * 64);
+    for (int s0 = 1; s0 < C::S - 1; ++s0) stage_w<BN, BH>(wring, s0, wave, wr, w_src, b0 + (s0 & 1) * odd0 + (s0 >> 1) * pair0);
+  }
   int so = 0;
-  int64_t koff = kfirst + (int64_t)(C::S - 1) * 64;  // W source offset of the tile staged next (kt + S - 1)
-  for (int s = s_lo; s < s_hi; ++s) {
+  auto slice_body = [&](int a, auto steps_tag) __attribute__((always_inline)) {
+    constexpr int STEPS = decltype(steps_tag)::value;
+    constexpr bool PAIRED = STEPS == 18;
+    // W offsets: this slice (its type is this body's) and the next (paired, 9-step or past the end)
+    const int bc = wbase(a), bn_ = wbase(a + 1);
+    const bool nlast = a + 1 >= n_aslice, npair = a + 1 < NH;
+    const int odd_n = nlast ? 0 : npair ? hop : 64, pair_n = nlast ? 0 : npair ? 64 : 128;
     // recomputed per slice (8 VGPRs live in the slice loop, not 8 more hoisted across it): the empty asm hides
     // wp0's loop invariance from LICM
     int wpl = wp0;
     asm volatile("" : "+v"(wpl));
-    const int woff = (int)(wins - lds) + (s & 1) * C::WBYTES;
+    const int woff = (int)(wins - lds) + (a & 1) * C::WBYTES;
     int a_off[8];
     if constexpr (!FLAT) {
 #pragma unroll
       for (int r = 0; r < 8; ++r) a_off[r] = wpl * 64 + (win_pos(g, wpl + r) << 4) + woff;
     }
 #pragma unroll
-    for (int tap = 0; tap < 9; ++tap) {
-      // groups issued after kt's, still allowed in flight: W tiles kt+1 .. kt+S-2, plus the window riding with the
-      // next slice's first tap
-      vm_wait(C::NWG * (C::S - 2) + (tap >= 11 - C::S ? C::WROUNDS : 0));
+    for (int st = 0; st < STEPS; ++st) {
+      const int tap = PAIRED ? st >> 1 : st;
+      // groups issued after this step's W tile, still allowed in flight: W tiles +1 .. +S-2, plus the window riding
+      // with the next A-slice's first step (issued at step STEPS - S + 1)
+      vm_wait(C::NWG * (C::S - 2) + (st >= STEPS - C::S + 2 ? C::WROUNDS : 0));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // kt landed everywhere; every wave is done with kt-1 (its slot is re-staged next)
+      __builtin_amdgcn_s_barrier();  // this tile landed everywhere; every wave is done with the last (re-staged next)
       __builtin_amdgcn_sched_barrier(0);
-      stage_w<BN, BH>(wring, so == 0 ? C::S - 1 : so - 1, wave, w_src, koff < klast ? koff : klast);
-      if (tap + C::S - 1 == 9) stage_win<BN, BH>(p, wins, s + 1, wave, wsrc, wok, s + 1 == s_hi);
-      koff += 64;
+      {
+        const int r = st + C::S - 1;  // the W step this group stages: in this slice, or r - STEPS in the next
+        int ko;
+        if (r < STEPS) ko = bc + (PAIRED ? (r & 1) * hop + (r >> 1) * 64 : r * 64);
+        else ko = bn_ + ((r - STEPS) & 1) * odd_n + ((r - STEPS) >> 1) * pair_n;
+        stage_w<BN, BH>(wring, so == 0 ? C::S - 1 : so - 1, wave, wr, w_src, ko);
+      }
+      if (st == STEPS - C::S + 1) {
+        const int64_t nch = a + 1 < n_aslice ? aslice_ch(a + 1) : 0;
+        if constexpr (FLAT) stage_win<BN, BH>(abase, wins, (a + 1) & 1, nch, wave, wsrc, a + 1 == n_aslice);
+        else stage_win<BN, BH>(ir, wins, (a + 1) & 1, nch, wave, wsrc, a + 1 == n_aslice);
+      }
       const char* Ws = wring + so * C::WT + b_off;
       so = so + 1 == C::S ? 0 : so + 1;
       b8 b[C::FN];
@@ -269,19 +346,26 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
       }
 #pragma unroll
       for (int i = 0; i < C::FM; ++i) {
-        b8 a;
+        b8 ai;
         if constexpr (FLAT) {
-          a = *reinterpret_cast<const b8*>(at + i * 1024);
+          ai = *reinterpret_cast<const b8*>(at + i * 1024);
         } else {
           const int c = (tap / 3 + i) * WE + tap % 3;  // window pixel offset of (tap, block row i)
-          a = *reinterpret_cast<const b8*>(lds + a_off[c & 7] + c * 64);
+          ai = *reinterpret_cast<const b8*>(lds + a_off[c & 7] + c * 64);
         }
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ai, b[j], acc[i][j], 0, 0, 0);
       }
     }
+  };
+  int a = 0;
+  if constexpr (!FLAT) {
+#pragma unroll 1
+    for (; a < NH; ++a) slice_body(a, std::integral_constant<int, 18>());
   }
+#pragma unroll 1
+  for (; a < n_aslice; ++a) slice_body(a, std::integral_constant<int, 9>());
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();  // LDS becomes the epilogue staging area
 
@@ -449,8 +533,12 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
 // bn: 256 or 128 output channels per tile (0 = 256 when N % 256 == 0, else 128); bh: block rows (16, or 8 with
 // bn 256).  Needs a bf16 stride-1 conv in the
 // channel-block-major K order with 32-channel slices (conv_kblock == 32); returns false otherwise.
+// one image of the A operand must be addressable by the window's 32-bit buffer offsets
+static bool halo_img_ok(const GemmArgs& a) { return (int64_t)a.cv_IH * a.cv_IW * a.cv_Cp * 2 < 0x7ff00000LL; }
+
 bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh) {
   if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
+  if (!halo_img_ok(a)) return false;
   if (bn == 0) bn = a.N % 256 == 0 ? 256 : 128;
   if (bh == 8 && bn != 256) return false;
   if (a.N % bn != 0 || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
@@ -523,6 +611,7 @@ bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b
                               float* conf, float* logits, uint8_t* mask, hipStream_t stream) {
   if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
   if (a.N != 128 || !a.bias || a.act != MAPA_ACT_RELU || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
+  if (!halo_img_ok(a)) return false;
   const int hw = a.cv_OH * a.cv_OW;
   const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + 15) / 16) * ((a.cv_OW + BW - 1) / BW);
   if (tiles >= (int64_t(1) << 31)) return false;

@@ -115,7 +115,10 @@ def main():
         for name, n, H, W_, C, Co, *st in CONVS:  # optional 7th field: stride
             stride = st[0] if st else 1
             OH, OW = (H - 1) // stride + 1, (W_ - 1) // stride + 1
-            x = (torch.randn(n, H, W_, C, device="cuda") * 0.5).to(dt)
+            # KB_SPLIT=1: C is the logical [hi | hi | lo] width of a split-precision operand (the fp32-exact heads):
+            # the stored operand is [hi | lo] (2C/3 per pixel) and the weight is tagged as split-packed
+            split = bool(os.environ.get("KB_SPLIT")) and C % 3 == 0 and (C // 3) % 32 == 0
+            x = (torch.randn(n, H, W_, 2 * C // 3 if split else C, device="cuda") * 0.5).to(dt)
             w0 = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(dt)
             b = torch.randn(Co, device="cuda")
             o = torch.empty(n * OH * OW, Co, device="cuda", dtype=dt)
@@ -126,6 +129,8 @@ def main():
                 if kb and C % kb == 0:
                     w = w0.view(Co, 9, C // kb, kb).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
                     w._mapa_kblock = kb
+                if split:
+                    w._mapa_split = True
                 combos += [(var, kb, w) for var in VARIANTS]
 
             def runc(var, w):
