@@ -643,6 +643,9 @@ class MapAnything:
         err = None
         st = self._fault_state()
         slot, st.pending = st.pending, None
+        if slot is not None and os.environ.get("MAPA_FAULT_WAIT", "1") == "0":  # A/B switch: publish, never wait
+            slot.armed = False
+            slot = None
         if slot is not None:
             comm = self._comm if plan is not None else None
             try:
