@@ -662,7 +662,7 @@ class MapAnything:
                                 "aborted)") from e
             except nat.NativeError as e:
                 err = e
-        if plan is not None and self._gather is not None and plan.world > 1:
+        if plan is not None and self._gather is not None and plan.world > 1 and hasattr(self._comm, "all_agree"):
             if not self._comm.all_agree(err is None, self._device):
                 raise err or nat.NativeError("a device fault on another rank (include/mapa.h fault channel)")
         elif err is not None:

@@ -305,6 +305,14 @@ class ThreadComm:
                 torch.cuda.current_stream().synchronize()
         self._barrier.wait()
 
+    def all_agree(self, ok: bool, device=None) -> bool:
+        """True on every rank thread iff ok on every one (barrier-exchanged flags)."""
+        self._bufs[self.rank] = bool(ok)
+        self._barrier.wait()
+        res = all(bool(b) for b in self._bufs)
+        self._barrier.wait()
+        return res
+
     def gather_views(self, local: torch.Tensor, counts: List[int], dst: Optional[int]) -> Optional[torch.Tensor]:
         if local.is_cuda:
             torch.cuda.current_stream().synchronize()
