@@ -330,10 +330,18 @@ __device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const Epi
   }
   if constexpr (MODE == 1) {
     if (p.act == MAPA_ACT_GELU) {
+      if (p.lp_f16) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v0[e] = gelu_erf(v0[e]);
-        v1[e] = gelu_erf(v1[e]);
+        for (int e = 0; e < 4; ++e) {
+          v0[e] = gelu_erf(v0[e]);
+          v1[e] = gelu_erf(v1[e]);
+        }
+      } else {  // bf16 output only: the cheaper tail fit, 1/256 of the output's ulp (mapa_common.h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v0[e] = gelu_bf16out(v0[e]);
+          v1[e] = gelu_bf16out(v1[e]);
+        }
       }
     }
     uint4 u;

@@ -87,6 +87,37 @@ def test_gemm_gelu_epilogue_fp32_exactness(nat, dtype):
     assert bool((err <= 8 * ulp + 1e-7 * pre.abs().double()).all()), float((err / (ulp + 1e-30)).max())
 
 
+@pytest.mark.parametrize("variant", [0, 2570, 2571, 2574])
+def test_gemm_gelu_bf16_output(nat, variant):
+    """The bf16-only GELU epilogue (epi_mode 1, the transformer fc1: mapa_common.h gelu_bf16out, a degree-8 fit of
+    the normal tail, 2^-16 relative): every output within one bf16 rounding of torch's exact-erf GELU of the same
+    kernel's fp32 pre-activation, and rounded differently from it in well under 1 % of the elements."""
+    M, N, K = 2741, 3072, 768
+    A = (_rand(M, K, seed=90) * 1.5).to(torch.bfloat16)
+    W = _rand(N, K, scale=K ** -0.5, seed=91).to(torch.bfloat16)
+    b = _rand(N, seed=92)
+    pre = torch.empty(M, N, device="cuda")
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(A, W, M, N, K, bias=b, out_f32=pre)
+        nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=out)
+        torch.cuda.synchronize()
+    finally:
+        nat.gemm_set_variant(0)
+    # x * Phi(x) with an accurate tail (F.gelu's 0.5 x (1 + erf(x / sqrt 2)) cancels to -0 below x ~ -5.9 even in
+    # fp64; the kernel keeps the true tail, e.g. GELU(-8.38) = -2.2e-16)
+    xd = pre.double()
+    ref = xd * 0.5 * torch.special.erfc(-xd * 0.7071067811865476)  # Phi(x) through erfc: no cancellation
+    assert float(pre.abs().max()) > 4.0 and float(pre.min()) < -6.0  # the tail is exercised
+    err = (out.double() - ref).abs()
+    assert bool((err <= ref.abs() * 2.0 ** -8 + 1e-30).all()), float((err / ref.abs().clamp_min(1e-30)).max())
+    flips = (out != ref.float().to(torch.bfloat16)).float().mean().item()
+    assert flips < 5e-3, flips
+    # against torch's own GELU: identical up to those tail values (absolute 1e-15) and rounding flips
+    assert float((out.double() - F.gelu(xd)).abs().max()) <= float(F.gelu(xd).abs().max()) * 2.0 ** -8
+
+
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2571, 2568, 2572, 2573, 2574, 2587])
 @pytest.mark.parametrize("M,N,K", [(10960, 1024, 4096), (10960, 768, 3072), (3000, 200, 264), (513, 136, 72),
                                    (3000, 200, 256), (10960, 3072, 1024), (700, 4100, 128)])

@@ -85,12 +85,19 @@ def main():
             x = torch.randn(M, N, device="cuda") if resid else None
             gam = torch.randn(N, device="cuda") * 0.1 if resid else None
             gelu = name.endswith("fc1") and not os.environ.get("KB_NO_RESID")  # the MLP's first linear: GELU epilogue
+            # KB_LN=1: the residual linears with the next sub-block's LayerNorm fused (mapa_gemm_desc.ln_*, bf16 out)
+            lnargs = None
+            if resid and os.environ.get("KB_LN"):
+                lnargs = (torch.randn(N, device="cuda"), torch.randn(N, device="cuda"), 1e-6,
+                          torch.empty(M, N, device="cuda", dtype=dt))
 
             def run(var, gm=0):
                 def f():
                     nat.gemm_set_variant(var)
                     nat.gemm_tune(nat.TUNE_TILE_GROUP, gm)
-                    if resid:
+                    if resid and lnargs is not None:
+                        nat.gemm(A, W, M, N, K, bias=b, gamma=gam, resid1=x, out_f32=x, ln=lnargs)
+                    elif resid:
                         nat.gemm(A, W, M, N, K, bias=b, gamma=gam, resid1=x, out_f32=x)
                     elif gelu:
                         nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=o)
