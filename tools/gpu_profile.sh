@@ -6,12 +6,14 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out/prof gpurun_out/prof_e gpurun_out/pmc_f gpurun_out/pmc_w gpurun_out/pmc_m
-B="python bench.py --no-cpu-baseline --no-fast-mode --strong-views 0 --batch-scenes 0"
-# PART=1: steps 1-2, PART=2: steps 3-4 (each under gpurun's 20-minute limit); default both
-PART=${PART:-12}
+B="python bench.py --no-cpu-baseline --no-fast-mode --strong-views 0 --batch-scenes 0 --cfg4-views 0"
+# PART=1: step 1, PART=e: step 2, PART=2: steps 3-4 (each under gpurun's 20-minute limit); default all
+PART=${PART:-1e2}
 if [[ $PART == *1* ]]; then
 # 1. the driver's exact bench command (BENCH_r*.cmd) under the kernel tracer
 timeout -k 10 700 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_rocprof.json 2> gpurun_out/rocprof.err || { tail -20 gpurun_out/rocprof.err; exit 1; }
+fi
+if [[ $PART == *e* ]]; then
 export MAPA_HIP_GRAPHS=0
 S="--steps 2 --warmup 1 --no-kernel-timing"
 MAPA_LAUNCH_SHAPES=1 MAPA_LAUNCH_LOG=gpurun_out/prof_e/launch_log.json timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/prof_e -o run --output-format csv -- $B $S > gpurun_out/prof_e.log 2>&1 || { tail -20 gpurun_out/prof_e.log; exit 1; }

@@ -58,8 +58,14 @@ def dispatch_kinds(names, log_path, keep_shape=False):
     a_log = [k for k in log if k.startswith("attention")]
     gi = ai = 0
     out = []
+    prev_ln = False
     for n in names:
-        if _is_gemm(n):
+        # an LN-fused call is cut into launches of at most the co-resident grid (gemm_big.hip launch_gemm_big_ln):
+        # back-to-back LN-kernel dispatches are one logged call
+        is_ln = re.search(r"gemm_big_kernel<[^>]*, true>", n) is not None
+        if is_ln and prev_ln:
+            out.append(out[-1])
+        elif _is_gemm(n):
             out.append(g_log[gi] if gi < len(g_log) else None)
             gi += 1
         elif "attn_fwd" in n:
@@ -67,6 +73,7 @@ def dispatch_kinds(names, log_path, keep_shape=False):
             ai += 1
         else:
             out.append(None)
+        prev_ln = is_ln
     if gi != len(g_log) or ai != len(a_log):
         raise SystemExit(f"launch log does not match the trace: {gi}/{len(g_log)} gemm, {ai}/{len(a_log)} attention")
     return out
