@@ -177,8 +177,8 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *   MAPA_TUNE_TILE_GROUP (default 0 = 4): the 256-row data-parallel GEMM kernels walk each XCD's tile range in
  *     groups of this many tile rows (all tile columns of a group before the next group).
  *   MAPA_TUNE_LN_FUSE (default 2, or the environment's MAPA_LN_FUSE): 2 = ln_out requests run on the LayerNorm-fused
- *     kernel whatever the automatic tile choice of the shape; 1 = only where that choice is the 192-row kernel; 0 =
- *     always as a separate mapa_layernorm launch (A/B).
+ *     kernel whatever the automatic tile choice of the shape; 1 = only where that choice is the 192-row kernel; 3 =
+ *     only N % 256 == 0 (the 192x256-tile form); 0 = always as a separate mapa_layernorm launch (A/B).
  *   MAPA_TUNE_LN_SPIN (default 0 = 2^22): polls of the fused LayerNorm's band barrier before it gives up.
  *   MAPA_TUNE_LN_TEST_SKIP (test hook, default 0): the next `value` LayerNorm-fused launches each have one tile
  *     (band 0, column tile 0) skip its statistics publish, so band 0 times out and raises MAPA_FAULT_LN_BARRIER. */

@@ -340,6 +340,7 @@ static int pick_ln_fused(const mapa_gemm_desc* d, int variant, int sk) {
   if (g_ln_fuse < 0) g_ln_fuse = getenv("MAPA_LN_FUSE") ? atoi(getenv("MAPA_LN_FUSE")) : 2;
   if (!d->ln_out || !g_ln_fuse || d->dtype != MAPA_BF16 || d->a_mode != MAPA_A_DENSE || d->a_split || sk) return 0;
   if (g_ln_fuse == 2) return d->N % 256 == 0 ? 14 : d->N % 192 == 0 ? 15 : 0;
+  if (g_ln_fuse == 3) return d->N % 256 == 0 ? 14 : 0;  // A/B: the 192x256 form only (whole model: = mode 2)
   return variant == 2574 ? 14 : variant == 2587 ? 15 : 0;
 }
 static int pick_flat(const GemmArgs& a) {
@@ -557,7 +558,7 @@ extern "C" int mapa_gemm_tune(int key, int value) {
   if (key == MAPA_TUNE_CONV_HALO) g_halo = value == 2 || value == 3 ? value : value ? 1 : 0;
   else if (key == MAPA_TUNE_HALO_SPLIT) g_halo_split = value;
   else if (key == MAPA_TUNE_TILE_GROUP) g_tile_gm = value ? value : 4;
-  else if (key == MAPA_TUNE_LN_FUSE) g_ln_fuse = value == 2 ? 2 : value ? 1 : 0;
+  else if (key == MAPA_TUNE_LN_FUSE) g_ln_fuse = value >= 2 && value <= 3 ? value : value ? 1 : 0;
   else g_tail_sk = value ? 1 : 0;
   return 0;
 }

@@ -812,14 +812,15 @@ class MapaEngine:
         return L if next_ln is not None else 0
 
     # ----------------------------------------------------------------------------------------------- DPT
-    def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None, head=None):
+    def dpt(self, fused_lp, l11, l17, fin_lp, VB, hp, wp, H, W, taps=None, head=None, join=None):
         """DPTFeature + DPTRegressionProcessor (dpt.py:180-311).  Inputs are head operands (_hop rows); fused_lp
         is the first DPT input — the fused encoder features (ENC_DIM) or, with three info-sharing taps
         (model.py:1748-1768), the first tap; its width comes from the packed weight.  Returns the ReLU'd 128-ch
         hidden map at HxW (fp32 in split mode, else lp), or None when `head` (see dpt_regress) took the dense head
-        into the last conv."""
+        into the last conv.  join: called right before the first kernel that reads `head`'s pose / scale rows (the
+        pose / scale heads' branch, run_heads)."""
         owned = [self.dpt_feature(fused_lp, l11, l17, fin_lp, VB, hp, wp, taps)[0]]
-        return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W, head)  # freed after its first conv
+        return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W, head, join)  # freed after its first conv
 
     def fused_head_out(self):
         """Whether the regressor's conv2 can carry the dense head in its epilogue (mapa_regressor_head_out: bf16
@@ -894,7 +895,7 @@ class MapaEngine:
         feat_lp = self._upsample_outconv(o, n, h0, w0, 1, lowp=True, taps=t)
         return feat_lp, (t["dpt_feature"] if t is not None else None)
 
-    def dpt_regress(self, feat_lp, n, hf, wf, H, W, head=None):
+    def dpt_regress(self, feat_lp, n, hf, wf, H, W, head=None, join=None):
         """DPTRegressionProcessor up to the last ReLU (dpt.py:285-311): conv3x3 256->128 at 8x, bilinear
         (align_corners) to HxW, conv3x3 128->128 + ReLU -> hidden [n*H*W][128] (fp32 in split mode, else lp).
         feat_lp (a head operand) may be a one-element list, handed over so that the 8x map is freed as soon as it
@@ -912,6 +913,8 @@ class MapaEngine:
         nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u, split_out=self.hsplit)
         del r1
         if head is not None:
+            if join is not None:
+                join()
             self._hconv3(r1u, n, H, W, 128, w.reg_c2, 128, bias=w.reg_b2, act=nat.ACT_RELU,
                          head_out=(w.reg_w6, w.reg_b6) + tuple(head))
             return None
@@ -968,6 +971,16 @@ class MapaEngine:
         return out
 
     # ------------------------------------------------------------------------------------- pose / scale
+    def _head_stream(self):
+        """The side stream of the pose / scale heads' branch (run_heads), one per engine; None runs them in line
+        (MAPA_HEAD_BRANCH=0, A/B)."""
+        if os.environ.get("MAPA_HEAD_BRANCH", "1") == "0":
+            return None
+        st = self.__dict__.get("_side_stream")
+        if st is None:
+            st = self._side_stream = torch.cuda.Stream(self.device)
+        return st
+
     def pose(self, fin_lp, VB, T, taps=None):
         """PoseHead (pose_head.py:50-159) on the final features (a head operand) -> raw (VB, 7)."""
         w = self.w
@@ -1074,17 +1087,36 @@ class MapaEngine:
         B = scenes
         V = VB // B
         with torch.cuda.device(self.device):
-            pose_raw = self.pose(fin_lp, VB, T, taps)
-            scale_raw = self.scale(tok, taps)
             pose_out = self._empty(VB, 19, dtype=torch.float32)
             scale = self._empty(B, dtype=torch.float32)
             poses44 = self._empty(VB, 4, 4, dtype=torch.float32)
-            for b in range(B):  # each scene's views take its own metric scale
-                sl = slice(b * V, (b + 1) * V)
-                nat.pose_scale_finalize(pose_raw[sl], scale_raw[b:b + 1], V, 1, pose_out[sl], scale[b:b + 1],
-                                        poses44[sl])
             # one scale per image for the dense head when scenes are batched (image i: scale[i // V])
-            scale_img = scale if B == 1 else scale.repeat_interleave(V)
+            scale_img = scale if B == 1 else self._empty(VB, dtype=torch.float32)
+            # The pose and scale heads depend only on the transformer's outputs and feed only the last DPT conv (its
+            # fused dense head): they run as a branch on a side stream, forked here and joined right before that conv,
+            # so their small, under-filling launches (7 GEMMs over 301 tiles, pooling, MLPs) overlap the DPT's.
+            # Every side-stream segment starts behind all earlier work of the main stream (wait_stream), and the
+            # branch's own temporaries never leave it, so the caching allocator's per-stream reuse stays safe; the
+            # outputs above are main-stream buffers.  Captured as a fork / join of the HIP graph.
+            side = self._head_stream()
+            cur = torch.cuda.current_stream(self.device)
+            if side is not None:
+                side.wait_stream(cur)
+            with torch.cuda.stream(side if side is not None else cur):
+                pose_raw = self.pose(fin_lp, VB, T, taps)
+                scale_raw = self.scale(tok, taps)
+                for b in range(B):  # each scene's views take its own metric scale
+                    sl = slice(b * V, (b + 1) * V)
+                    nat.pose_scale_finalize(pose_raw[sl], scale_raw[b:b + 1], V, 1, pose_out[sl], scale[b:b + 1],
+                                            poses44[sl])
+                if B > 1:
+                    scale_img.view(B, V).copy_(scale.view(B, 1).expand(B, V))
+            joined = [side is None]
+
+            def join():
+                if not joined[0]:
+                    cur.wait_stream(side)
+                    joined[0] = True
             f = torch.float32
             out = dict(
                 pts3d=self._empty(VB, H, W, 3, dtype=f), pts3d_cam=self._empty(VB, H, W, 3, dtype=f),
@@ -1101,11 +1133,14 @@ class MapaEngine:
                 outs = tuple(out[k][v0:v0 + n] for k in ("pts3d", "pts3d_cam", "ray_directions", "depth_along_ray",
                                                          "conf", "non_ambiguous_mask_logits", "non_ambiguous_mask"))
                 hid = self.dpt(first[r0:r1], l11[r0:r1], l17[r0:r1], fin_lp[r0:r1], n, hp, wp, H, W,
-                               taps if n == VB else None, head=(pose_out[v0:v0 + n],) + sc + outs if fuse else None)
+                               taps if n == VB else None, head=(pose_out[v0:v0 + n],) + sc + outs if fuse else None,
+                               join=join)
                 if not fuse:  # the unfused head's batch = scales: scale[i % batch] (one scale, or one per image)
+                    join()
                     nat.dense_head_out(hid, n, H * W, self.w.reg_w6, self.w.reg_b6, pose_out[v0:v0 + n], sc[0],
                                        1 if B == 1 else n, *outs)
                 del hid
+            join()
             out["cam_trans"] = pose_out[:, 0:3]
             out["cam_quats"] = pose_out[:, 3:7]
             out["metric_scaling_factor"] = scale.view(B, 1)

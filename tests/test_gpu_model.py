@@ -482,6 +482,30 @@ def test_hip_graph_replay_matches_eager(model, precision):
     assert not torch.equal(g_a["pts3d"], g_b["pts3d"])
 
 
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_pose_scale_head_branch_matches_inline(model, precision, monkeypatch):
+    """The pose / scale heads run on a side-stream branch joined before the last DPT conv (run_heads): the same
+    kernels on the same inputs, so every output is bit-identical to running them in line, eager and captured, and
+    with the unfused dense head (MAPA_FUSED_HEAD=0, joined before dense_head_out) as well."""
+    eng = model.engine(precision)
+    imgs = torch.cat([v["img"] for v in _views(dict(views=3, h=224, w=294, seed=21))], 0).cuda()
+    monkeypatch.setenv("MAPA_HEAD_BRANCH", "0")
+    inline = eng.run(imgs)
+    monkeypatch.setenv("MAPA_HEAD_BRANCH", "1")
+    branch = eng.run(imgs)
+    graph = model._run_engine(eng, imgs, None, None, None)
+    graph2 = model._run_engine(eng, imgs, None, None, None)
+    monkeypatch.setenv("MAPA_FUSED_HEAD", "0")
+    unfused = eng.run(imgs)
+    for k in inline:
+        assert torch.equal(branch[k], inline[k]), k
+        assert torch.equal(graph[k], inline[k]), k
+        assert torch.equal(graph2[k], inline[k]), k
+    for k in ("cam_trans", "cam_quats", "metric_scaling_factor", "camera_poses"):
+        assert torch.equal(unfused[k], inline[k]), k
+    assert rel_l2(unfused["pts3d"].float().cpu().numpy(), inline["pts3d"].float().cpu().numpy()) < 1e-5
+
+
 # ------------------------------------------------------------------------------ info-sharing variants (§8(f) row 4)
 @pytest.mark.parametrize("name", ["gat_224", "aatpe_224", "aatnoref_224", "aat48_224"])
 def test_info_sharing_variants_match_reference(golden, name):

@@ -46,6 +46,12 @@ def main():
     elif what == "fusedhead":
         arms = [("fused", lambda: os.environ.__setitem__("MAPA_FUSED_HEAD", "1")),
                 ("twolaunch", lambda: os.environ.__setitem__("MAPA_FUSED_HEAD", "0"))]
+    elif what == "headbranch":  # pose / scale heads on a side-stream branch vs in line
+        arms = [("branch", lambda: os.environ.__setitem__("MAPA_HEAD_BRANCH", "1")),
+                ("inline", lambda: os.environ.__setitem__("MAPA_HEAD_BRANCH", "0"))]
+    elif what == "lnfuse":  # residual linears with the next LayerNorm fused: all / N % 256 only / none
+        arms = [("all", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 2)), ("n256", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 3)),
+                ("none", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 0))]
     else:
         raise SystemExit(f"unknown A/B {what}")
     models, sd = [], None

@@ -173,21 +173,42 @@ def main():
         cases = [("enc", V, 16, T + 1), ("frame", V, 12, T), ("global", 1, 12, L)]
         if os.environ.get("KB_ATTN_WIDE"):
             cases += [("global1", 1, 12, T + 1), ("global32", 1, 12, 32 * T + 1)]
+        kvm = int(os.environ.get("KB_ATTN_KVMUL", "1"))  # seq_kv = kvm * seq_q (per-task overhead vs per-tile cost)
         for name, B, Hh, S in cases:
             C = Hh * 64
-            qkv = torch.randn(B * S, 3 * C, device="cuda").to(dt)
+            qkv = torch.randn(B * S * kvm, 3 * C, device="cuda").to(dt)
             o = torch.empty(B * S, C, device="cuda", dtype=dt)
             rs = 3 * C
-            f = lambda: nat.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B, heads=Hh, seq_q=S, seq_kv=S,
-                                      q_bstride=S * rs, q_rstride=rs, k_bstride=S * rs, k_rstride=rs,
-                                      v_bstride=S * rs, v_rstride=rs, o_bstride=S * C, o_rstride=C)
-            ms = timeit(f, reps)
+            Skv = S * kvm
+
+            def mk():
+                def f():
+                    nat.attention(qkv, qkv[:, C:], qkv[:, 2 * C:], o, batch=B, heads=Hh, seq_q=S, seq_kv=Skv,
+                                  q_bstride=Skv * rs, q_rstride=rs, k_bstride=Skv * rs, k_rstride=rs,
+                                  v_bstride=Skv * rs, v_rstride=rs, o_bstride=S * C, o_rstride=C)
+                return f
+            fns = [mk()]
+            if os.environ.get("KB_ATTN_HM"):  # head-major [B*H][S][64] q / k / v (contiguous 128-B key rows)
+                qh = torch.randn(B * Hh, S, 64, device="cuda").to(dt)
+                kh = torch.randn(B * Hh, Skv, 64, device="cuda").to(dt)
+                vh = torch.randn(B * Hh, Skv, 64, device="cuda").to(dt)
+                oh = torch.empty(B * Hh, S, 64, device="cuda", dtype=dt)
+                fns.append(lambda: nat.attention(qh, kh, vh, oh, batch=B * Hh, heads=1, seq_q=S, seq_kv=Skv,
+                                                 q_bstride=S * 64, q_rstride=64, k_bstride=Skv * 64, k_rstride=64,
+                                                 v_bstride=Skv * 64, v_rstride=64, o_bstride=S * 64, o_rstride=64))
+            mss = interleaved(fns, reps)
+            if os.environ.get("KB_ATTN_HM"):
+                print(f"attn {name:10s} head-major kv x{kvm}: {mss[-1]*1e3:8.1f} us  "
+                      f"{4*B*Hh*S*Skv*64/mss[-1]/1e9:7.1f} TF/s", flush=True)
+                mss = mss[:-1]
+            ms = mss[0]
+            S2 = S * Skv
             if "torch" in sys.argv:
                 t = qkv.view(B, S, 3, Hh, 64).permute(2, 0, 3, 1, 4)
                 q, k, v = t[0].contiguous(), t[1].contiguous(), t[2].contiguous()
                 ms_t = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(q, k, v), reps)
                 print(f"  torch SDPA {name}: {4*B*Hh*S*S*64/ms_t/1e9:7.1f} TF/s", flush=True)
-            print(f"attn {name:10s} B={B} H={Hh} S={S}: {ms*1e3:8.1f} us  {4*B*Hh*S*S*64/ms/1e9:7.1f} TF/s",
+            print(f"attn {name:10s} B={B} H={Hh} S={S} kv x{kvm}: {ms*1e3:8.1f} us  {4*B*Hh*S2*64/ms/1e9:7.1f} TF/s",
                   flush=True)
 
 
