@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--res", type=int, default=518)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
                     help="autocast operand dtype of the encoder / transformer (infer(amp_dtype=...)); fp32 = use_amp off")
-    ap.add_argument("--head-precision", default="fp32", choices=["fp32", "bf16"],
+    ap.add_argument("--head-precision", default="tf32", choices=["tf32", "fp32", "bf16"],
                     help="fp32 = the reference's recipe (autocast disabled for the heads); bf16 = fast mode")
     ap.add_argument("--no-fast-mode", action="store_true", help="skip the bf16-heads fast-mode measurement")
     ap.add_argument("--strong-views", type=int, default=100,
@@ -176,10 +176,8 @@ def main():
     ms = dt / args.steps * 1e3
     value = V_total * args.steps / dt
 
-    fast = None
-    if world == 1 and not args.no_fast_mode and args.head_precision == "fp32" and args.precision == "bf16":
-        # opt-in bf16-heads fast mode on the same workload (NOT the reference's recipe; reported, never headline)
-        fm = MapAnything(**released_config(), precision=args.precision, head_precision="bf16").to(dev).eval()
+    def other_heads(hp):
+        fm = MapAnything(**released_config(), precision=args.precision, head_precision=hp).to(dev).eval()
         fm._sd = model._sd
         for _ in range(args.warmup):
             fm.infer(views, **amp)
@@ -189,12 +187,21 @@ def main():
             fm.infer(views, **amp)
         torch.cuda.synchronize()
         fdt = time.perf_counter() - t0
-        fast = {"value": V_total * args.steps / fdt, "unit": "views/s", "ms_per_step": fdt / args.steps * 1e3,
-                "head_precision": "bf16",
-                "note": "opt-in fast mode: DPT / pose heads on plain bf16 operands (the reference runs them in fp32, "
-                        "model.py:1774); not like-for-like, not the headline"}
         del fm
         torch.cuda.empty_cache()
+        return {"value": V_total * args.steps / fdt, "unit": "views/s", "ms_per_step": fdt / args.steps * 1e3,
+                "head_precision": hp}
+
+    fast = exact = None
+    if world == 1 and not args.no_fast_mode and args.head_precision != "bf16" and args.precision == "bf16":
+        # opt-in bf16-heads fast mode on the same workload (NOT the reference's recipe; reported, never headline)
+        fast = other_heads("bf16")
+        fast["note"] = ("opt-in fast mode: DPT / pose heads on plain bf16 operands (the reference runs them with "
+                        "autocast disabled, model.py:1774); not like-for-like, not the headline")
+        if args.head_precision == "tf32":  # the fp32-exact split-bf16 heads beside the TF32-equivalent headline
+            exact = other_heads("fp32")
+            exact["note"] = ("heads fp32-exact (split bf16 x3, ~2^-16 relative per product) instead of the reference's "
+                             "TF32 recipe: the previous rounds' headline configuration")
 
     batched = None
     if world == 1 and args.batch_scenes > 1 and not args.geometric and not args.total_views:
@@ -291,9 +298,14 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
             "head_precision": args.head_precision,
-            "precision_recipe": ("reference autocast recipe: bf16 encoder + transformer, fp32-exact geometric "
-                                 "encoders and heads (split-precision bf16 GEMMs)") if args.head_precision == "fp32"
-            else "bf16 heads (fast mode, not the reference recipe)",
+            "precision_recipe": {
+                "tf32": "reference GPU recipe: bf16 autocast encoder + transformer, fp32-exact geometric encoders "
+                        "(split bf16 GEMMs), heads at TF32 precision as the reference's fp32 convs / linears run on its "
+                        "GPUs (cudnn default, matmul.allow_tf32 at model.py:93): binary16 [hi | lo] activations x f16 "
+                        "weights",
+                "fp32": "reference autocast recipe with fp32-exact geometric encoders and heads (split-precision bf16 "
+                        "GEMMs)",
+                "bf16": "bf16 heads (fast mode, not the reference recipe)"}[args.head_precision],
             "config": {"workload": f"{V_total}-view {H}x{W} " + (
                            "images+intrinsics+sparse depth (cfg4 inputs)" if args.geometric else
                            ("image-only MapAnything.infer (fixed job, strong scaling)" if args.total_views else
@@ -312,6 +324,7 @@ def main():
             "batched_scenes": batched,
             "multimodal_cfg4": cfg4,
             "fast_mode_bf16_heads": fast,
+            "fp32_exact_heads": exact,
             "strong_scaling": strong,
             # one GPU, or a view shard over RCCL (kernels and collectives captured together; MAPA_SHARD_GRAPHS=0 or a
             # failed capture on any rank: eager, with the reason)

@@ -26,7 +26,12 @@ typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
  * accepted as an OUTPUT dtype by mapa_layernorm (y_lp) and mapa_bilinear_ac */
 /* MAPA_F16: IEEE binary16 operands (the fp16 autocast recipe, infer(amp_dtype="fp16")); accepted by mapa_gemm (dense
  * A), mapa_attention, mapa_attn_merge, and as an output dtype of mapa_layernorm / mapa_patchify / mapa_convert_rows */
-enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2, MAPA_F16 = 3 };
+/* MAPA_F16X2: TF32-equivalent head operand rows [hi | lo] of binary16 (2x the logical width): v = hi + lo, hi = f16(v),
+ * lo = f16(v - hi).  Read by mapa_gemm with dtype MAPA_F16 as a plain 2C-wide operand against f16 weights packed
+ * [w | w] (the conv's channels doubled), written by mapa_gemm's out_s3 / out_s3_relu when dtype is MAPA_F16, and
+ * accepted as an output dtype by mapa_layernorm, mapa_bilinear_ac and mapa_split_rows.  A value outside binary16's
+ * range (|v| > 65504, or not finite) sets MAPA_FAULT_F16_RANGE. */
+enum { MAPA_F32 = 0, MAPA_BF16 = 1, MAPA_BF16X3 = 2, MAPA_F16 = 3, MAPA_F16X2 = 4 };
 enum { MAPA_A_DENSE = 0, MAPA_A_CONV3X3 = 1 };
 enum { MAPA_OUT_ROWMAJOR = 0, MAPA_OUT_PIXSHUF = 1 };
 /* GELU is the exact-erf form (nn.GELU()), erf evaluated branch-free to within 1.2 ulp of fp32 erff (two minimax
@@ -54,7 +59,9 @@ int mapa_stream_check(mapa_stream_t stream, const char* what);
  *     queued after the publish (MapAnything.infer publishes after the transformer and checks before returning).
  *   mapa_fault_status: synchronous read of the fault word (and reset to 0 when `reset`); -1 on a HIP error.
  *   mapa_stream_check also reports and clears it. */
-enum { MAPA_FAULT_LN_BARRIER = 1 };
+/* MAPA_FAULT_F16_RANGE: a MAPA_F16X2 producer met a value outside binary16's range (the TF32-equivalent heads'
+ * operands); the outputs of that forward are not trustworthy and MapAnything.infer raises. */
+enum { MAPA_FAULT_LN_BARRIER = 1, MAPA_FAULT_F16_RANGE = 2 };
 int mapa_fault_slot_create(uint32_t** host, uint32_t** dev);
 int mapa_fault_slot_destroy(uint32_t* host);
 int mapa_fault_publish(uint32_t* dev_slot, mapa_stream_t stream);
@@ -336,6 +343,10 @@ int mapa_convert_rows(const float* src, int64_t lds, int rows, int cols, void* d
  * Replaces the fp32 conv/linear operands of DenseRepresentationEncoder (dense_rep_encoder.py:234-287). */
 int mapa_split_bf16x3(const float* x, int64_t ldx, int64_t rows, int cols, int cols_padded, void* y,
                       mapa_stream_t stream);
+/* The same for either split form: dtype MAPA_BF16X3 (as mapa_split_bf16x3) or MAPA_F16X2 (the TF32-equivalent heads:
+ * y binary16 [rows][2*cols_padded] = [hi | lo], hi = f16(x), lo = f16(x - hi); range faults: MAPA_FAULT_F16_RANGE). */
+int mapa_split_rows(const float* x, int64_t ldx, int64_t rows, int cols, int cols_padded, void* y, int dtype,
+                    mapa_stream_t stream);
 
 /* Deterministic synthetic weights on device: out[i] = (2*u_i - 1)*half + mid, u_i = splitmix64 stream of
  * `seed` (bit-identical to mapanything/utils/synthetic.py). */

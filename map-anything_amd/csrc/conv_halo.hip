@@ -171,7 +171,8 @@ __device__ __forceinline__ void stage_win(const char* abase, char* wins, int buf
   stage_win_t<BN, BH, int64_t>(abase, wins, buf, ch, wave, wsrc, dummy);
 }
 
-template <int BN, bool HO = false, int BH = 16, bool FLAT = false>
+// F16: fp16 operands (the TF32-equivalent heads' MAPA_F16X2 split rows against f16 weights); same staging and tiles
+template <int BN, bool HO = false, int BH = 16, bool FLAT = false, bool F16 = false>
 __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel(GemmArgs p, HeadOut ho, HSplit sp) {
   using C = HCfg<BN, BH>;
   static_assert(!FLAT || (BN == 128 && BH == 16 && !HO), "flat blocks: 128-wide tiles of 256 positions");
@@ -241,7 +242,7 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  typedef bf16x8 b8;  // raw 16-bit operand words (bf16, or fp16 with F16)
   const int g = lane >> 4, r16 = lane & 15;
   // B fragment j of this lane: ring row rb = wn*TN + j*16 + r16; the swizzle depends on bits 2-3 of rb only, so
   // fragment j sits at b_off + j*1024 (an immediate offset of one address)
@@ -355,7 +356,7 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
         }
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ai, b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32<F16>(ai, b[j], acc[i][j]);
       }
     }
   };
@@ -531,7 +532,7 @@ __global__ void __launch_bounds__(HT, (2 * HCfg<BN, BH>::MINB)) conv_halo_kernel
 }  // namespace
 
 // bn: 256 or 128 output channels per tile (0 = 256 when N % 256 == 0, else 128); bh: block rows (16, or 8 with
-// bn 256).  Needs a bf16 stride-1 conv in the
+// bn 256).  Needs a bf16 (or f16: a.lp_f16) stride-1 conv in the
 // channel-block-major K order with 32-channel slices (conv_kblock == 32); returns false otherwise.
 // one image of the A operand must be addressable by the window's 32-bit buffer offsets
 static bool halo_img_ok(const GemmArgs& a) { return (int64_t)a.cv_IH * a.cv_IW * a.cv_Cp * 2 < 0x7ff00000LL; }
@@ -547,12 +548,13 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh) {
   if (tiles >= (int64_t(1) << 31)) return false;
   const HeadOut none{};
   const HSplit one{1, 0, nullptr, nullptr};
-  if (bh == 8)
-    hipLaunchKernelGGL((conv_halo_kernel<256, false, 8>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
-  else if (bn == 256)
-    hipLaunchKernelGGL((conv_halo_kernel<256>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
+  void (*k)(GemmArgs, HeadOut, HSplit);
+  if (a.lp_f16)
+    k = bh == 8 ? conv_halo_kernel<256, false, 8, false, true>
+        : bn == 256 ? conv_halo_kernel<256, false, 16, false, true> : conv_halo_kernel<128, false, 16, false, true>;
   else
-    hipLaunchKernelGGL((conv_halo_kernel<128>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
+    k = bh == 8 ? conv_halo_kernel<256, false, 8> : bn == 256 ? conv_halo_kernel<256> : conv_halo_kernel<128>;
+  hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
   return true;
 }
 
@@ -601,8 +603,12 @@ bool launch_conv_halo_flat(const GemmArgs& a, int nsplit, void* ws, int64_t ws_b
     sp.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + ticket_bytes);
   }
   const HeadOut none{};
-  hipLaunchKernelGGL((conv_halo_kernel<128, false, 16, true>), dim3((unsigned)(tiles * nsplit)), dim3(HT), 0, stream,
-                     a, none, sp);
+  if (a.lp_f16)
+    hipLaunchKernelGGL((conv_halo_kernel<128, false, 16, true, true>), dim3((unsigned)(tiles * nsplit)), dim3(HT), 0,
+                       stream, a, none, sp);
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<128, false, 16, true>), dim3((unsigned)(tiles * nsplit)), dim3(HT), 0, stream,
+                       a, none, sp);
   return true;
 }
 
@@ -620,8 +626,12 @@ bool launch_conv_halo_headout(const GemmArgs& a, const float* w6, const float* b
   h.w6 = w6; h.b6 = b6; h.pose = pose; h.scale = scale; h.vps = vps;
   h.pts3d = pts3d; h.pts3d_cam = pts3d_cam; h.rays = rays; h.depth = depth; h.conf = conf; h.logits = logits;
   h.mask = mask;
-  hipLaunchKernelGGL((conv_halo_kernel<128, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h,
-                     HSplit{1, 0, nullptr, nullptr});
+  if (a.lp_f16)
+    hipLaunchKernelGGL((conv_halo_kernel<128, true, 16, false, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h,
+                       HSplit{1, 0, nullptr, nullptr});
+  else
+    hipLaunchKernelGGL((conv_halo_kernel<128, true>), dim3((unsigned)tiles), dim3(HT), 0, stream, a, h,
+                       HSplit{1, 0, nullptr, nullptr});
   return true;
 }
 

@@ -119,9 +119,10 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 // grid-stride form spent more on 64-bit index division than on its memory traffic.
 // BIL_ROWS: output rows per thread (8 for the x2 upsamples: 74 -> 148 60.3 -> 42.3 us, 148 -> 296 split 222 -> 161;
 // 4 for 296 -> 518: 339 -> 254, 264 with 8; kbench 'bil', 8 views, interleaved against the one-row kernel)
-template <typename TI, typename TO, bool S3 = false, int BIL_ROWS = 4>  // S3: split operand rows [hi | lo] (2C wide)
+// S3: split operand rows [hi | lo] (2C wide): 1 = bf16 (MAPA_BF16X3), 2 = binary16 (MAPA_F16X2; range faults -> fault)
+template <typename TI, typename TO, int S3 = 0, int BIL_ROWS = 4>
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
-                                   int OW, int c8_shift, TO* __restrict__ out) {
+                                   int OW, int c8_shift, TO* __restrict__ out, unsigned* fault) {
   const int c8 = C / 8;
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= OW * c8) return;
@@ -168,17 +169,27 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
       TO* op = out + ((size_t)rr * OW + ox) * (S3 ? 2 * C : C) + c;
       const f32x4 r0 = ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0);
       const f32x4 r1 = ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1);
-      if constexpr (S3) {  // 8 channels: one 16-B store of hi and one of lo
+      if constexpr (S3 != 0) {  // 8 channels: one 16-B store of hi and one of lo
         uint4 hv, lv;
         uint32_t* hp = &hv.x;
         uint32_t* lp = &lv.x;
+        bool ok = true;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float v0 = k < 2 ? r0[2 * k] : r1[2 * k - 4], v1 = k < 2 ? r0[2 * k + 1] : r1[2 * k - 3];
-          const bf16_t h0 = f32_to_bf16(v0), h1 = f32_to_bf16(v1);
-          hp[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-          lp[k] = pack_bf16x2(v0 - bf16_to_f32(h0), v1 - bf16_to_f32(h1));
+          if constexpr (S3 == 2) {
+            uint32_t h0, l0, h1, l1;
+            ok &= split_f16(v0, h0, l0);
+            ok &= split_f16(v1, h1, l1);
+            hp[k] = h0 | (h1 << 16);
+            lp[k] = l0 | (l1 << 16);
+          } else {
+            const bf16_t h0 = f32_to_bf16(v0), h1 = f32_to_bf16(v1);
+            hp[k] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+            lp[k] = pack_bf16x2(v0 - bf16_to_f32(h0), v1 - bf16_to_f32(h1));
+          }
         }
+        if constexpr (S3 == 2) f16_range_fault(fault, !ok);
         typedef uint32_t nt4 __attribute__((ext_vector_type(4)));
         // 1.1 GB at 518^2: streamed past the caches
         __builtin_nontemporal_store(nt4{hv.x, hv.y, hv.z, hv.w}, reinterpret_cast<nt4*>(op));
@@ -353,15 +364,18 @@ __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, 
 // fp32 rows -> [hi | lo] bf16 column blocks of width cp (zero-padded past cols), hi = bf16(x), lo = bf16(x - hi):
 // read by a bf16 GEMM as the logical K blocks [hi | hi | lo] (mapa_gemm_desc.a_split) against weights packed
 // [hi | lo | hi], it accumulates x_hi*w_hi + x_hi*w_lo + x_lo*w_hi (the split form of an fp32 product, ~2^-16).
+// f16: the TF32-equivalent form instead (MAPA_F16X2: hi = f16(x), lo = f16(x - hi), read as a plain 2C-wide f16
+// operand against weights [w | w]); values outside binary16's range set MAPA_FAULT_F16_RANGE.
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, int64_t ldx, int64_t rows, int cols, int cp,
-                                    bf16_t* __restrict__ y) {
+                                    bf16_t* __restrict__ y, int f16, unsigned* fault) {
   const int g4 = cp / 4;
   const int64_t total = rows * g4;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = e / g4;
     const int c = (int)(e - r * g4) * 4;
     const f32x4 v = c < cols ? *reinterpret_cast<const f32x4*>(x + r * ldx + c) : f32x4{0.f, 0.f, 0.f, 0.f};
-    store_split3(y + r * 2 * cp + c, cp, v);
+    if (f16) store_split2h(y + r * 2 * cp + c, cp, v, fault);
+    else store_split3(y + r * 2 * cp + c, cp, v);
   }
 }
 
@@ -420,24 +434,18 @@ static void bilinear_launch(const void* in, int in_dtype, int n, int IH, int IW,
                             int c8_shift, void* out, int out_dtype, hipStream_t stream) {
   const int64_t groups = ((int64_t)n * OH + RW - 1) / RW;
   const dim3 g((unsigned)((OW * (C / 8) + TPB - 1) / TPB), (unsigned)std::min<int64_t>(groups, 65535)), b(TPB);
-  if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32)
-    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, true, RW>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (out_dtype == MAPA_BF16X3)
-    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, true, RW>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW,
-                       C, OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16)
-    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, bf16_t, false, RW>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW,
-                       C, OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16)
-    hipLaunchKernelGGL((bilinear_ac_kernel<float, bf16_t, false, RW>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, c8_shift, (bf16_t*)out);
-  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_F32)
-    hipLaunchKernelGGL((bilinear_ac_kernel<bf16_t, float, false, RW>), g, b, 0, stream, (const bf16_t*)in, n, IH, IW,
-                       C, OHf, OWf, OH, OW, c8_shift, (float*)out);
-  else
-    hipLaunchKernelGGL((bilinear_ac_kernel<float, float, false, RW>), g, b, 0, stream, (const float*)in, n, IH, IW, C,
-                       OHf, OWf, OH, OW, c8_shift, (float*)out);
+  unsigned* fault = mapa_gemm_impl::fault_word();
+#define MAPA_BIL(TI, TO, S)                                                                                          \
+  hipLaunchKernelGGL((bilinear_ac_kernel<TI, TO, S, RW>), g, b, 0, stream, (const TI*)in, n, IH, IW, C, OHf, OWf, OH, \
+                     OW, c8_shift, (TO*)out, fault)
+  if (out_dtype == MAPA_F16X2 && in_dtype == MAPA_F32) MAPA_BIL(float, bf16_t, 2);
+  else if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32) MAPA_BIL(float, bf16_t, 1);
+  else if (out_dtype == MAPA_BF16X3) MAPA_BIL(bf16_t, bf16_t, 1);
+  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16) MAPA_BIL(bf16_t, bf16_t, 0);
+  else if (in_dtype == MAPA_F32 && out_dtype == MAPA_BF16) MAPA_BIL(float, bf16_t, 0);
+  else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_F32) MAPA_BIL(bf16_t, float, 0);
+  else MAPA_BIL(float, float, 0);
+#undef MAPA_BIL
 }
 
 extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
@@ -447,7 +455,8 @@ extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int
   MAPA_CHECK_ARG((int64_t)OW * c8 < (1LL << 31) && (int64_t)n * OH + 8 * 65536 < (1LL << 31),
                  "mapa_bilinear_ac: too large");
   MAPA_CHECK_ARG((in_dtype == MAPA_F32 || in_dtype == MAPA_BF16) &&
-                     (out_dtype == MAPA_F32 || out_dtype == MAPA_BF16 || out_dtype == MAPA_BF16X3),
+                     (out_dtype == MAPA_F32 || out_dtype == MAPA_BF16 || out_dtype == MAPA_BF16X3 ||
+                      (out_dtype == MAPA_F16X2 && in_dtype == MAPA_F32)),
                  "mapa_bilinear_ac: bad dtypes");
   if (OH >= 2 * IH - 1)
     bilinear_launch<8>(in, in_dtype, n, IH, IW, C, OHf, OWf, OH, OW, c8_shift, out, out_dtype, stream);
@@ -544,8 +553,21 @@ extern "C" int mapa_split_bf16x3(const float* x, int64_t ldx, int64_t rows, int 
                      ldx >= cols && ldx % 4 == 0,
                  "mapa_split_bf16x3: bad args (cols %% 4, cols_padded %% 8, ldx %% 4)");
   hipLaunchKernelGGL(split_bf16x3_kernel, dim3(grid_for(rows * (cols_padded / 4))), dim3(TPB), 0, stream, x, ldx,
-                     rows, cols, cols_padded, (bf16_t*)y);
+                     rows, cols, cols_padded, (bf16_t*)y, 0, nullptr);
   MAPA_CHECK_LAUNCH("mapa_split_bf16x3");
+  return 0;
+}
+
+extern "C" int mapa_split_rows(const float* x, int64_t ldx, int64_t rows, int cols, int cols_padded, void* y,
+                               int dtype, hipStream_t stream) {
+  MAPA_CHECK_ARG(dtype == MAPA_BF16X3 || dtype == MAPA_F16X2, "mapa_split_rows: dtype must be MAPA_BF16X3 or MAPA_F16X2");
+  if (dtype == MAPA_BF16X3) return mapa_split_bf16x3(x, ldx, rows, cols, cols_padded, y, stream);
+  MAPA_CHECK_ARG(x && y && rows > 0 && cols > 0 && cols % 4 == 0 && cols_padded % 8 == 0 && cols_padded >= cols &&
+                     ldx >= cols && ldx % 4 == 0,
+                 "mapa_split_rows: bad args (cols %% 4, cols_padded %% 8, ldx %% 4)");
+  hipLaunchKernelGGL(split_bf16x3_kernel, dim3(grid_for(rows * (cols_padded / 4))), dim3(TPB), 0, stream, x, ldx,
+                     rows, cols, cols_padded, (bf16_t*)y, 1, mapa_gemm_impl::fault_word());
+  MAPA_CHECK_LAUNCH("mapa_split_rows");
   return 0;
 }
 

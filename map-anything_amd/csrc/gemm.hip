@@ -371,7 +371,7 @@ static int forced_variant() {
 int pick_streamk(int dtype, bool conv, int M, int N, int K) {
   const int f = forced_variant();
   if (f) return f >= 2580 && f <= 2582 ? f : 0;
-  if (dtype != MAPA_BF16) return 0;
+  if (dtype != MAPA_BF16 && dtype != MAPA_F16) return 0;
   const int64_t big_tiles = (int64_t)((M + 255) / 256) * ((N + 127) / 128);
   // 256x256 stream-K tiles from N = 512 up at a few thousand rows (the stride-2 768-channel DPT conv at 37 -> 19,
   // M = views * 361: 244 -> 152 us); the 224^2 geometric encoders (M = views * 256) keep 256x128
@@ -396,13 +396,14 @@ static int gemm_args(const mapa_gemm_desc* d, GemmArgs& a) {
   MAPA_CHECK_ARG(d->M > 0 && d->N > 0 && d->K > 0, "mapa_gemm: bad shape M=%d N=%d K=%d", d->M, d->N, d->K);
   MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || d->dtype == MAPA_F32 || d->dtype == MAPA_F16,
                  "mapa_gemm: dtype must be bf16, f16 or f32");
-  // fp16: the transformer linears of the fp16 autocast recipe (dense A; the heads stay fp32-exact split bf16)
-  MAPA_CHECK_ARG(d->dtype != MAPA_F16 || (d->a_mode == MAPA_A_DENSE && !d->a_split && d->out_mode == MAPA_OUT_ROWMAJOR),
-                 "mapa_gemm: f16 takes dense row-major problems only");
+  // fp16: the transformer linears of the fp16 autocast recipe, and the TF32-equivalent heads (MAPA_F16X2 operands:
+  // split rows [hi | lo] read as a plain 2C-wide f16 operand against weights [w | w]; out_s3 then writes f16 splits)
+  MAPA_CHECK_ARG(d->dtype != MAPA_F16 || !d->a_split, "mapa_gemm: a_split is the bf16 split (MAPA_BF16X3) only");
   const int E = d->dtype == MAPA_F32 ? 4 : 8;
   MAPA_CHECK_ARG(d->K % E == 0, "mapa_gemm: K=%d must be a multiple of %d", d->K, E);
   MAPA_CHECK_ARG(d->A && d->W, "mapa_gemm: null operand");
-  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 || (!d->out_s3 && !d->out_s3_relu), "mapa_gemm: split outputs need dtype bf16");
+  MAPA_CHECK_ARG(d->dtype != MAPA_F32 || (!d->out_s3 && !d->out_s3_relu),
+                 "mapa_gemm: split outputs need dtype bf16 (MAPA_BF16X3 rows) or f16 (MAPA_F16X2 rows)");
   a.lp_f16 = d->dtype == MAPA_F16 ? 1 : 0;
   MAPA_CHECK_ARG(d->act >= MAPA_ACT_NONE && d->act <= MAPA_ACT_GELU_POST, "mapa_gemm: bad act %d", d->act);
   MAPA_CHECK_ARG(d->act != MAPA_ACT_GELU_POST || !d->gamma, "mapa_gemm: GELU_POST takes no gamma");
@@ -456,6 +457,7 @@ static int gemm_args(const mapa_gemm_desc* d, GemmArgs& a) {
   a.out_mode = d->out_mode; a.ps_s = d->ps_s; a.ps_h = d->ps_h; a.ps_w = d->ps_w; a.ps_cout = d->ps_cout;
   a.vec_ok = (d->N % 4 == 0) && (d->out_mode == MAPA_OUT_PIXSHUF || d->ldo % 4 == 0);
   a.tile_gm = g_tile_gm;
+  a.fault = fault_word();
   if (d->ln_out) {
     MAPA_CHECK_ARG(d->ln_w && d->ln_b && d->out_f32 && d->out_mode == MAPA_OUT_ROWMAJOR,
                    "mapa_gemm: ln_out needs ln_w, ln_b and a row-major out_f32");
@@ -479,11 +481,12 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
   // 3) wins for the implicit convs and K < 1024; 128-B rows x 2 stages for the K >= 1024 linears.
   const int forced = forced_variant();
   const int variant = forced ? forced : pick_variant(d->dtype, conv, d->M, d->N, d->K);
-  const int sk = d->dtype == MAPA_BF16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
-  const bool halo = conv && d->dtype == MAPA_BF16 &&
+  const bool lp16 = d->dtype == MAPA_BF16 || d->dtype == MAPA_F16;
+  const int sk = lp16 ? pick_streamk(d->dtype, conv, d->M, d->N, d->K) : 0;
+  const bool halo = conv && lp16 &&
                     (forced ? (forced >= 2584 && forced <= 2586) || forced == 2588
                             : pick_halo(a.M, a.N, a.cv_OH, a.cv_OW, a.cv_kb));
-  const int flat = !conv || d->dtype != MAPA_BF16 ? 0
+  const int flat = !conv || !lp16 ? 0
                    : forced ? (forced == 2589 ? conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split) : 0)
                             : pick_flat(a);
   const int lnf = pick_ln_fused(d, variant, sk);
@@ -503,7 +506,8 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
              launch_gemm_big(a, conv, variant == 2587 ? 15 : variant - 2560, stream)) {
     // launched (bf16, or f16 for the tile kernels that carry an fp16 instantiation)
   } else if (d->dtype == MAPA_F16) {
-    launch_variant<TraitsF16, 0>(variant >= 2560 ? 1282 : variant, nblk, stream, a);
+    if (conv) launch_variant<TraitsF16, 1>(variant >= 2560 ? 643 : variant, nblk, stream, a);
+    else launch_variant<TraitsF16, 0>(variant >= 2560 ? 1282 : variant, nblk, stream, a);
   } else if (d->dtype == MAPA_BF16) {
     if (conv) launch_variant<TraitsBF16, 1>(variant, nblk, stream, a);
     else launch_variant<TraitsBF16, 0>(variant, nblk, stream, a);
@@ -528,9 +532,10 @@ extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6,
   MAPA_CHECK_ARG(w6 && b6 && pose_out && scale && pts3d && pts3d_cam && rays && depth && conf && logits && mask,
                  "mapa_regressor_head_out: null output or parameter");
   MAPA_CHECK_ARG(views_per_scale > 0, "mapa_regressor_head_out: views_per_scale %d must be > 0", views_per_scale);
-  MAPA_CHECK_ARG(d->dtype == MAPA_BF16 && d->a_mode == MAPA_A_CONV3X3 && !d->out_f32 && !d->out_lp &&
+  MAPA_CHECK_ARG((d->dtype == MAPA_BF16 || d->dtype == MAPA_F16) && d->a_mode == MAPA_A_CONV3X3 && !d->out_f32 &&
+                     !d->out_lp &&
                      !d->out_lp_relu && !d->out_s3 && !d->out_s3_relu && !d->resid1 && !d->resid2 && !d->gamma,
-                 "mapa_regressor_head_out: needs a bf16 3x3 conv descriptor without other outputs");
+                 "mapa_regressor_head_out: needs a bf16 / f16 3x3 conv descriptor without other outputs");
   MAPA_CHECK_ARG(launch_conv_halo_headout(a, w6, b6, pose_out, scale, views_per_scale, pts3d, pts3d_cam, rays, depth, conf, logits,
                                           mask, stream),
                  "mapa_regressor_head_out: conv must be stride 1, conv_kblock 32, N 128, ReLU with bias");
@@ -573,7 +578,7 @@ extern "C" int mapa_gemm_set_variant(int variant) {
 }
 
 extern "C" int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d) {
-  if (!d || d->dtype != MAPA_BF16 || d->M <= 0 || d->N <= 0 || d->K <= 0) return 0;
+  if (!d || (d->dtype != MAPA_BF16 && d->dtype != MAPA_F16) || d->M <= 0 || d->N <= 0 || d->K <= 0) return 0;
   if (d->ln_out && !forced_variant()) {
     const bool conv = d->a_mode == MAPA_A_CONV3X3;
     const int lnf = pick_ln_fused(d, pick_variant(d->dtype, conv, d->M, d->N, d->K),

@@ -756,7 +756,7 @@ struct SkArgs : mapa_idx::SkPlan {  // dp_tiles / base / total / per / nk: the i
 using mapa_idx::sk_slab;
 
 
-template <int AMODE, int BN, int RB, int STAGES, int PRIO, int MINB>
+template <int AMODE, int BN, int RB, int STAGES, int PRIO, int MINB, bool F16 = false>
 __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkArgs s) {
   using C = Cfg<BN, RB>;
   constexpr int MAIN = STAGES * C::STAGE;
@@ -825,19 +825,19 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
     auto compute = [&](int slot) __attribute__((always_inline)) {
       const char* As = lds + slot * C::STAGE;
       const char* Bs = As + C::A_BYTES;
-      b8 a[C::KG][C::FM], b[C::KG][C::FN];
+      bf16x8 a[C::KG][C::FM], b[C::KG][C::FN];  // raw 16-bit words: bf16, or fp16 with F16
 #pragma unroll
       for (int kg = 0; kg < C::KG; ++kg) {
         const int chunk = kg * 4 + g;
 #pragma unroll
         for (int j = 0; j < C::FN; ++j) {
           const int rb = wn * C::TN + j * 16 + r16;
-          b[kg][j] = *reinterpret_cast<const b8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
+          b[kg][j] = *reinterpret_cast<const bf16x8*>(Bs + rb * RB + ((chunk ^ swz<RB>(rb)) << 4));
         }
 #pragma unroll
         for (int i = 0; i < C::FM; ++i) {
           const int ra = wm * C::TM + i * 16 + r16;
-          a[kg][i] = *reinterpret_cast<const b8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
+          a[kg][i] = *reinterpret_cast<const bf16x8*>(As + ra * RB + ((chunk ^ swz<RB>(ra)) << 4));
         }
       }
 #pragma unroll
@@ -847,7 +847,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
         for (int i = 0; i < C::FM; ++i)
 #pragma unroll
           for (int j = 0; j < C::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kg][i], b[kg][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16x16x32<F16>(a[kg][i], b[kg][j], acc[i][j]);
         if (PRIO) __builtin_amdgcn_s_setprio(0);
       }
     };
@@ -982,14 +982,26 @@ bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stre
   const int BMv = bms[variant];
   const int nblk = ((a.M + BMv - 1) / BMv) * ((a.N + BN - 1) / BN);
   void (*k)(GemmArgs) = nullptr;
-  if (a.lp_f16) {  // fp16 operands: the tile kernels the automatic choice uses for dense linears
-    if (conv) return false;
+  if (a.lp_f16) {  // fp16 operands: the tile kernels the automatic choice uses for dense linears and for the
+                   // TF32-equivalent head convs (MAPA_F16X2 operands)
     switch (variant) {
-      case 8: k = gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, BBM, true>; break;
-      case 10: k = gemm_big_kernel<0, 128, 64, 3, 0, 0, 2, BBM, true>; break;
-      case 11: k = gemm_big_kernel<0, 128, 64, 3, 0, 1, 2, BBM, true>; break;
-      case 14: k = gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, true>; break;
-      case 15: k = gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, true>; break;
+      case 8:
+        k = conv ? gemm_big_kernel<1, 256, 128, 2, 0, 1, 1, BBM, true> : gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, BBM, true>;
+        break;
+      case 10:
+        if (conv) return false;
+        k = gemm_big_kernel<0, 128, 64, 3, 0, 0, 2, BBM, true>;
+        break;
+      case 11:
+        k = conv ? gemm_big_kernel<1, 128, 64, 3, 0, 1, 2, BBM, true> : gemm_big_kernel<0, 128, 64, 3, 0, 1, 2, BBM, true>;
+        break;
+      case 14:
+        k = conv ? gemm_big_kernel<1, 256, 128, 2, 0, 1, 1, 192, true> : gemm_big_kernel<0, 256, 128, 2, 0, 1, 1, 192, true>;
+        break;
+      case 15:
+        if (conv) return false;
+        k = gemm_big_kernel<0, 192, 128, 2, 0, 1, 1, 192, true>;
+        break;
       default: return false;
     }
     hipLaunchKernelGGL(k, dim3(nblk), dim3(BTHREADS), 0, stream, a);
@@ -1170,10 +1182,27 @@ bool launch_gemm_streamk(const GemmArgs& a, bool conv, int variant, void* ws, in
   s.tickets = reinterpret_cast<int*>(ws);
   s.slabs = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + SK_TICKET_BYTES);
   void (*k)(GemmArgs, SkArgs);
-  if (variant != 1) k = gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
-  else k = conv ? gemm_sk_kernel<1, 256, 64, 3, 1, 1> : gemm_sk_kernel<0, 256, 64, 3, 1, 1>;
+  if (a.lp_f16) {  // the TF32-equivalent head convs / linears (MAPA_F16X2 operands)
+    if (variant != 1) k = gemm_sk_kernel<0, 128, 64, 3, 1, 4, true>;
+    else k = conv ? gemm_sk_kernel<1, 256, 64, 3, 1, 1, true> : gemm_sk_kernel<0, 256, 64, 3, 1, 1, true>;
+  } else if (variant != 1) {
+    k = gemm_sk_kernel<0, 128, 64, 3, 1, 4>;
+  } else {
+    k = conv ? gemm_sk_kernel<1, 256, 64, 3, 1, 1> : gemm_sk_kernel<0, 256, 64, 3, 1, 1>;
+  }
   hipLaunchKernelGGL(k, dim3(G), dim3(BTHREADS), 0, stream, a, s);
   return true;
+}
+
+unsigned* fault_word() {
+  static unsigned* cache[16] = {nullptr};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
+  if (!cache[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mapa_fault)) == hipSuccess) cache[dev] = static_cast<unsigned*>(p);
+  }
+  return cache[dev];
 }
 
 }  // namespace mapa_gemm_impl

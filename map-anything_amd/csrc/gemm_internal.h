@@ -46,7 +46,12 @@ struct GemmArgs {
   int ln_band0, ln_nbands;       // this launch's bands [ln_band0, ln_band0 + ln_nbands) (co-resident by construction)
   unsigned ln_spin;              // bounded wait: polls before the band barrier gives up and raises the fault word
   int ln_skip;                   // test hook: tile (band 0, column 0) skips its publish (mapa_gemm_tune LN_TEST_SKIP)
+  unsigned* fault;               // the library's device fault word (f16 split outputs out of binary16 range)
 };
+
+// Device address of the library's fault word on the current device (gemm_big.hip; other translation units pass it
+// to their kernels, as device globals are per translation unit without relocatable device code).
+unsigned* fault_word();
 
 using mapa_idx::group_coords;
 using mapa_idx::tile_coords;
@@ -164,10 +169,14 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
         u.y = pack_lp2(p.lp_f16, fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
         *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
       }
-      if (p.out_s3) store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v);
+      if (p.out_s3) {
+        if (p.lp_f16) store_split2h(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v, p.fault);
+        else store_split3(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v);
+      }
       if (p.out_s3_relu) {
         const f32x4 rr = {fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
-        store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, rr);
+        if (p.lp_f16) store_split2h(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, rr, p.fault);
+        else store_split3(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, rr);
       }
     } else {
       if (p.out_lp) *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.out_lp) + off) = v;
@@ -190,8 +199,14 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
       if constexpr (sizeof(T) == 2) {
         if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_lp(p.lp_f16, x);
         if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_lp(p.lp_f16, fmaxf(x, 0.f));
-        if (p.out_s3) store_split1(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + e, ld, x);
-        if (p.out_s3_relu) store_split1(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + e, ld, fmaxf(x, 0.f));
+        if (p.out_s3) {
+          if (p.lp_f16) store_split2h1(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + e, ld, x, p.fault);
+          else store_split1(reinterpret_cast<bf16_t*>(p.out_s3) + off3 + e, ld, x);
+        }
+        if (p.out_s3_relu) {
+          if (p.lp_f16) store_split2h1(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + e, ld, fmaxf(x, 0.f), p.fault);
+          else store_split1(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3 + e, ld, fmaxf(x, 0.f));
+        }
       } else {
         if (p.out_lp) reinterpret_cast<float*>(p.out_lp)[o] = x;
         if (p.out_lp_relu) reinterpret_cast<float*>(p.out_lp_relu)[o] = fmaxf(x, 0.f);
@@ -284,11 +299,15 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
                        pack_lp2(h, fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f)), pack_lp2(h, fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f))};
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp_relu) + off) = u;
     }
-    if (p.out_s3) store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0, v1);
+    if (p.out_s3) {
+      if (p.lp_f16) store_split2h_x8(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0, v1, p.fault);
+      else store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3) + off3, ld, v0, v1);
+    }
     if (p.out_s3_relu) {
       const f32x4 r0 = {fmaxf(v0[0], 0.f), fmaxf(v0[1], 0.f), fmaxf(v0[2], 0.f), fmaxf(v0[3], 0.f)};
       const f32x4 r1 = {fmaxf(v1[0], 0.f), fmaxf(v1[1], 0.f), fmaxf(v1[2], 0.f), fmaxf(v1[3], 0.f)};
-      store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, r0, r1);
+      if (p.lp_f16) store_split2h_x8(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, r0, r1, p.fault);
+      else store_split3x8(reinterpret_cast<bf16_t*>(p.out_s3_relu) + off3, ld, r0, r1);
     }
   } else {
     if (p.out_lp) {

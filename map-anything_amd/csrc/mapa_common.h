@@ -119,6 +119,55 @@ __device__ __forceinline__ void store_split1(bf16_t* p, int64_t ld, float x) {
   p[ld] = f32_to_bf16(x - bf16_to_f32(h));
 }
 
+// TF32-equivalent head operands (MAPA_F16X2): v = hi + lo with hi = f16(v), lo = f16(v - hi) (22 significant bits,
+// stored [hi | lo] like the bf16 split), multiplied against f16 weights [w | w] — the reference's TF32 heads on its own
+// hardware round both operands to 11 significant bits; here only the weights are.  binary16 spans |v| <= 65504: a
+// larger (or non-finite) value sets MAPA_FAULT_F16_RANGE in the library's fault word (`fault`; the host raises).
+namespace mapa_gemm_impl {
+unsigned* fault_word();  // device address of the library's fault word on the current device (gemm_big.hip)
+}
+constexpr float F16_MAX = 65504.f;
+constexpr unsigned FAULT_F16_RANGE = 2u;  // MAPA_FAULT_F16_RANGE
+__device__ __forceinline__ void f16_range_fault(unsigned* fault, bool bad) {
+  if (bad && fault) __hip_atomic_fetch_or(fault, FAULT_F16_RANGE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// hi / lo halves of one value: (hi, lo) 16-bit words; returns whether |x| fits binary16
+__device__ __forceinline__ bool split_f16(float x, uint32_t& h, uint32_t& l) {
+  const _Float16 hh = (_Float16)x;
+  h = __builtin_bit_cast(uint16_t, hh);
+  l = f32_to_f16(x - (float)hh);
+  return fabsf(x) <= F16_MAX;
+}
+__device__ __forceinline__ void store_split2h(bf16_t* p, int64_t ld, f32x4 v, unsigned* fault) {
+  uint32_t h[4], l[4];
+  bool ok = true;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) ok &= split_f16(v[e], h[e], l[e]);
+  *reinterpret_cast<uint2*>(p) = uint2{h[0] | (h[1] << 16), h[2] | (h[3] << 16)};
+  *reinterpret_cast<uint2*>(p + ld) = uint2{l[0] | (l[1] << 16), l[2] | (l[3] << 16)};
+  f16_range_fault(fault, !ok);
+}
+__device__ __forceinline__ void store_split2h_x8(bf16_t* p, int64_t ld, f32x4 a, f32x4 b, unsigned* fault) {
+  uint32_t h[8], l[8];
+  bool ok = true;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    ok &= split_f16(a[e], h[e], l[e]);
+    ok &= split_f16(b[e], h[e + 4], l[e + 4]);
+  }
+  *reinterpret_cast<uint4*>(p) = uint4{h[0] | (h[1] << 16), h[2] | (h[3] << 16), h[4] | (h[5] << 16), h[6] | (h[7] << 16)};
+  *reinterpret_cast<uint4*>(p + ld) =
+      uint4{l[0] | (l[1] << 16), l[2] | (l[3] << 16), l[4] | (l[5] << 16), l[6] | (l[7] << 16)};
+  f16_range_fault(fault, !ok);
+}
+__device__ __forceinline__ void store_split2h1(bf16_t* p, int64_t ld, float x, unsigned* fault) {
+  uint32_t h, l;
+  const bool ok = split_f16(x, h, l);
+  p[0] = (bf16_t)h;
+  p[ld] = (bf16_t)l;
+  f16_range_fault(fault, !ok);
+}
+
 // erf for the GELU epilogues, faithful to fp32 erff (≤ 1.2 ulp over the whole range, tools/erf_check.py; the
 // reference's GELU is exact-erf, dinov2 layers/mlp.py:29-39 / nn.GELU): two minimax pieces evaluated branch-free
 // and selected per lane —

@@ -14,7 +14,7 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
                                                         const float* __restrict__ w, const float* __restrict__ b,
                                                         float eps, float* __restrict__ yf, void* __restrict__ ylp,
                                                         int lp_bf16, int64_t ldy, int group, int64_t gstride,
-                                                        int row_off) {
+                                                        int row_off, unsigned* fault) {
   constexpr int DIM = 256 * NV;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -50,6 +50,8 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     if (ylp) {
       if (lp_bf16 == 2) {  // split operand row: [hi | lo], 2*ldy wide
         store_split3(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y);
+      } else if (lp_bf16 == 4) {  // MAPA_F16X2 split row
+        store_split2h(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y, fault);
       } else if (lp_bf16) {  // 1 = bf16, 3 = fp16
         uint2 pk;
         pk.x = pack_lp2(lp_bf16 == 3, y[0], y[1]);
@@ -70,7 +72,7 @@ __global__ void __launch_bounds__(256) layernorm8_kernel(const float* __restrict
                                                          const float* __restrict__ w, const float* __restrict__ b,
                                                          float eps, float* __restrict__ yf, void* __restrict__ ylp,
                                                          int lp_bf16, int64_t ldy, int group, int64_t gstride,
-                                                         int row_off) {
+                                                         int row_off, unsigned* fault) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -134,6 +136,8 @@ __global__ void __launch_bounds__(256) layernorm8_kernel(const float* __restrict
         bf16_t* dst = reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c;
         *reinterpret_cast<uint4*>(dst) = hv;
         *reinterpret_cast<uint4*>(dst + ldy) = lv;
+      } else if (lp_bf16 == 4) {  // MAPA_F16X2 split row
+        store_split2h_x8(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y[0], y[1], fault);
       } else if (lp_bf16) {  // 1 = bf16, 3 = fp16
         const bool h = lp_bf16 == 3;
         uint4 pk;
@@ -160,23 +164,26 @@ extern "C" int mapa_layernorm(const float* x, int64_t ldx, int rows, int dim, co
   MAPA_CHECK_ARG(dim == 768 || dim == 1024 || dim == 512 || dim == 256, "mapa_layernorm: dim %d unsupported", dim);
   MAPA_CHECK_ARG(ldx % 4 == 0 && ldy % 4 == 0, "mapa_layernorm: strides must be multiples of 4");
   const dim3 grid((rows + 3) / 4), blk(256);
-  MAPA_CHECK_ARG(lp_dtype == MAPA_F32 || lp_dtype == MAPA_BF16 || lp_dtype == MAPA_BF16X3 || lp_dtype == MAPA_F16,
+  MAPA_CHECK_ARG(lp_dtype == MAPA_F32 || lp_dtype == MAPA_BF16 || lp_dtype == MAPA_BF16X3 || lp_dtype == MAPA_F16 ||
+                     lp_dtype == MAPA_F16X2,
                  "mapa_layernorm: bad lp_dtype");
-  const int bf = lp_dtype == MAPA_BF16X3 ? 2 : lp_dtype == MAPA_BF16 ? 1 : lp_dtype == MAPA_F16 ? 3 : 0;
+  const int bf = lp_dtype == MAPA_BF16X3 ? 2 : lp_dtype == MAPA_BF16 ? 1 : lp_dtype == MAPA_F16 ? 3
+                 : lp_dtype == MAPA_F16X2 ? 4 : 0;
+  unsigned* fault = mapa_gemm_impl::fault_word();
   static const bool f4_only = getenv("MAPA_LN_F4") != nullptr;  // A/B: the float4-per-lane kernel for every width
   // 1024 wide: 8-channel groups (kbench 13.2 -> 12.4 us); 768 wide keeps float4 lanes (10.0 vs 10.5: half the
   // lanes would idle in the second group)
   if (dim == 1024 && ldx % 8 == 0 && ldy % 8 == 0 && !f4_only) {
     hipLaunchKernelGGL(layernorm8_kernel<2>, grid, blk, 0, stream, x, ldx, rows, dim, w, b, eps, y_f32, y_lp, bf, ldy,
-                       in_group, in_group_stride, in_row_off);
+                       in_group, in_group_stride, in_row_off, fault);
     MAPA_CHECK_LAUNCH("mapa_layernorm");
     return 0;
   }
   switch (dim / 256) {
-    case 1: hipLaunchKernelGGL(layernorm_kernel<1>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off); break;
-    case 2: hipLaunchKernelGGL(layernorm_kernel<2>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off); break;
-    case 3: hipLaunchKernelGGL(layernorm_kernel<3>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off); break;
-    default: hipLaunchKernelGGL(layernorm_kernel<4>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off); break;
+    case 1: hipLaunchKernelGGL(layernorm_kernel<1>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off, fault); break;
+    case 2: hipLaunchKernelGGL(layernorm_kernel<2>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off, fault); break;
+    case 3: hipLaunchKernelGGL(layernorm_kernel<3>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off, fault); break;
+    default: hipLaunchKernelGGL(layernorm_kernel<4>, grid, blk, 0, stream, x, ldx, rows, w, b, eps, y_f32, y_lp, bf, ldy, in_group, in_group_stride, in_row_off, fault); break;
   }
   MAPA_CHECK_LAUNCH("mapa_layernorm");
   return 0;

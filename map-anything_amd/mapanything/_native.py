@@ -15,7 +15,7 @@ import torch
 _LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libmapa.so")
 _lib = None
 
-F32, BF16, BF16X3, F16 = 0, 1, 2, 3
+F32, BF16, BF16X3, F16, F16X2 = 0, 1, 2, 3, 4
 A_DENSE, A_CONV3X3 = 0, 1
 OUT_ROWMAJOR, OUT_PIXSHUF = 0, 1
 ACT_NONE, ACT_GELU, ACT_RELU, ACT_GELU_POST = 0, 1, 2, 3
@@ -28,12 +28,13 @@ EXPORTED = (
     "mapa_linear_small", "mapa_pose_scale_finalize", "mapa_dense_head_out", "mapa_convert_rows",
     "mapa_fill_splitmix", "mapa_postprocess_mask", "mapa_recover_intrinsics", "mapa_denorm_image",
     "mapa_pixel_unshuffle", "mapa_depth_norm_factors", "mapa_pose_inputs", "mapa_add_view_vectors", "mapa_add_f32",
-    "mapa_split_bf16x3", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
+    "mapa_split_bf16x3", "mapa_split_rows", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
     "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_tune",
     "mapa_regressor_head_out", "mapa_stream_check", "mapa_fault_slot_create", "mapa_fault_slot_destroy",
     "mapa_fault_publish", "mapa_fault_status",
 )
 FAULT_LN_BARRIER = 1  # include/mapa.h MAPA_FAULT_LN_BARRIER
+FAULT_F16_RANGE = 2  # include/mapa.h MAPA_FAULT_F16_RANGE
 
 
 class GemmDesc(ctypes.Structure):
@@ -119,6 +120,7 @@ def load_library(path: Optional[str] = None):
     L.mapa_add_view_vectors.argtypes = [vp, i, i, i, vp, vp, i, vp]
     L.mapa_add_f32.argtypes = [vp, vp, i64, vp]
     L.mapa_split_bf16x3.argtypes = [vp, i64, i64, i, i, vp, vp]
+    L.mapa_split_rows.argtypes = [vp, i64, i64, i, i, vp, i, vp]
     L.mapa_view_rays.argtypes = [vp, vp, vp, i, i, i, vp, vp, vp]
     L.mapa_apply_mask.argtypes = [vp, vp, vp, vp, i64, vp]
     L.mapa_confidence_mask.argtypes = [vp, vp, vp, i, i64, f, vp]
@@ -198,6 +200,9 @@ def _fault_message(bits: int) -> str:
     if bits & FAULT_LN_BARRIER:
         return ("a LayerNorm-fused GEMM band barrier timed out on the device (include/mapa.h MAPA_FAULT_LN_BARRIER): "
                 "the normalised rows of that launch are invalid, so this call's outputs were discarded")
+    if bits & FAULT_F16_RANGE:
+        return ("a TF32-equivalent head operand left binary16's range (include/mapa.h MAPA_FAULT_F16_RANGE): this "
+                "call's outputs were discarded; head_precision='fp32' runs the heads fp32-exact")
     return f"device fault word 0x{bits:x}"
 
 
@@ -431,9 +436,9 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     d.out_f32 = None if out_f32 is None else out_f32.data_ptr()
     d.out_lp = None if out_lp is None else out_lp.data_ptr()
     d.out_lp_relu = None if out_lp_relu is None else out_lp_relu.data_ptr()
-    for t in (out_s3, out_s3_relu):
-        if t is not None and t.dtype != torch.bfloat16:
-            raise NativeError("split outputs are bf16 [rows][2*ld]")
+    for t in (out_s3, out_s3_relu):  # MAPA_BF16X3 rows from a bf16 GEMM, MAPA_F16X2 rows from an f16 one
+        if t is not None and t.dtype != (torch.float16 if A.dtype == torch.float16 else torch.bfloat16):
+            raise NativeError("split outputs are [rows][2*ld] of the GEMM's 16-bit dtype (bf16 or f16)")
     d.out_s3 = None if out_s3 is None else out_s3.data_ptr()
     d.out_s3_relu = None if out_s3_relu is None else out_s3_relu.data_ptr()
     d.ldo = ldo if ldo is not None else N
@@ -462,7 +467,7 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
         check(lib().mapa_gemm(ctypes.byref(d), stream()), "mapa_gemm")
     # split-precision GEMMs (K = 3 x the logical K) are timed as their own class: executed MFMA flops; residual
     # linears with their output LayerNorm (ln=) too ("gemm_ln": the GEMM flops over the fused launch's time)
-    kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if split_a else "") + \
+    kind = ("conv3x3" if conv is not None else "gemm") + ("_split" if getattr(W, "_mapa_split", False) else "") + \
         ("_ln" if ln is not None else "")
     if _LAUNCH_LOG is not None:
         _LAUNCH_LOG.append(f"{kind}:{M}x{N}x{K}" + (f":{conv[1]}x{conv[2]}s{conv[5]}" if conv is not None else "")
@@ -502,11 +507,12 @@ def attention(q, k, v, o, *, batch, heads, seq_q, seq_kv, q_bstride, q_rstride, 
 
 def layernorm(x, rows, dim, w, b, *, eps=1e-6, ldx=None, y_f32=None, y_lp=None, y_s3=None, ldy=None, group=0,
               group_stride=0, row_off=0):
-    """y_s3: split-precision operand rows (bf16 [rows][2*ldy], [hi | lo]) instead of y_lp."""
+    """y_s3: split-precision operand rows ([rows][2*ldy], [hi | lo]: bf16 = MAPA_BF16X3, f16 = MAPA_F16X2) instead of
+    y_lp."""
     if y_s3 is not None:
-        if y_lp is not None or y_s3.dtype != torch.bfloat16:
-            raise NativeError("layernorm: y_s3 (bf16) replaces y_lp")
-        y_lp, lp_dtype = y_s3, BF16X3
+        if y_lp is not None or y_s3.dtype not in (torch.bfloat16, torch.float16):
+            raise NativeError("layernorm: y_s3 (bf16 or f16 split rows) replaces y_lp")
+        y_lp, lp_dtype = y_s3, (F16X2 if y_s3.dtype == torch.float16 else BF16X3)
     else:
         lp_dtype = dt_code(y_lp.dtype) if y_lp is not None else F32
     tok = _tic()
@@ -530,11 +536,13 @@ def add_rowvec(x, ldx, r0, r1, dim, vec):
 
 
 def bilinear_ac(inp, n, IH, IW, C, OHf, OWf, OH, OW, out, split_out=False):
-    """split_out: out is a split-precision operand (bf16 [pixels][2*C], [hi | lo])."""
-    if split_out and out.dtype != torch.bfloat16:
-        raise NativeError("bilinear_ac: split output is bf16")
-    check(lib().mapa_bilinear_ac(ptr(inp), dt_code(inp.dtype), n, IH, IW, C, OHf, OWf, OH, OW, ptr(out),
-                                 BF16X3 if split_out else dt_code(out.dtype), stream()), "mapa_bilinear_ac")
+    """split_out: out is a split-precision operand ([pixels][2*C], [hi | lo]: bf16 = MAPA_BF16X3, f16 =
+    MAPA_F16X2)."""
+    if split_out and out.dtype not in (torch.bfloat16, torch.float16):
+        raise NativeError("bilinear_ac: split output is bf16 or f16")
+    sdt = (F16X2 if out.dtype == torch.float16 else BF16X3) if split_out else dt_code(out.dtype)
+    check(lib().mapa_bilinear_ac(ptr(inp), dt_code(inp.dtype), n, IH, IW, C, OHf, OWf, OH, OW, ptr(out), sdt,
+                                 stream()), "mapa_bilinear_ac")
 
 
 def mean_tokens(x, n, T, C, y):
@@ -569,6 +577,16 @@ def split_bf16x3(x, rows, cols, cols_padded, y, ldx=None):
         raise AssertionError("split_bf16x3: fp32 input, bf16 output of rows x 2*cols_padded")
     check(lib().mapa_split_bf16x3(ptr(x), cols if ldx is None else ldx, rows, cols, cols_padded, ptr(y), stream()),
           "mapa_split_bf16x3")
+
+
+def split_rows(x, rows, cols, cols_padded, y, ldx=None):
+    """x fp32 [rows][cols] -> y [rows][2*cols_padded] = [hi | lo]: the bf16 split (MAPA_BF16X3) for a bf16 y, the
+    TF32-equivalent binary16 split (MAPA_F16X2) for an f16 y (mapa.h mapa_split_rows)."""
+    if x.dtype != torch.float32 or y.dtype not in (torch.bfloat16, torch.float16) or \
+            y.numel() < rows * 2 * cols_padded:
+        raise AssertionError("split_rows: fp32 input, bf16 / f16 output of rows x 2*cols_padded")
+    check(lib().mapa_split_rows(ptr(x), cols if ldx is None else ldx, rows, cols, cols_padded, ptr(y),
+                                F16X2 if y.dtype == torch.float16 else BF16X3, stream()), "mapa_split_rows")
 
 
 def fill_splitmix(out, seed, half, mid):

@@ -104,6 +104,23 @@ class GeoInputs:
 KBLOCK = 32  # channel block of the head convs' K order (include/mapa.h conv_kblock)
 
 
+def _f16x2_pack(w: np.ndarray, dev) -> torch.Tensor:
+    """[out][taps][cin] fp32 -> binary16 [out][taps * 2 * ceil8(cin)] = [w | w] per tap: the weight side of the
+    TF32-equivalent heads (activations stored [hi | lo] of binary16, include/mapa.h MAPA_F16X2), a plain f16 GEMM over
+    K = 2C that accumulates w*(x_hi + x_lo): the weight at 11 significant bits as TF32 rounds it, the activation at 22."""
+    o, taps, cin = w.shape
+    wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+    if bool((wt.abs() > 65504).any()):
+        raise ValueError("a head weight exceeds binary16's range: use head_precision='fp32'")
+    h = wt.to(torch.float16)
+    cp = _ceil8(cin)
+    out = torch.zeros(o, taps, 2, cp, dtype=torch.float16, device=dev)
+    out[:, :, 0, :cin], out[:, :, 1, :cin] = h, h
+    out = out.reshape(o, -1)
+    out._mapa_split = True  # timed with the split heads (nat.gemm: "gemm_split" / "conv3x3_split")
+    return out
+
+
 def _split_pack(w: np.ndarray, dev) -> torch.Tensor:
     """[out][taps][cin] fp32 -> bf16 [out][taps * 3 * ceil8(cin)] = [hi | lo | hi] per tap: the weight side of a
     split-precision GEMM against activations stored [hi | lo] and read as [hi | hi | lo] (mapa_split_bf16x3 / the
@@ -125,10 +142,11 @@ class PackedWeights:
     heads' GEMM weights are packed for split-precision operands (the reference's fp32 heads in bf16 mode)."""
 
     def __init__(self, sd: Dict[str, object], device, lp_dtype: torch.dtype, info: InfoSharingSpec = RELEASED_INFO,
-                 head_split: bool = False):
+                 head_split: bool = False, head_fmt: str = "bf16x3"):
         self.device = device
         self.lp = lp_dtype
         self.head_split = head_split
+        self.head_fmt = head_fmt
         self.sd = sd
         g = self._get
         dev = device
@@ -153,7 +171,7 @@ class PackedWeights:
 
         def hpack(w):  # head weights [out][taps][cin]: lp (or fp32) [out][taps*cin], or split-packed
             if head_split:
-                return _split_pack(w, dev)
+                return _f16x2_pack(w, dev) if head_fmt == "f16x2" else _split_pack(w, dev)
             return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev, self.lp)
 
         def hlin(name):
@@ -341,34 +359,44 @@ class MapaEngine:
                  info: InfoSharingSpec = RELEASED_INFO, heads: str = "fp32"):
         if precision not in ("bf16", "fp16", "fp32"):
             raise ValueError(f"precision must be 'bf16', 'fp16' or 'fp32', got {precision}")
-        if heads not in ("fp32", "bf16"):
-            raise ValueError(f"heads must be 'fp32' (the reference's recipe) or 'bf16' (fast mode), got {heads}")
-        if precision == "fp16" and heads != "fp32":
-            raise ValueError("the fp16 recipe runs the heads fp32-exact (heads='fp32'); the bf16-heads fast mode is bf16")
+        if heads not in ("tf32", "fp32", "bf16"):
+            raise ValueError(f"heads must be 'tf32' (the reference's GPU recipe), 'fp32' (fp32-exact) or 'bf16' (fast "
+                             f"mode), got {heads}")
+        if precision == "fp16" and heads == "bf16":
+            raise ValueError("the bf16-heads fast mode is bf16; the fp16 recipe runs the heads at 'tf32' or 'fp32'")
         nat.lib()  # fail loudly without the HIP library / a gfx950 device
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.precision = precision
         # operand dtype of the encoder / transformer GEMMs and attention: bf16 or fp16 autocast (model.py:2287-2302)
         self.lp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[precision]
-        # heads at the reference's fp32 under autocast: split-precision bf16 operands (hsplit); fp32 mode is exact
+        # heads under autocast run as the reference runs them, autocast disabled (model.py:1774), as split operands
+        # (hsplit): heads='tf32' — the reference's GPU recipe, whose fp32 convs / linears run TF32 (cudnn's default,
+        # matmul.allow_tf32 = True at model.py:93): binary16 [hi | lo] activations against f16 weights [w | w]
+        # (MAPA_F16X2, 2x the bf16 MFMA work); heads='fp32': fp32-exact split bf16 [hi | lo] read as [hi | hi | lo]
+        # against [hi | lo | hi] (MAPA_BF16X3, 3x).  fp32 mode is exact throughout.
         self.heads = "fp32" if precision == "fp32" else heads
-        self.hsplit = precision != "fp32" and heads == "fp32"
+        self.hsplit = precision != "fp32" and heads in ("tf32", "fp32")
+        self.hfmt = "f16x2" if self.hsplit and heads == "tf32" else "bf16x3"
         self._sd = sd  # host state dict: the geometric encoders are packed on first use
         self.info = info
         with torch.cuda.device(self.device):
-            self.w = PackedWeights(sd, self.device, self.lp, info, head_split=self.hsplit)
+            self.w = PackedWeights(sd, self.device, self.lp, info, head_split=self.hsplit, head_fmt=self.hfmt)
 
     # ------------------------------------------------------------------------- head operands (model.py:1774)
     def _hop(self, rows, C):
-        """Operand buffer of a head GEMM/conv input with C channels: split rows [hi | lo] (bf16, 2C wide; read as
-        the logical K blocks [hi | hi | lo]) when the heads run at the reference's fp32 in bf16 mode, else lp rows."""
+        """Operand buffer of a head GEMM/conv input with C channels: split rows [hi | lo], 2C wide — binary16 for the
+        TF32-equivalent heads (read as a plain 2C-wide f16 operand), bf16 for the fp32-exact ones (read as the
+        logical K blocks [hi | hi | lo]) — when the heads run split under autocast, else lp rows."""
         if self.hsplit:
-            return torch.empty(rows, 2 * C, dtype=torch.bfloat16, device=self.device)
+            dt = torch.float16 if self.hfmt == "f16x2" else torch.bfloat16
+            return torch.empty(rows, 2 * C, dtype=dt, device=self.device)
         return self._empty(rows, C)
 
     def _hw(self, C):
-        """Logical per-pixel K width of a head input with C channels (3C for split operands)."""
-        return 3 * C if self.hsplit else C
+        """Logical per-pixel K width of a head input with C channels (2C / 3C for the f16x2 / bf16x3 split)."""
+        if not self.hsplit:
+            return C
+        return 2 * C if self.hfmt == "f16x2" else 3 * C
 
     def _hout(self, buf=None, relu=None):
         """GEMM output keywords writing head operands: out_s3 / out_s3_relu in split mode, else out_lp / _relu."""
@@ -384,7 +412,7 @@ class MapaEngine:
         R, C = x_f32.shape
         if self.hsplit:
             y = self._hop(R, C)
-            nat.split_bf16x3(x_f32.contiguous(), R, C, C, y)
+            nat.split_rows(x_f32.contiguous(), R, C, C, y)
             return y
         return x_f32.to(self.lp).contiguous()
 
@@ -823,10 +851,10 @@ class MapaEngine:
         return self.dpt_regress(owned, VB, 8 * hp, 8 * wp, H, W, head, join)  # freed after its first conv
 
     def fused_head_out(self):
-        """Whether the regressor's conv2 can carry the dense head in its epilogue (mapa_regressor_head_out: bf16
-        operands, channel-block-major conv weight).  MAPA_FUSED_HEAD=0 keeps the two launches (A/B)."""
+        """Whether the regressor's conv2 can carry the dense head in its epilogue (mapa_regressor_head_out: bf16 or
+        f16 operands, channel-block-major conv weight).  MAPA_FUSED_HEAD=0 keeps the two launches (A/B)."""
         c2 = self.w.reg_c2
-        return (c2.dtype == torch.bfloat16 and getattr(c2, "_mapa_kblock", 0) == 32
+        return (c2.dtype in (torch.bfloat16, torch.float16) and getattr(c2, "_mapa_kblock", 0) == 32
                 and os.environ.get("MAPA_FUSED_HEAD", "1") != "0")
 
     def _hconv3(self, x, n, IH, IW, C, wmat, Cout, stride=1, **epi):
@@ -1066,7 +1094,13 @@ class MapaEngine:
                     first = self.head_rows(fused_f32[:VB * T])
             inter, fin_lp, tok = self.aat(fused_lp, VB, T, taps, shard=shard, comm=comm, pe_idx=pe_idx,
                                           fused_f32=fused_f32, scenes=B)
-            if fault is not None:
+            # the device fault word is published after the transformer — or, when the TF32-equivalent heads can
+            # raise MAPA_FAULT_F16_RANGE, once the last binary16 split operand exists: right before the regressor's
+            # last conv (which writes fp32 outputs only), so ~1 ms of GPU work is still queued when the host sees
+            # the slot and returns (run_heads; MAPA_FAULT_AT=transformer forces the early point, =end the very end)
+            at = os.environ.get("MAPA_FAULT_AT", "last_conv")
+            late = self.hfmt == "f16x2" and self.hsplit and at != "transformer"
+            if fault is not None and not late:
                 fault.publish()
             if len(inter) == 3:
                 first, l11, l17 = inter
@@ -1074,10 +1108,15 @@ class MapaEngine:
                 if first is None:
                     first = self.head_rows(fused_f32[:VB * T])
                 l11, l17 = inter
-            return self.run_heads(first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=taps, dpt_chunk=dpt_chunk,
-                              scenes=B)
+            pending = [fault if late else None]
+            out = self.run_heads(first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=taps, dpt_chunk=dpt_chunk,
+                                 scenes=B, fault=pending if at != "end" else None)
+            if pending[0] is not None:  # not published inside the heads (chunked dense head, unfused, "end")
+                pending[0].publish()
+            return out
 
-    def run_heads(self, first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=None, dpt_chunk=None, scenes: int = 1):
+    def run_heads(self, first, l11, l17, fin_lp, tok, VB, hp, wp, H, W, taps=None, dpt_chunk=None, scenes: int = 1,
+                  fault=None):
         """downstream_head + output assembly (model.py:1774-1923): pose head on the final features, scale head on the
         scale-token feature, DPT + regressor + dense head on [first, l11, l17, final].  first / l11 / l17 / fin_lp are
         head operands (head_rows: split rows in the bf16 recipe, fp32 rows in fp32 mode; fin_lp may carry the scale
@@ -1113,7 +1152,15 @@ class MapaEngine:
                     scale_img.view(B, V).copy_(scale.view(B, 1).expand(B, V))
             joined = [side is None]
 
-            def join():
+            one_pass = not dpt_chunk or int(dpt_chunk) >= VB
+
+            def join():  # before the last conv of the (single-pass) dense head: its inputs are all written by then
+                if one_pass and fault is not None and fault[0] is not None:
+                    if not joined[0]:
+                        cur.wait_stream(side)
+                        joined[0] = True
+                    fault[0].publish()  # the last binary16 split operand exists (run())
+                    fault[0] = None
                 if not joined[0]:
                     cur.wait_stream(side)
                     joined[0] = True

@@ -10,9 +10,13 @@ Differences that are by design:
     checkpoint; there is no hub download (no network on this box),
   * `precision="bf16"` (default) mirrors `infer(use_amp=True, amp_dtype="bf16")` (`amp_dtype="fp16"` the same on
     fp16 operands) — bf16 encoder/transformer, the
-    geometric encoders and the downstream heads fp32-exact as the reference runs them with autocast disabled
-    (model.py:1377, 1774; split-precision bf16 GEMMs on MI355X); `use_amp=False` (or precision="fp32") runs the
-    exact-fp32 MFMA path; `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
+    geometric encoders and the downstream heads as the reference runs them with autocast disabled (model.py:1377,
+    1774): the geometric encoders fp32-exact (split-precision bf16 GEMMs on MI355X), the heads by default
+    (`head_precision="tf32"`) at the precision the reference's fp32 head convs / linears get on its own GPUs — TF32
+    (cudnn's default; matmul.allow_tf32 = True at model.py:93) — as binary16 split activations against f16 weights
+    (both TF32 operands round to 11 significant bits; here only the weight does); `head_precision="fp32"` keeps the
+    fp32-exact split-bf16 heads; `use_amp=False` (or precision="fp32") runs the exact-fp32 MFMA path;
+    `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
   * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687): image-only scenes run as ONE engine
     call (encoder, frame layers and heads over all B x V images, global attention, scale token and scale head per
     scene, as the reference's batched forward, model.py:687-721); scenes with geometric inputs or on a view-sharded
@@ -86,7 +90,7 @@ class MapAnything:
                  geometric_input_config: Dict, fusion_norm_layer=None, pretrained_checkpoint_path: str = None,
                  load_specific_pretrained_submodules: bool = False, specific_pretrained_submodules: list = None,
                  torch_hub_force_reload: bool = False, precision: str = "bf16", hip_graphs: bool = True,
-                 head_precision: str = "fp32"):
+                 head_precision: str = "tf32"):
         _check_config(encoder_config, info_sharing_config, pred_head_config)
         self.info = InfoSharingSpec.from_config(info_sharing_config)
         self.name = name
@@ -101,8 +105,8 @@ class MapAnything:
                                     specific_pretrained_submodules=specific_pretrained_submodules,
                                     torch_hub_force_reload=torch_hub_force_reload)
         self.precision = precision
-        if head_precision not in ("fp32", "bf16"):
-            raise ValueError(f"head_precision must be 'fp32' or 'bf16', got {head_precision}")
+        if head_precision not in ("tf32", "fp32", "bf16"):
+            raise ValueError(f"head_precision must be 'tf32', 'fp32' or 'bf16', got {head_precision}")
         self.head_precision = head_precision
         self._sd: Optional[Dict[str, np.ndarray]] = None
         self._engines: Dict[tuple, Any] = {}
@@ -737,7 +741,7 @@ class MapAnything:
         if not memory_efficient:
             return None
         free = torch.cuda.mem_get_info(self._device)[0]
-        per_view = 420 if self.head_precision == "fp32" else 320
+        per_view = 320 if self.head_precision == "bf16" else 420
         return max(1, int(0.95 * free / (per_view * 1024 * 1024)))
 
     def _local_views(self, views):

@@ -49,6 +49,8 @@ def main():
     elif what == "headbranch":  # pose / scale heads on a side-stream branch vs in line
         arms = [("branch", lambda: os.environ.__setitem__("MAPA_HEAD_BRANCH", "1")),
                 ("inline", lambda: os.environ.__setitem__("MAPA_HEAD_BRANCH", "0"))]
+    elif what == "heads":  # TF32-equivalent heads (f16 x2) vs fp32-exact split bf16 heads (x3) vs bf16 fast mode
+        arms = [(h, (lambda h=h: os.environ.__setitem__("MAPA_AB_HEADS", h))) for h in ("tf32", "fp32", "bf16")]
     elif what == "lnfuse":  # residual linears with the next LayerNorm fused: all / N % 256 only / none
         arms = [("all", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 2)), ("n256", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 3)),
                 ("none", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 0))]
@@ -57,7 +59,7 @@ def main():
     models, sd = [], None
     for name, setup in arms:
         setup()
-        m = MapAnything(**released_config()).to(dev).eval()
+        m = MapAnything(**released_config(), head_precision=os.environ.get("MAPA_AB_HEADS", "tf32")).to(dev).eval()
         if sd is None:
             m.load_synthetic_weights()
             sd = m._sd
