@@ -299,10 +299,10 @@ def main():
             "dtype": args.precision, "data": "synthetic (seeded uint8 images, named-PRNG synthetic weights)",
             "head_precision": args.head_precision,
             "precision_recipe": {
-                "tf32": "reference GPU recipe: bf16 autocast encoder + transformer, fp32-exact geometric encoders "
-                        "(split bf16 GEMMs), heads at TF32 precision as the reference's fp32 convs / linears run on its "
-                        "GPUs (cudnn default, matmul.allow_tf32 at model.py:93): binary16 [hi | lo] activations x f16 "
-                        "weights",
+                "tf32": "reference GPU recipe: bf16 autocast encoder + transformer; geometric encoders and heads "
+                        "(autocast disabled, model.py:1377 / 1774) at the TF32 precision the reference's fp32 convs / "
+                        "linears run at on its GPUs (cudnn default, matmul.allow_tf32 at model.py:93): binary16 "
+                        "[hi | lo] activations x f16 weights",
                 "fp32": "reference autocast recipe with fp32-exact geometric encoders and heads (split-precision bf16 "
                         "GEMMs)",
                 "bf16": "bf16 heads (fast mode, not the reference recipe)"}[args.head_precision],

@@ -282,21 +282,24 @@ class PackedWeights:
 
     def geometric(self, sd: Dict[str, object]) -> Dict[str, object]:
         """Kernel-layout weights of the dense (ray, depth) and global (depth-scale, camera) encoders, packed on
-        first use.  The reference runs them with autocast disabled (model.py:1377): fp32 mode keeps fp32 GEMMs; bf16
-        mode runs the dense encoders' convs / linears in split precision (split_bf16x3: weights [hi | lo | hi] per
-        tap against activations [hi | hi | lo], ~2^-16 relative, on the bf16 MFMA pipe)."""
+        first use.  The reference runs them with autocast disabled (model.py:1377), i.e. as fp32 convs / linears that
+        its GPUs run in TF32: fp32 mode keeps fp32 GEMMs; bf16 / fp16 mode runs the dense encoders' convs / linears
+        on split operands in the heads' form (head_fmt): TF32-equivalent binary16 [hi | lo] activations against f16
+        weights [w | w] (MAPA_F16X2), or the fp32-exact split bf16 (weights [hi | lo | hi] per tap against
+        activations read [hi | hi | lo], ~2^-16 relative) with head_precision='fp32' or the bf16 fast-mode heads."""
         if getattr(self, "_geo", None) is not None:
             return self._geo
         dev = self.device
-        split = self.lp != torch.float32  # bf16 / fp16 autocast: the encoders' fp32 GEMMs as split bf16
+        split = self.lp != torch.float32  # bf16 / fp16 autocast: the encoders' fp32 GEMMs on split operands
+        fmt = self.head_fmt if self.head_split else "bf16x3"
 
         def t(name):
             return torch.from_numpy(np.ascontiguousarray(_np(sd[name]))).to(dev)
 
-        def pack(w):  # [out][taps][cin] fp32 -> fp32 [out][taps*cin] or bf16 [out][taps*3*cinp] (hi | lo | hi)
+        def pack(w):  # [out][taps][cin] fp32 -> fp32 [out][taps*cin], or split-packed ([w | w] f16 / [hi | lo | hi])
             if not split:
                 return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev)
-            return _split_pack(w, dev)
+            return _f16x2_pack(w, dev) if fmt == "f16x2" else _split_pack(w, dev)
 
         def c3(name):
             w = _np(sd[f"{name}.weight"])
@@ -316,6 +319,7 @@ class PackedWeights:
                 d["blocks"].append(dict(c1=c3(f"{n}.conv1"), b1=t(f"{n}.conv1.bias"), c2=c3(f"{n}.conv2"),
                                         b2=t(f"{n}.conv2.bias"), sc=l1(f"{n}.shortcut"), sc_b=t(f"{n}.shortcut.bias")))
             d["split"] = split
+            d["fmt"] = fmt
             geo[enc] = d
         for enc in ("depth_scale_encoder", "cam_rot_encoder", "cam_trans_encoder", "cam_trans_scale_encoder"):
             names = ("encoder.0.0.0.0", "encoder.0.0.1", "encoder.0.1", "encoder.1")
@@ -621,13 +625,14 @@ class MapaEngine:
         M = n * hp * wp
         cin = C * PATCH * PATCH
 
-        def operand(x, c):  # GEMM A operand and its logical per-tap width: fp32 as is, or split [hi | lo] bf16
+        def operand(x, c):  # GEMM A operand and its logical per-tap width: fp32 as is, or split [hi | lo]
             if not g["split"]:
                 return x, c
             cp = _ceil8(c)
-            y = self._empty(M, 2 * cp, dtype=torch.bfloat16)
-            nat.split_bf16x3(x, M, c, cp, y)
-            return y, 3 * cp
+            f16 = g.get("fmt") == "f16x2"
+            y = self._empty(M, 2 * cp, dtype=torch.float16 if f16 else torch.bfloat16)
+            nat.split_rows(x, M, c, cp, y)
+            return y, (2 if f16 else 3) * cp
 
         u = self._empty(M, cin, dtype=f32)
         nat.pixel_unshuffle(data, n, H, W, C, PATCH, u, view_div=view_div)

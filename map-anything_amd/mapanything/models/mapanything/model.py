@@ -15,7 +15,8 @@ Differences that are by design:
     (`head_precision="tf32"`) at the precision the reference's fp32 head convs / linears get on its own GPUs — TF32
     (cudnn's default; matmul.allow_tf32 = True at model.py:93) — as binary16 split activations against f16 weights
     (both TF32 operands round to 11 significant bits; here only the weight does); `head_precision="fp32"` keeps the
-    fp32-exact split-bf16 heads; `use_amp=False` (or precision="fp32") runs the exact-fp32 MFMA path;
+    fp32-exact split-bf16 heads (the default of the fp16 recipe, amp_dtype="fp16", whose transformer rounds 8x finer
+    than bf16: its tolerance is the reference's own fp16 spread measured with exact fp32 heads); `use_amp=False` (or precision="fp32") runs the exact-fp32 MFMA path;
     `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
   * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687): image-only scenes run as ONE engine
     call (encoder, frame layers and heads over all B x V images, global attention, scale token and scale head per
@@ -90,7 +91,7 @@ class MapAnything:
                  geometric_input_config: Dict, fusion_norm_layer=None, pretrained_checkpoint_path: str = None,
                  load_specific_pretrained_submodules: bool = False, specific_pretrained_submodules: list = None,
                  torch_hub_force_reload: bool = False, precision: str = "bf16", hip_graphs: bool = True,
-                 head_precision: str = "tf32"):
+                 head_precision: Optional[str] = None):
         _check_config(encoder_config, info_sharing_config, pred_head_config)
         self.info = InfoSharingSpec.from_config(info_sharing_config)
         self.name = name
@@ -105,9 +106,10 @@ class MapAnything:
                                     specific_pretrained_submodules=specific_pretrained_submodules,
                                     torch_hub_force_reload=torch_hub_force_reload)
         self.precision = precision
-        if head_precision not in ("tf32", "fp32", "bf16"):
-            raise ValueError(f"head_precision must be 'tf32', 'fp32' or 'bf16', got {head_precision}")
-        self.head_precision = head_precision
+        if head_precision not in (None, "tf32", "fp32", "bf16"):
+            raise ValueError(f"head_precision must be 'tf32', 'fp32' or 'bf16' (None: the recipe's default), got "
+                             f"{head_precision}")
+        self.head_precision = head_precision  # None: "tf32" under bf16 autocast, "fp32" under fp16 autocast
         self._sd: Optional[Dict[str, np.ndarray]] = None
         self._engines: Dict[tuple, Any] = {}
         self._device = torch.device("cpu")
@@ -288,6 +290,13 @@ class MapAnything:
     def device(self) -> torch.device:
         return self._device
 
+    def heads_for(self, precision: str) -> str:
+        """The head precision a run at `precision` uses: head_precision, or by default 'tf32' (the reference's GPU
+        recipe) under bf16 autocast and 'fp32' under the fp16 recipe."""
+        if self.head_precision is not None:
+            return self.head_precision
+        return "fp32" if precision == "fp16" else "tf32"
+
     def engine(self, precision: Optional[str] = None):
         prec = precision or self.precision
         if self._sd is None:
@@ -295,10 +304,11 @@ class MapAnything:
                                "load_synthetic_weights()")
         if self._device.type != "cuda":
             raise nat.NativeError("MapAnything (MI355X engine) runs on a gfx950 device only: call .to('cuda')")
-        key = (str(self._device), prec, self.head_precision)
+        heads = self.heads_for(prec)
+        key = (str(self._device), prec, heads)
         if key not in self._engines:
             from .engine import MapaEngine
-            self._engines[key] = MapaEngine(self._sd, self._device, prec, self.info, heads=self.head_precision)
+            self._engines[key] = MapaEngine(self._sd, self._device, prec, self.info, heads=heads)
         return self._engines[key]
 
     def enable_view_sharding(self, group=None, comm=None, gather_outputs: Optional[str] = None):
@@ -741,7 +751,7 @@ class MapAnything:
         if not memory_efficient:
             return None
         free = torch.cuda.mem_get_info(self._device)[0]
-        per_view = 320 if self.head_precision == "bf16" else 420
+        per_view = 320 if self.heads_for(self.precision) == "bf16" else 420
         return max(1, int(0.95 * free / (per_view * 1024 * 1024)))
 
     def _local_views(self, views):

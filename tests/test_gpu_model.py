@@ -376,9 +376,11 @@ def test_fp32_geometric_fused_tap(model, golden):
     assert rel_l2(fused[:, ::tap_step, ::tap_step], g["tap_fused_nhwc"]) < 1e-4
 
 
-def test_bf16_mode_geometric_encoders_are_split_precision(model):
-    """bf16 mode runs the (autocast-disabled, model.py:1377) ray / depth dense encoders as split-precision bf16
-    GEMMs: their features stay within 1e-4 of the exact-fp32 engine's (plain bf16 operands would be ~3e-3)."""
+@pytest.mark.parametrize("heads", ["fp32", "tf32"])
+def test_bf16_mode_geometric_encoders_are_split_precision(model, heads):
+    """bf16 mode runs the (autocast-disabled, model.py:1377) ray / depth dense encoders on split operands in the heads'
+    form: fp32-exact split bf16 (head_precision='fp32') within 1e-4 of the exact-fp32 engine's features, the
+    TF32-equivalent binary16 split (the default) within 1e-3 (plain bf16 operands would be ~3e-3)."""
     from mapanything.utils.inference import preprocess_input_views_for_inference, validate_input_views_for_inference
 
     case = CASES["mixed_224"]
@@ -392,14 +394,21 @@ def test_bf16_mode_geometric_encoders_are_split_precision(model):
     geo = model._geo_inputs(views, None, metric)
     V, H, W = case["views"], case["h"], case["w"]
     feats = {}
-    for prec in ("fp32", "bf16"):
-        eng = model.engine(prec)
+    saved = model.head_precision
+    model.head_precision = heads
+    try:
+        engines = {prec: model.engine(prec) for prec in ("fp32", "bf16")}
+    finally:
+        model.head_precision = saved
+    for prec, eng in engines.items():
         g = eng.w.geometric(eng._sd)
         assert g["ray_dirs_encoder"]["split"] == (prec == "bf16")
+        if prec == "bf16":
+            assert g["ray_dirs_encoder"]["fmt"] == ("f16x2" if heads == "tf32" else "bf16x3")
         feats[prec] = (eng._dense_rep(geo.rays.contiguous(), V, H, W, 3, g["ray_dirs_encoder"]).cpu(),
                        eng._dense_rep(geo.depth.contiguous(), V, H, W, 1, g["depth_encoder"]).cpu())
     for a, b in zip(feats["bf16"], feats["fp32"]):
-        assert rel_l2(a, b) < 1e-4
+        assert rel_l2(a, b) < (1e-4 if heads == "fp32" else 1e-3)
 
 
 def test_ignore_all_geometric_inputs_is_image_only(model):
