@@ -14,7 +14,8 @@ if [[ $PART == *1* ]]; then
 timeout -k 10 700 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/bench_rocprof.json 2> gpurun_out/rocprof.err || { tail -20 gpurun_out/rocprof.err; exit 1; }
 fi
 if [[ $PART == *e* ]]; then
-export MAPA_HIP_GRAPHS=0
+# eager, and the pose / scale branch in line, so no two kernels overlap in the per-kind / per-shape trace
+export MAPA_HIP_GRAPHS=0 MAPA_HEAD_BRANCH=0
 S="--steps 2 --warmup 1 --no-kernel-timing"
 MAPA_LAUNCH_SHAPES=1 MAPA_LAUNCH_LOG=gpurun_out/prof_e/launch_log.json timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/prof_e -o run --output-format csv -- $B $S > gpurun_out/prof_e.log 2>&1 || { tail -20 gpurun_out/prof_e.log; exit 1; }
 fi
