@@ -56,7 +56,7 @@ def main():
     ap.add_argument("--res", type=int, default=518)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
                     help="autocast operand dtype of the encoder / transformer (infer(amp_dtype=...)); fp32 = use_amp off")
-    ap.add_argument("--head-precision", default="tf32", choices=["tf32", "fp32", "bf16"],
+    ap.add_argument("--head-precision", default="tf32", choices=["tf32", "tf32x2", "fp32", "bf16"],
                     help="fp32 = the reference's recipe (autocast disabled for the heads); bf16 = fast mode")
     ap.add_argument("--no-fast-mode", action="store_true", help="skip the bf16-heads fast-mode measurement")
     ap.add_argument("--strong-views", type=int, default=100,
@@ -302,7 +302,8 @@ def main():
                 "tf32": "reference GPU recipe: bf16 autocast encoder + transformer; geometric encoders and heads "
                         "(autocast disabled, model.py:1377 / 1774) at the TF32 precision the reference's fp32 convs / "
                         "linears run at on its GPUs (cudnn default, matmul.allow_tf32 at model.py:93): binary16 "
-                        "[hi | lo] activations x f16 weights",
+                        "operands (TF32's 11 significant bits), fp32 accumulation",
+                "tf32x2": "as tf32 with 22-bit activations (binary16 [hi | lo] x f16 weights, 2x the head work)",
                 "fp32": "reference autocast recipe with fp32-exact geometric encoders and heads (split-precision bf16 "
                         "GEMMs)",
                 "bf16": "bf16 heads (fast mode, not the reference recipe)"}[args.head_precision],

@@ -26,7 +26,11 @@ typedef struct ihipStream_t* mapa_stream_t; /* == hipStream_t */
  * accepted as an OUTPUT dtype by mapa_layernorm (y_lp) and mapa_bilinear_ac */
 /* MAPA_F16: IEEE binary16 operands (the fp16 autocast recipe, infer(amp_dtype="fp16")); accepted by mapa_gemm (dense
  * A), mapa_attention, mapa_attn_merge, and as an output dtype of mapa_layernorm / mapa_patchify / mapa_convert_rows */
-/* MAPA_F16X2: TF32-equivalent head operand rows [hi | lo] of binary16 (2x the logical width): v = hi + lo, hi = f16(v),
+/* MAPA_F16 as the TF32-equivalent heads' operand (round 5 default): binary16 activations and weights have exactly
+ * TF32's 11 significant bits, so an f16 mapa_gemm / conv with fp32 accumulation is the reference's TF32 arithmetic for
+ * values in binary16's normal range; mapa_gemm's out_lp / out_lp_relu of an f16 GEMM, mapa_layernorm, mapa_bilinear_ac
+ * (from f32) and mapa_convert_rows write such rows and raise MAPA_FAULT_F16_RANGE on values outside the range.
+ * MAPA_F16X2: TF32-equivalent head operand rows [hi | lo] of binary16 (2x the logical width): v = hi + lo, hi = f16(v),
  * lo = f16(v - hi).  Read by mapa_gemm with dtype MAPA_F16 as a plain 2C-wide operand against f16 weights packed
  * [w | w] (the conv's channels doubled), written by mapa_gemm's out_s3 / out_s3_relu when dtype is MAPA_F16, and
  * accepted as an output dtype by mapa_layernorm, mapa_bilinear_ac and mapa_split_rows.  A value outside binary16's

@@ -541,7 +541,9 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh) {
   if (a.cv_kb != 32 || a.cv_stride != 1 || a.cv_OH != a.cv_IH || a.cv_OW != a.cv_IW || a.K != 9 * a.cv_C) return false;
   if (!halo_img_ok(a)) return false;
   if (bn == 0) bn = a.N % 256 == 0 ? 256 : 128;
-  if (bh == 8 && bn != 256) return false;
+  // 256-wide tiles only with 8-row blocks (the 148^2 DPT convs): 16-row 256-wide tiles measured slower than 128-wide
+  // ones everywhere (kbench, round 2), and their epilogue no longer unrolls into registers (scratch), so they are gone
+  if ((bh == 8) != (bn == 256)) return false;
   if (a.N % bn != 0 || (a.sp_half != 0x7fffffff && a.sp_half % 32 != 0)) return false;
   const int hw = a.cv_OH * a.cv_OW;
   const int64_t tiles = (int64_t)(a.M / hw) * ((a.cv_OH + bh - 1) / bh) * ((a.cv_OW + BW - 1) / BW) * (a.N / bn);
@@ -550,10 +552,9 @@ bool launch_conv_halo(const GemmArgs& a, int bn, hipStream_t stream, int bh) {
   const HSplit one{1, 0, nullptr, nullptr};
   void (*k)(GemmArgs, HeadOut, HSplit);
   if (a.lp_f16)
-    k = bh == 8 ? conv_halo_kernel<256, false, 8, false, true>
-        : bn == 256 ? conv_halo_kernel<256, false, 16, false, true> : conv_halo_kernel<128, false, 16, false, true>;
+    k = bh == 8 ? conv_halo_kernel<256, false, 8, false, true> : conv_halo_kernel<128, false, 16, false, true>;
   else
-    k = bh == 8 ? conv_halo_kernel<256, false, 8> : bn == 256 ? conv_halo_kernel<256> : conv_halo_kernel<128>;
+    k = bh == 8 ? conv_halo_kernel<256, false, 8> : conv_halo_kernel<128>;
   hipLaunchKernelGGL(k, dim3((unsigned)tiles), dim3(HT), 0, stream, a, none, one);
   return true;
 }

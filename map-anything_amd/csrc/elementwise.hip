@@ -119,7 +119,8 @@ __device__ __forceinline__ void store4(T* p, f32x4 v) {
 // grid-stride form spent more on 64-bit index division than on its memory traffic.
 // BIL_ROWS: output rows per thread (8 for the x2 upsamples: 74 -> 148 60.3 -> 42.3 us, 148 -> 296 split 222 -> 161;
 // 4 for 296 -> 518: 339 -> 254, 264 with 8; kbench 'bil', 8 views, interleaved against the one-row kernel)
-// S3: split operand rows [hi | lo] (2C wide): 1 = bf16 (MAPA_BF16X3), 2 = binary16 (MAPA_F16X2; range faults -> fault)
+// S3: split operand rows [hi | lo] (2C wide): 1 = bf16 (MAPA_BF16X3), 2 = binary16 (MAPA_F16X2; range faults -> fault);
+// 3 = plain binary16 rows (MAPA_F16, the TF32-equivalent heads' operand; range faults -> fault)
 template <typename TI, typename TO, int S3 = 0, int BIL_ROWS = 4>
 __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int IW, int C, int OHf, int OWf, int OH,
                                    int OW, int c8_shift, TO* __restrict__ out, unsigned* fault) {
@@ -166,7 +167,7 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
         load8(base + o11, d0, d1);
       }
       pim = im; py0 = y0; py1 = y1;
-      TO* op = out + ((size_t)rr * OW + ox) * (S3 ? 2 * C : C) + c;
+      TO* op = out + ((size_t)rr * OW + ox) * (S3 == 1 || S3 == 2 ? 2 * C : C) + c;
       const f32x4 r0 = ly0 * (lx0 * a0 + lx1 * b0) + ly1 * (lx0 * c0 + lx1 * d0);
       const f32x4 r1 = ly0 * (lx0 * a1 + lx1 * b1) + ly1 * (lx0 * c1 + lx1 * d1);
       if constexpr (S3 != 0) {  // 8 channels: one 16-B store of hi and one of lo
@@ -177,7 +178,7 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float v0 = k < 2 ? r0[2 * k] : r1[2 * k - 4], v1 = k < 2 ? r0[2 * k + 1] : r1[2 * k - 3];
-          if constexpr (S3 == 2) {
+          if constexpr (S3 >= 2) {
             uint32_t h0, l0, h1, l1;
             ok &= split_f16(v0, h0, l0);
             ok &= split_f16(v1, h1, l1);
@@ -189,7 +190,12 @@ __global__ void bilinear_ac_kernel(const TI* __restrict__ in, int n, int IH, int
             lp[k] = pack_bf16x2(v0 - bf16_to_f32(h0), v1 - bf16_to_f32(h1));
           }
         }
-        if constexpr (S3 == 2) f16_range_fault(fault, !ok);
+        if constexpr (S3 >= 2) f16_range_fault(fault, !ok);
+        if constexpr (S3 == 3) {  // the hi words are the plain binary16 rows
+          typedef uint32_t nt3 __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(nt3{hv.x, hv.y, hv.z, hv.w}, reinterpret_cast<nt3*>(op));
+          continue;
+        }
         typedef uint32_t nt4 __attribute__((ext_vector_type(4)));
         // 1.1 GB at 518^2: streamed past the caches
         __builtin_nontemporal_store(nt4{hv.x, hv.y, hv.z, hv.w}, reinterpret_cast<nt4*>(op));
@@ -350,15 +356,18 @@ __global__ void __launch_bounds__(256) normalize_image_kernel(const uint8_t* __r
 }
 
 __global__ void convert_rows_kernel(const float* __restrict__ src, int64_t lds, int rows, int cols, void* dst,
-                                    int bf, int64_t ldd) {
+                                    int bf, int64_t ldd, unsigned* fault) {
   const int64_t total = (int64_t)rows * cols;
+  bool ok = true;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
     const int c = (int)(e % cols);
     const int64_t r = e / cols;
     const float v = src[r * lds + c];
+    if (bf == 2) ok &= f16_ok(v);
     if (bf) reinterpret_cast<bf16_t*>(dst)[r * ldd + c] = f32_to_lp(bf == 2, v);  // 1 bf16, 2 fp16
     else reinterpret_cast<float*>(dst)[r * ldd + c] = v;
   }
+  f16_range_fault(fault, !ok);
 }
 
 // fp32 rows -> [hi | lo] bf16 column blocks of width cp (zero-padded past cols), hi = bf16(x), lo = bf16(x - hi):
@@ -439,6 +448,7 @@ static void bilinear_launch(const void* in, int in_dtype, int n, int IH, int IW,
   hipLaunchKernelGGL((bilinear_ac_kernel<TI, TO, S, RW>), g, b, 0, stream, (const TI*)in, n, IH, IW, C, OHf, OWf, OH, \
                      OW, c8_shift, (TO*)out, fault)
   if (out_dtype == MAPA_F16X2 && in_dtype == MAPA_F32) MAPA_BIL(float, bf16_t, 2);
+  else if (out_dtype == MAPA_F16 && in_dtype == MAPA_F32) MAPA_BIL(float, bf16_t, 3);
   else if (out_dtype == MAPA_BF16X3 && in_dtype == MAPA_F32) MAPA_BIL(float, bf16_t, 1);
   else if (out_dtype == MAPA_BF16X3) MAPA_BIL(bf16_t, bf16_t, 1);
   else if (in_dtype == MAPA_BF16 && out_dtype == MAPA_BF16) MAPA_BIL(bf16_t, bf16_t, 0);
@@ -456,7 +466,7 @@ extern "C" int mapa_bilinear_ac(const void* in, int in_dtype, int n, int IH, int
                  "mapa_bilinear_ac: too large");
   MAPA_CHECK_ARG((in_dtype == MAPA_F32 || in_dtype == MAPA_BF16) &&
                      (out_dtype == MAPA_F32 || out_dtype == MAPA_BF16 || out_dtype == MAPA_BF16X3 ||
-                      (out_dtype == MAPA_F16X2 && in_dtype == MAPA_F32)),
+                      ((out_dtype == MAPA_F16X2 || out_dtype == MAPA_F16) && in_dtype == MAPA_F32)),
                  "mapa_bilinear_ac: bad dtypes");
   if (OH >= 2 * IH - 1)
     bilinear_launch<8>(in, in_dtype, n, IH, IW, C, OHf, OWf, OH, OW, c8_shift, out, out_dtype, stream);
@@ -542,7 +552,8 @@ extern "C" int mapa_convert_rows(const float* src, int64_t lds, int rows, int co
                                  int64_t ldd, hipStream_t stream) {
   MAPA_CHECK_ARG(src && dst && rows > 0 && cols > 0, "mapa_convert_rows: bad args");
   hipLaunchKernelGGL(convert_rows_kernel, dim3(grid_for((int64_t)rows * cols)), dim3(TPB), 0, stream, src, lds, rows,
-                     cols, dst, dst_dtype == MAPA_BF16 ? 1 : dst_dtype == MAPA_F16 ? 2 : 0, ldd);
+                     cols, dst, dst_dtype == MAPA_BF16 ? 1 : dst_dtype == MAPA_F16 ? 2 : 0, ldd,
+                     mapa_gemm_impl::fault_word());
   MAPA_CHECK_LAUNCH("mapa_convert_rows");
   return 0;
 }

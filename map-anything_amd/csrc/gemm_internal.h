@@ -157,6 +157,7 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
     }
     if (p.out_f32) *reinterpret_cast<f32x4*>(p.out_f32 + off) = v;
     if constexpr (sizeof(T) == 2) {
+      if (p.lp_f16 && (p.out_lp || p.out_lp_relu)) f16_check4(p.fault, v);
       if (p.out_lp) {
         uint2 u;
         u.x = pack_lp2(p.lp_f16, v[0], v[1]);
@@ -197,6 +198,7 @@ __device__ __forceinline__ void epi_store_row(const GemmArgs& p, const EpiCol& c
       if (p.act == MAPA_ACT_GELU_POST) x = gelu_erf(x);
       if (p.out_f32) p.out_f32[o] = x;
       if constexpr (sizeof(T) == 2) {
+        if (p.lp_f16 && (p.out_lp || p.out_lp_relu)) f16_range_fault(p.fault, !f16_ok(x));
         if (p.out_lp) reinterpret_cast<bf16_t*>(p.out_lp)[o] = f32_to_lp(p.lp_f16, x);
         if (p.out_lp_relu) reinterpret_cast<bf16_t*>(p.out_lp_relu)[o] = f32_to_lp(p.lp_f16, fmaxf(x, 0.f));
         if (p.out_s3) {
@@ -287,6 +289,10 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
     *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = v1;
   }
   if constexpr (sizeof(T) == 2) {
+    if (p.lp_f16 && (p.out_lp || p.out_lp_relu)) {
+      f16_check4(p.fault, v0);
+      f16_check4(p.fault, v1);
+    }
     if (p.out_lp) {
       const bool h = p.lp_f16;
       const uint4 u = {pack_lp2(h, v0[0], v0[1]), pack_lp2(h, v0[2], v0[3]), pack_lp2(h, v1[0], v1[1]),
@@ -364,11 +370,15 @@ __device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const Epi
       }
     }
     uint4 u;
-    if (p.lp_f16)
+    if (p.lp_f16) {
+      f16_check4(p.fault, v0);
+      f16_check4(p.fault, v1);
       u = uint4{pack_f16x2(v0[0], v0[1]), pack_f16x2(v0[2], v0[3]), pack_f16x2(v1[0], v1[1]), pack_f16x2(v1[2], v1[3])};
-    else
+    }
+    else {
       u = uint4{pack_bf16x2(v0[0], v0[1]), pack_bf16x2(v0[2], v0[3]), pack_bf16x2(v1[0], v1[1]),
                 pack_bf16x2(v1[2], v1[3])};
+    }
     *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.out_lp) + off) = u;
   } else {
     if (p.gamma) {

@@ -138,6 +138,12 @@ __device__ __forceinline__ bool split_f16(float x, uint32_t& h, uint32_t& l) {
   l = f32_to_f16(x - (float)hh);
   return fabsf(x) <= F16_MAX;
 }
+// binary16 outputs (TF32-equivalent head operands, MAPA_F16; also the fp16 recipe's transformer operands): values
+// outside binary16's range raise MAPA_FAULT_F16_RANGE (NaN compares false and raises too)
+__device__ __forceinline__ bool f16_ok(float x) { return fabsf(x) <= F16_MAX; }
+__device__ __forceinline__ void f16_check4(unsigned* fault, f32x4 v) {
+  f16_range_fault(fault, !(f16_ok(v[0]) && f16_ok(v[1]) && f16_ok(v[2]) && f16_ok(v[3])));
+}
 __device__ __forceinline__ void store_split2h(bf16_t* p, int64_t ld, f32x4 v, unsigned* fault) {
   uint32_t h[4], l[4];
   bool ok = true;

@@ -53,6 +53,7 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
       } else if (lp_bf16 == 4) {  // MAPA_F16X2 split row
         store_split2h(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y, fault);
       } else if (lp_bf16) {  // 1 = bf16, 3 = fp16
+        if (lp_bf16 == 3) f16_check4(fault, y);
         uint2 pk;
         pk.x = pack_lp2(lp_bf16 == 3, y[0], y[1]);
         pk.y = pack_lp2(lp_bf16 == 3, y[2], y[3]);
@@ -140,6 +141,10 @@ __global__ void __launch_bounds__(256) layernorm8_kernel(const float* __restrict
         store_split2h_x8(reinterpret_cast<bf16_t*>(ylp) + (int64_t)row * 2 * ldy + c, ldy, y[0], y[1], fault);
       } else if (lp_bf16) {  // 1 = bf16, 3 = fp16
         const bool h = lp_bf16 == 3;
+        if (h) {
+          f16_check4(fault, y[0]);
+          f16_check4(fault, y[1]);
+        }
         uint4 pk;
         pk.x = pack_lp2(h, y[0][0], y[0][1]);
         pk.y = pack_lp2(h, y[0][2], y[0][3]);

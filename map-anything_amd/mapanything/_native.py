@@ -201,8 +201,9 @@ def _fault_message(bits: int) -> str:
         return ("a LayerNorm-fused GEMM band barrier timed out on the device (include/mapa.h MAPA_FAULT_LN_BARRIER): "
                 "the normalised rows of that launch are invalid, so this call's outputs were discarded")
     if bits & FAULT_F16_RANGE:
-        return ("a TF32-equivalent head operand left binary16's range (include/mapa.h MAPA_FAULT_F16_RANGE): this "
-                "call's outputs were discarded; head_precision='fp32' runs the heads fp32-exact")
+        return ("a binary16 operand (the TF32-equivalent heads, or the fp16 recipe) left binary16's range (include/"
+                "mapa.h MAPA_FAULT_F16_RANGE): this call's outputs were discarded; head_precision='fp32' runs the heads "
+                "fp32-exact")
     return f"device fault word 0x{bits:x}"
 
 

@@ -104,6 +104,22 @@ class GeoInputs:
 KBLOCK = 32  # channel block of the head convs' K order (include/mapa.h conv_kblock)
 
 
+def _f16_pack(w: np.ndarray, dev) -> torch.Tensor:
+    """[out][taps][cin] fp32 -> binary16 [out][taps * ceil8(cin)]: the weight side of the TF32-equivalent heads
+    (activations binary16 too, include/mapa.h MAPA_F16): both operands at TF32's 11 significant bits, fp32
+    accumulation, on the f16 MFMA pipe at the bf16 rate."""
+    o, taps, cin = w.shape
+    wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+    if bool((wt.abs() > 65504).any()):
+        raise ValueError("a head weight exceeds binary16's range: use head_precision='fp32'")
+    cp = _ceil8(cin)
+    out = torch.zeros(o, taps, cp, dtype=torch.float16, device=dev)
+    out[:, :, :cin] = wt.to(torch.float16)
+    out = out.reshape(o, -1)
+    out._mapa_split = True  # timed with the fp32-recipe heads (nat.gemm: "gemm_split" / "conv3x3_split")
+    return out
+
+
 def _f16x2_pack(w: np.ndarray, dev) -> torch.Tensor:
     """[out][taps][cin] fp32 -> binary16 [out][taps * 2 * ceil8(cin)] = [w | w] per tap: the weight side of the
     TF32-equivalent heads (activations stored [hi | lo] of binary16, include/mapa.h MAPA_F16X2), a plain f16 GEMM over
@@ -171,7 +187,7 @@ class PackedWeights:
 
         def hpack(w):  # head weights [out][taps][cin]: lp (or fp32) [out][taps*cin], or split-packed
             if head_split:
-                return _f16x2_pack(w, dev) if head_fmt == "f16x2" else _split_pack(w, dev)
+                return {"f16": _f16_pack, "f16x2": _f16x2_pack}.get(head_fmt, _split_pack)(w, dev)
             return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev, self.lp)
 
         def hlin(name):
@@ -299,7 +315,7 @@ class PackedWeights:
         def pack(w):  # [out][taps][cin] fp32 -> fp32 [out][taps*cin], or split-packed ([w | w] f16 / [hi | lo | hi])
             if not split:
                 return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev)
-            return _f16x2_pack(w, dev) if fmt == "f16x2" else _split_pack(w, dev)
+            return {"f16": _f16_pack, "f16x2": _f16x2_pack}.get(fmt, _split_pack)(w, dev)
 
         def c3(name):
             w = _np(sd[f"{name}.weight"])
@@ -363,9 +379,9 @@ class MapaEngine:
                  info: InfoSharingSpec = RELEASED_INFO, heads: str = "fp32"):
         if precision not in ("bf16", "fp16", "fp32"):
             raise ValueError(f"precision must be 'bf16', 'fp16' or 'fp32', got {precision}")
-        if heads not in ("tf32", "fp32", "bf16"):
-            raise ValueError(f"heads must be 'tf32' (the reference's GPU recipe), 'fp32' (fp32-exact) or 'bf16' (fast "
-                             f"mode), got {heads}")
+        if heads not in ("tf32", "tf32x2", "fp32", "bf16"):
+            raise ValueError(f"heads must be 'tf32' (the reference's GPU recipe), 'tf32x2', 'fp32' (fp32-exact) or "
+                             f"'bf16' (fast mode), got {heads}")
         if precision == "fp16" and heads == "bf16":
             raise ValueError("the bf16-heads fast mode is bf16; the fp16 recipe runs the heads at 'tf32' or 'fp32'")
         nat.lib()  # fail loudly without the HIP library / a gfx950 device
@@ -373,14 +389,15 @@ class MapaEngine:
         self.precision = precision
         # operand dtype of the encoder / transformer GEMMs and attention: bf16 or fp16 autocast (model.py:2287-2302)
         self.lp = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}[precision]
-        # heads under autocast run as the reference runs them, autocast disabled (model.py:1774), as split operands
-        # (hsplit): heads='tf32' — the reference's GPU recipe, whose fp32 convs / linears run TF32 (cudnn's default,
-        # matmul.allow_tf32 = True at model.py:93): binary16 [hi | lo] activations against f16 weights [w | w]
-        # (MAPA_F16X2, 2x the bf16 MFMA work); heads='fp32': fp32-exact split bf16 [hi | lo] read as [hi | hi | lo]
-        # against [hi | lo | hi] (MAPA_BF16X3, 3x).  fp32 mode is exact throughout.
+        # heads under autocast run as the reference runs them, autocast disabled (model.py:1774), on their own operand
+        # form (hsplit): heads='tf32' — the reference's GPU recipe, whose fp32 convs / linears run TF32 (cudnn's
+        # default, matmul.allow_tf32 = True at model.py:93): binary16 activations and weights, TF32's 11 significant
+        # bits each, fp32 accumulation (MAPA_F16, 1x the bf16 MFMA work); 'tf32x2': binary16 [hi | lo] activations
+        # (22 bits) against f16 weights [w | w] (MAPA_F16X2, 2x); 'fp32': fp32-exact split bf16 [hi | lo] read as
+        # [hi | hi | lo] against [hi | lo | hi] (MAPA_BF16X3, 3x).  fp32 mode is exact throughout.
         self.heads = "fp32" if precision == "fp32" else heads
-        self.hsplit = precision != "fp32" and heads in ("tf32", "fp32")
-        self.hfmt = "f16x2" if self.hsplit and heads == "tf32" else "bf16x3"
+        self.hsplit = precision != "fp32" and heads in ("tf32", "tf32x2", "fp32")
+        self.hfmt = ({"tf32": "f16", "tf32x2": "f16x2"}.get(heads, "bf16x3")) if self.hsplit else "bf16x3"
         self._sd = sd  # host state dict: the geometric encoders are packed on first use
         self.info = info
         with torch.cuda.device(self.device):
@@ -391,6 +408,8 @@ class MapaEngine:
         """Operand buffer of a head GEMM/conv input with C channels: split rows [hi | lo], 2C wide — binary16 for the
         TF32-equivalent heads (read as a plain 2C-wide f16 operand), bf16 for the fp32-exact ones (read as the
         logical K blocks [hi | hi | lo]) — when the heads run split under autocast, else lp rows."""
+        if self.hsplit and self.hfmt == "f16":
+            return torch.empty(rows, C, dtype=torch.float16, device=self.device)
         if self.hsplit:
             dt = torch.float16 if self.hfmt == "f16x2" else torch.bfloat16
             return torch.empty(rows, 2 * C, dtype=dt, device=self.device)
@@ -398,22 +417,27 @@ class MapaEngine:
 
     def _hw(self, C):
         """Logical per-pixel K width of a head input with C channels (2C / 3C for the f16x2 / bf16x3 split)."""
-        if not self.hsplit:
+        if not self.hsplit or self.hfmt == "f16":
             return C
         return 2 * C if self.hfmt == "f16x2" else 3 * C
 
     def _hout(self, buf=None, relu=None):
         """GEMM output keywords writing head operands: out_s3 / out_s3_relu in split mode, else out_lp / _relu."""
         d = {}
+        s3 = self.hsplit and self.hfmt != "f16"
         if buf is not None:
-            d["out_s3" if self.hsplit else "out_lp"] = buf
+            d["out_s3" if s3 else "out_lp"] = buf
         if relu is not None:
-            d["out_s3_relu" if self.hsplit else "out_lp_relu"] = relu
+            d["out_s3_relu" if s3 else "out_lp_relu"] = relu
         return d
 
     def head_rows(self, x_f32):
         """fp32 rows [R][C] -> a head operand (module-level API inputs, model.py:1774 fp32 heads)."""
         R, C = x_f32.shape
+        if self.hsplit and self.hfmt == "f16":
+            y = self._hop(R, C)
+            nat.convert_rows(x_f32, x_f32.stride(0), R, C, y, C)  # range-checked (MAPA_FAULT_F16_RANGE)
+            return y
         if self.hsplit:
             y = self._hop(R, C)
             nat.split_rows(x_f32.contiguous(), R, C, C, y)
@@ -450,8 +474,8 @@ class MapaEngine:
                       group_stride=gstride, row_off=off)
 
     def _ln_head(self, x, rows, dim, w, b, out, **kw):
-        """LayerNorm whose output feeds a head: split operand rows in split mode, else lp rows."""
-        if self.hsplit:
+        """LayerNorm whose output feeds a head: split operand rows in split mode, else lp (or binary16) rows."""
+        if self.hsplit and self.hfmt != "f16":
             self._ln(x, rows, dim, w, b, y_s3=out, **kw)
         else:
             self._ln(x, rows, dim, w, b, y_lp=out, **kw)
@@ -629,6 +653,12 @@ class MapaEngine:
             if not g["split"]:
                 return x, c
             cp = _ceil8(c)
+            if g.get("fmt") == "f16":  # binary16 rows, zero-padded to cp
+                y = self._empty(M, cp, dtype=torch.float16)
+                if cp != c:
+                    y[:, c:].zero_()
+                nat.convert_rows(x, c, M, c, y, cp)
+                return y, cp
             f16 = g.get("fmt") == "f16x2"
             y = self._empty(M, 2 * cp, dtype=torch.float16 if f16 else torch.bfloat16)
             nat.split_rows(x, M, c, cp, y)
@@ -943,7 +973,7 @@ class MapaEngine:
                      **({"out_f32": r1} if self.hsplit else {"out_lp": r1}))
         del feat_lp
         r1u = self._hop(n * H * W, 128)
-        nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u, split_out=self.hsplit)
+        nat.bilinear_ac(r1, n, hf, wf, 128, H, W, H, W, r1u, split_out=self.hsplit and self.hfmt != "f16")
         del r1
         if head is not None:
             if join is not None:
@@ -993,7 +1023,7 @@ class MapaEngine:
         nat.gemm(o, d["out"], n * h * w_, 256, self._hw(256), bias=d["out_b"], out_f32=y)
         if lowp:
             out = self._hop(n * oh * ow, 256)
-            nat.bilinear_ac(y, n, h, w_, 256, Hf, Wf, oh, ow, out, split_out=self.hsplit)
+            nat.bilinear_ac(y, n, h, w_, 256, Hf, Wf, oh, ow, out, split_out=self.hsplit and self.hfmt != "f16")
             if taps is not None:
                 f = self._empty(n * oh * ow, 256, dtype=torch.float32)
                 nat.bilinear_ac(y, n, h, w_, 256, Hf, Wf, oh, ow, f)
@@ -1104,7 +1134,7 @@ class MapaEngine:
             # last conv (which writes fp32 outputs only), so ~1 ms of GPU work is still queued when the host sees
             # the slot and returns (run_heads; MAPA_FAULT_AT=transformer forces the early point, =end the very end)
             at = os.environ.get("MAPA_FAULT_AT", "last_conv")
-            late = self.hfmt == "f16x2" and self.hsplit and at != "transformer"
+            late = self.hfmt in ("f16", "f16x2") and self.hsplit and at != "transformer"
             if fault is not None and not late:
                 fault.publish()
             if len(inter) == 3:

@@ -13,8 +13,9 @@ Differences that are by design:
     geometric encoders and the downstream heads as the reference runs them with autocast disabled (model.py:1377,
     1774): the geometric encoders fp32-exact (split-precision bf16 GEMMs on MI355X), the heads by default
     (`head_precision="tf32"`) at the precision the reference's fp32 head convs / linears get on its own GPUs — TF32
-    (cudnn's default; matmul.allow_tf32 = True at model.py:93) — as binary16 split activations against f16 weights
-    (both TF32 operands round to 11 significant bits; here only the weight does); `head_precision="fp32"` keeps the
+    (cudnn's default; matmul.allow_tf32 = True at model.py:93): both operands rounded to 11 significant bits, fp32
+    accumulation — as binary16 operands (the same 11 bits; `"tf32x2"` keeps 22 bits of each activation as a binary16
+    [hi | lo] pair at twice the work); `head_precision="fp32"` keeps the
     fp32-exact split-bf16 heads (the default of the fp16 recipe, amp_dtype="fp16", whose transformer rounds 8x finer
     than bf16: its tolerance is the reference's own fp16 spread measured with exact fp32 heads); `use_amp=False` (or precision="fp32") runs the exact-fp32 MFMA path;
     `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
@@ -106,9 +107,9 @@ class MapAnything:
                                     specific_pretrained_submodules=specific_pretrained_submodules,
                                     torch_hub_force_reload=torch_hub_force_reload)
         self.precision = precision
-        if head_precision not in (None, "tf32", "fp32", "bf16"):
-            raise ValueError(f"head_precision must be 'tf32', 'fp32' or 'bf16' (None: the recipe's default), got "
-                             f"{head_precision}")
+        if head_precision not in (None, "tf32", "tf32x2", "fp32", "bf16"):
+            raise ValueError(f"head_precision must be 'tf32', 'tf32x2', 'fp32' or 'bf16' (None: the recipe's default), "
+                             f"got {head_precision}")
         self.head_precision = head_precision  # None: "tf32" under bf16 autocast, "fp32" under fp16 autocast
         self._sd: Optional[Dict[str, np.ndarray]] = None
         self._engines: Dict[tuple, Any] = {}

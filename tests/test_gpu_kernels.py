@@ -298,7 +298,7 @@ def test_conv3x3_channel_block_k_order(nat, variant, dtype, n, H, W, C, Co, stri
     assert rel_l2(got.cpu(), ref.cpu()) < (1e-5 if dtype == torch.float32 else 1e-4)
 
 
-@pytest.mark.parametrize("variant", [2584, 2585, 2586, 2588])
+@pytest.mark.parametrize("variant", [2584, 2586, 2588])
 @pytest.mark.parametrize("n,H,W,C,Co", [(2, 37, 29, 96, 256), (1, 50, 48, 256, 128), (3, 16, 16, 32, 256),
                                         (1, 148, 148, 256, 256), (2, 13, 21, 64, 256)])
 def test_conv3x3_halo_window(nat, variant, n, H, W, C, Co):

@@ -198,10 +198,10 @@ def test_fp32_taps_match_reference(model, golden):
 # TF32-equivalent heads (f16 weights: 2^-12 per product, the reference's own TF32 rounding of its weights) at 2e-3,
 # an order of magnitude under the reference's own bf16-recipe deviation on every output (golden_bf16_spread.json)
 # and three orders under what a tile-order or split-K indexing error gives
-HEAD_BOUND = {"fp32": 1e-4, "tf32": 2e-3}
+HEAD_BOUND = {"fp32": 1e-4, "tf32x2": 2e-3, "tf32": 3e-3}
 
 
-@pytest.mark.parametrize("heads", ["fp32", "tf32"])
+@pytest.mark.parametrize("heads", ["fp32", "tf32x2", "tf32"])
 def test_split_precision_heads_match_fp32_heads_at_cfg2_size(model, heads):
     """Stage-level pin of the production (bf16-recipe) heads at configs[1]'s size, 8 views at 518x518: the fp32 engine's
     DPT / pose / scale inputs (fusion LayerNorm output, IFR taps L11 / L17, final features + scale token — each pinned
@@ -220,7 +220,7 @@ def test_split_precision_heads_match_fp32_heads_at_cfg2_size(model, heads):
         e32, e16 = model.engine("fp32"), model.engine("bf16")
     finally:
         model.head_precision = saved
-    assert e16.hfmt == ("f16x2" if heads == "tf32" else "bf16x3")
+    assert e16.hfmt == {"tf32": "f16", "tf32x2": "f16x2"}.get(heads, "bf16x3")
     assert not e32.hsplit and e16.hsplit
     taps = {}
     e32.run(imgs, taps=taps)
@@ -245,7 +245,7 @@ def test_split_precision_heads_match_fp32_heads_at_cfg2_size(model, heads):
     assert not bad, bad
     # the mask: identical wherever the logit is not within rounding of the threshold
     lg = res["fp32"]["non_ambiguous_mask_logits"]
-    sure = lg.abs() > (1e-3 if heads == "fp32" else 5e-2)
+    sure = lg.abs() > (1e-3 if heads == "fp32" else 1e-1)
     assert torch.equal(res["split"]["non_ambiguous_mask"][sure], res["fp32"]["non_ambiguous_mask"][sure])
 
 
@@ -376,7 +376,7 @@ def test_fp32_geometric_fused_tap(model, golden):
     assert rel_l2(fused[:, ::tap_step, ::tap_step], g["tap_fused_nhwc"]) < 1e-4
 
 
-@pytest.mark.parametrize("heads", ["fp32", "tf32"])
+@pytest.mark.parametrize("heads", ["fp32", "tf32x2", "tf32"])
 def test_bf16_mode_geometric_encoders_are_split_precision(model, heads):
     """bf16 mode runs the (autocast-disabled, model.py:1377) ray / depth dense encoders on split operands in the heads'
     form: fp32-exact split bf16 (head_precision='fp32') within 1e-4 of the exact-fp32 engine's features, the
@@ -404,11 +404,11 @@ def test_bf16_mode_geometric_encoders_are_split_precision(model, heads):
         g = eng.w.geometric(eng._sd)
         assert g["ray_dirs_encoder"]["split"] == (prec == "bf16")
         if prec == "bf16":
-            assert g["ray_dirs_encoder"]["fmt"] == ("f16x2" if heads == "tf32" else "bf16x3")
+            assert g["ray_dirs_encoder"]["fmt"] == {"tf32": "f16", "tf32x2": "f16x2"}.get(heads, "bf16x3")
         feats[prec] = (eng._dense_rep(geo.rays.contiguous(), V, H, W, 3, g["ray_dirs_encoder"]).cpu(),
                        eng._dense_rep(geo.depth.contiguous(), V, H, W, 1, g["depth_encoder"]).cpu())
     for a, b in zip(feats["bf16"], feats["fp32"]):
-        assert rel_l2(a, b) < (1e-4 if heads == "fp32" else 1e-3)
+        assert rel_l2(a, b) < (1e-4 if heads == "fp32" else 2e-3)
 
 
 def test_ignore_all_geometric_inputs_is_image_only(model):
@@ -687,7 +687,7 @@ def test_infer_raises_on_f16_range_fault(model, graphs):
     views = _views(CASES["cfg1_224"])
     kw = dict(use_amp=True, apply_mask=False)
     eng = model.engine("bf16")
-    assert eng.hfmt == "f16x2"
+    assert eng.hfmt == "f16"
     w = eng.w.refine[4]["resConfUnit2"]["c1"]
     keep = w.clone()
     model.hip_graphs = graphs

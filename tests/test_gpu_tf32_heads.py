@@ -68,11 +68,11 @@ def test_split_rows_f16x2_is_22_bits(nat):
     assert (hi + lo - x).abs().max().item() <= x.abs().max().item() * 2.0 ** -21
 
 
-# variant codes (mapa_gemm_set_variant): 0 automatic; 2584 / 2585 / 2588 halo-window conv (128-wide, 256-wide,
-# 8-row blocks); 2589 flat-raster split-K halo; 2568 / 2571 / 2574 implicit-GEMM tiles; 643 the 128-row kernel;
+# variant codes (mapa_gemm_set_variant): 0 automatic; 2584 / 2588 halo-window conv (128-wide 16-row / 256-wide 8-row
+# blocks); 2589 flat-raster split-K halo; 2568 / 2571 / 2574 implicit-GEMM tiles; 643 the 128-row kernel;
 # 2581 stream-K
 @pytest.mark.parametrize("variant,n,h,w,C,Co", [
-    (0, 2, 40, 40, 256, 256), (2584, 2, 37, 41, 64, 128), (2585, 1, 33, 30, 96, 256), (2588, 1, 34, 29, 64, 256),
+    (0, 2, 40, 40, 256, 256), (2584, 2, 37, 41, 64, 128), (2588, 1, 33, 30, 96, 256), (2588, 1, 34, 29, 64, 256),
     (2589, 3, 19, 19, 256, 256), (2568, 2, 21, 23, 64, 256), (2571, 2, 21, 23, 64, 128), (2574, 2, 20, 20, 64, 256),
     (643, 1, 13, 11, 32, 64), (2581, 2, 19, 19, 768, 256)])
 def test_f16x2_conv3x3_paths(nat, variant, n, h, w, C, Co):
@@ -215,3 +215,69 @@ def test_f16x2_regressor_head_out_fused(nat, n, H, W):
         assert rel_l2(g.cpu(), r.cpu()) < 1e-5
     sure = ref[5].abs() > 1e-4
     assert torch.equal(got[6][sure], ref[6][sure])
+
+
+# ------------------------------------------------------------------ plain binary16 operands (head_precision="tf32")
+def _tf32(t):
+    """TF32 rounding of fp32 values (10 explicit mantissa bits, round to nearest even), in float64."""
+    b = t.float().contiguous().view(torch.int32).to(torch.int64)
+    lsb = (b >> 13) & 1
+    r = ((b + 0xFFF + lsb) & ~0x1FFF) & 0xFFFFFFFF
+    r = torch.where(r >= 2 ** 31, r - 2 ** 32, r).to(torch.int32)
+    return r.view(torch.float32).double()
+
+
+@pytest.mark.parametrize("variant,n,h,w,C,Co", [
+    (0, 2, 40, 40, 256, 256), (2584, 2, 37, 41, 64, 128), (2588, 1, 33, 30, 96, 256), (2589, 3, 19, 19, 256, 256),
+    (2574, 2, 20, 20, 64, 256), (643, 1, 13, 11, 32, 64), (2581, 2, 19, 19, 768, 256)])
+def test_f16_conv3x3_is_the_tf32_product(nat, variant, n, h, w, C, Co):
+    """binary16 activations x binary16 weights (the TF32-equivalent heads): the float64 conv of the TF32-rounded
+    operands — the reference's own TF32 arithmetic on its GPUs — to fp32 accumulation order (<= 2e-5)."""
+    x = _rand(n, C, h, w, seed=20)
+    wt = _rand(Co, C, 3, 3, scale=(9 * C) ** -0.5, seed=21)
+    b = _rand(Co, seed=22)
+    ref = F.conv2d(_tf32(x).cpu(), _tf32(wt).cpu(), padding=1) + b.cpu().double()[None, :, None, None]
+    ref = ref.permute(0, 2, 3, 1).reshape(-1, Co)
+    M = n * h * w
+    a = torch.empty(M, C, dtype=torch.float16, device="cuda")
+    nat.convert_rows(x.permute(0, 2, 3, 1).reshape(M, C).contiguous(), C, M, C, a, C)
+    kb = 0 if variant == 643 else 32
+    wk = wt.permute(0, 2, 3, 1).reshape(Co, 9, C).half()
+    if kb:
+        wk = wk.reshape(Co, 9, C // kb, kb).permute(0, 2, 1, 3)
+    wp = wk.contiguous().reshape(Co, -1)
+    wp._mapa_split = True
+    if kb:
+        wp._mapa_kblock = kb
+    out = torch.empty(M, Co, device="cuda")
+    lp = torch.empty(M, Co, dtype=torch.float16, device="cuda")
+    nat.gemm_set_variant(variant)
+    try:
+        nat.gemm(a, wp, M, Co, 9 * C, bias=b, out_f32=out, out_lp=lp, conv=(C, h, w, h, w, 1))
+    finally:
+        nat.gemm_set_variant(0)
+    assert rel_l2(out.cpu(), ref) < 2e-5
+    assert torch.equal(lp, out.half())
+
+
+def test_f16_bilinear_and_convert_rows_range_faults(nat):
+    n, IH, IW, C, O = 2, 37, 41, 128, 64
+    src = _rand(n, IH, IW, C, seed=23)
+    out = torch.empty(n * O * O, C, dtype=torch.float16, device="cuda")
+    nat.bilinear_ac(src, n, IH, IW, C, O, O, O, O, out)
+    f32 = torch.empty(n * O * O, C, device="cuda")
+    nat.bilinear_ac(src, n, IH, IW, C, O, O, O, O, f32)
+    assert torch.equal(out, f32.half())
+    nat.check_faults()
+    src[1, 3, 4, 5] = 1.0e6  # every output pixel it feeds leaves the range
+    nat.bilinear_ac(src, n, IH, IW, C, O, O, O, O, out)
+    with pytest.raises(nat.NativeError, match="F16_RANGE"):
+        nat.check_faults()
+    x = _rand(50, 40, seed=24)
+    y = torch.empty(50, 40, dtype=torch.float16, device="cuda")
+    nat.convert_rows(x, 40, 50, 40, y, 40)
+    nat.check_faults()
+    x[3, 3] = -1.0e6
+    nat.convert_rows(x, 40, 50, 40, y, 40)
+    with pytest.raises(nat.NativeError, match="F16_RANGE"):
+        nat.check_faults()

@@ -50,7 +50,7 @@ def main():
         arms = [("branch", lambda: os.environ.__setitem__("MAPA_HEAD_BRANCH", "1")),
                 ("inline", lambda: os.environ.__setitem__("MAPA_HEAD_BRANCH", "0"))]
     elif what == "heads":  # TF32-equivalent heads (f16 x2) vs fp32-exact split bf16 heads (x3) vs bf16 fast mode
-        arms = [(h, (lambda h=h: os.environ.__setitem__("MAPA_AB_HEADS", h))) for h in ("tf32", "fp32", "bf16")]
+        arms = [(h, (lambda h=h: os.environ.__setitem__("MAPA_AB_HEADS", h))) for h in ("tf32", "tf32x2", "fp32", "bf16")]
     elif what == "lnfuse":  # residual linears with the next LayerNorm fused: all / N % 256 only / none
         arms = [("all", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 2)), ("n256", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 3)),
                 ("none", lambda: nat.gemm_tune(nat.TUNE_LN_FUSE, 0))]
