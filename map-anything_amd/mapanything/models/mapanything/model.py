@@ -293,7 +293,9 @@ class MapAnything:
 
     def heads_for(self, precision: str) -> str:
         """The head precision a run at `precision` uses: head_precision, or by default 'tf32' (the reference's GPU
-        recipe) under bf16 autocast and 'fp32' under the fp16 recipe."""
+        recipe) under bf16 autocast and 'fp32' under the fp16 recipe; exact fp32 throughout at precision 'fp32'."""
+        if precision == "fp32":
+            return "fp32"
         if self.head_precision is not None:
             return self.head_precision
         return "fp32" if precision == "fp16" else "tf32"
