@@ -208,24 +208,24 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
 // GELU for a bf16-rounded output (the transformer fc1 epilogues, epi_mode 1): x * Phi(x) with the normal tail
-// Q(t) = Phi(-t) = exp2(P(s)), s = min(|x|, 12) / 12, P a degree-9 fit of log2 Q on [0, 12] (tools/gelu_fit.py):
-// GELU = x >= 0 ? x - x Q : x Q.  Within 2.7e-5 relative of the exact-erf GELU (fp64) wherever |GELU| > 1e-30, and
-// within 1e-30 absolute below: far under a bf16 ulp (2^-8) — the rounded output differs from the exactly rounded one
-// in 0.06 % of the elements (the reference's own GELU, evaluated on the bf16-rounded linear output, differs in ~33 %).
-// 11 FMA-pipe instructions + one exp2 instead of erf_fast's ~24 (the fp32-output and fp16 epilogues keep gelu_erf).
+// Q(t) = Phi(-t) = exp2(P(t)), t = min(|x|, 12), P a degree-9 fit of log2 Q on [0, 12] in powers of t
+// (tools/gelu_fit.py): GELU = max(x, 0) - |x| Q (x >= 0: x - x Q; x < 0: x Q).  Within 3.2e-5 relative of the
+// exact-erf GELU (fp64) wherever |GELU| > 1e-30, and within 1e-30 absolute below: far under a bf16 ulp (2^-8) — the
+// rounded output differs from the exactly rounded one in 0.06 % of the elements (the reference's own GELU, evaluated on
+// the bf16-rounded linear output, differs in ~33 %).  fmin + 9 FMA + exp2 + max + FMA (|x| is a source modifier)
+// instead of erf_fast's ~24 (the fp32-output and fp16 epilogues keep gelu_erf).
 __device__ __forceinline__ float gelu_bf16out(float x) {
-  const float s = fminf(fabsf(x), 12.0f) * (1.0f / 12.0f);
-  float r = __builtin_fmaf(-12.983002662658691f, s, 74.06327056884766f);
-  r = __builtin_fmaf(r, s, -186.98208618164062f);
-  r = __builtin_fmaf(r, s, 276.977783203125f);
-  r = __builtin_fmaf(r, s, -270.02850341796875f);
-  r = __builtin_fmaf(r, s, 185.25404357910156f);
-  r = __builtin_fmaf(r, s, -94.32258605957031f);
-  r = __builtin_fmaf(r, s, -65.95738983154297f);
-  r = __builtin_fmaf(r, s, -13.816150665283203f);
-  r = __builtin_fmaf(r, s, -0.9999959468841553f);
-  const float xq = x * __builtin_amdgcn_exp2f(r);
-  return x >= 0.f ? x - xq : xq;
+  const float t = fminf(fabsf(x), 12.0f);
+  float r = __builtin_fmaf(-2.5161930317096903e-09f, t, 1.7224749626620905e-07f);
+  r = __builtin_fmaf(r, t, -5.2183268053340726e-06f);
+  r = __builtin_fmaf(r, t, 9.275929915020242e-05f);
+  r = __builtin_fmaf(r, t, -0.0010851839324459434f);
+  r = __builtin_fmaf(r, t, 0.008933933451771736f);
+  r = __builtin_fmaf(r, t, -0.05458483099937439f);
+  r = __builtin_fmaf(r, t, -0.45803743600845337f);
+  r = __builtin_fmaf(r, t, -1.1513458490371704f);
+  r = __builtin_fmaf(r, t, -0.9999959468841553f);
+  return __builtin_fmaf(-fabsf(x), __builtin_amdgcn_exp2f(r), fmaxf(x, 0.f));
 }
 
 template <typename T>
