@@ -722,13 +722,14 @@ class MapaEngine:
         when proj_embed is the identity.  pe_idx: (V_total,) int64 device tensor of view-PE table rows (row 0 for the
         reference view) when the variant encodes non-reference views too.  With `shard` (parallel.ShardPlan) this
         rank holds only its views (+ the scale-token replica) and the global layers all-gather K/V through `comm`.
-        scenes = B > 1 (no shard): VB = B x V images scene-major, rows [image][token] then the B scale tokens; frame
-        layers run over all images at once, global layers attend within each scene (its tokens + its scale token)."""
+        scenes = B > 1: VB = B x V images scene-major, rows [image][token] then the B scale tokens; frame layers run
+        over all images at once, global layers attend within each scene (its tokens + its scale token).  With a shard
+        too, V is this rank's view count of every scene (ShardPlan.scenes = B)."""
         w, info = self.w, self.info
         D, NH = info.dim, info.heads
         B = scenes
-        if B > 1 and (shard is not None or taps is not None or VB % B):
-            raise ValueError("batched scenes: no view sharding or taps, and VB a multiple of the scene count")
+        if B > 1 and (taps is not None or VB % B or (shard is not None and shard.scenes != B)):
+            raise ValueError("batched scenes: no taps, VB a multiple of the scene count, a shard plan of B scenes")
         V = VB // B
         L = VB * T + B
         if w.pe_proj is None:  # identity projection: the residual stream starts from the fp32 fused features
@@ -767,9 +768,12 @@ class MapaEngine:
                                          next_ln=nln)
                 elif shard is None:
                     normed = self._block_global_scenes(y, yn, qkv, ao, hbuf, L, p, B, V, T, g_scale, normed, nln)
-                else:
+                elif B == 1:
                     normed = self._block_global_sharded(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, g_scale,
                                                         normed, nln)
+                else:
+                    normed = self._block_global_sharded_scenes(y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm,
+                                                               V, T, g_scale, normed, nln)
             else:                   # frame attention inside each view; the scale token bypasses the block
                 normed = self._block(y, yn, qkv, ao, hbuf, VB * T, D, NH, p, attn_batch=VB, attn_seq=T,
                                      gamma=False, attn_scale=f_scale, normed=normed, next_ln=nln)
@@ -868,6 +872,34 @@ class MapaEngine:
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao_r, seq_kv=sum(sg[1] for sg in rest), kv_segments=rest,
                           lse=lse_r, kind="attention_global", **strides)
             nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, NH, C)
+        nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y, **self._lnf(p["n2w"], p["n2b"], yn))
+        nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
+        nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y,
+                 **(self._lnf(*next_ln, yn) if next_ln is not None else {}))
+        return L if next_ln is not None else 0
+
+    def _block_global_sharded_scenes(self, y, yn, q_loc, kv_full, ao, hbuf, L, p, shard, comm, V, T, scale=None,
+                                     normed=0, next_ln=None):
+        """Global SelfAttentionBlock of B batched scenes on a view shard (V = this rank's views per scene): Q for the
+        local rows, K/V of every rank in one slot all-gather, then per scene one attention of its local token rows
+        and one of its scale-token replica, both over the scene's keys on every rank (ShardPlan.scene_kv_segments).
+        The gather runs before the attention (the B = 1 layer overlaps it with the own-key partial)."""
+        C, NH = self.info.dim, self.info.heads
+        B = shard.scenes
+        self._norm1(y, yn, L, C, p, normed)
+        nat.gemm(yn, p["qkv"][:C], L, C, C, bias=p["qkv_b"][:C], out_lp=q_loc)
+        slot = kv_full[shard.rank * shard.max_rows:]
+        nat.gemm(yn, p["qkv"][C:], L, 2 * C, C, bias=p["qkv_b"][C:], out_lp=slot, ldo=2 * C)
+        if shard.world > 1 or force_collectives():
+            comm.allgather_slots(kv_full, shard.max_rows)
+        kw = dict(batch=1, heads=NH, q_bstride=0, q_rstride=C, k_bstride=0, k_rstride=2 * C, v_bstride=0,
+                  v_rstride=2 * C, o_bstride=0, o_rstride=C, scale=scale, kind="attention_global")
+        k, v = kv_full, kv_full[:, C:]
+        for b in range(B):
+            r0, tok = b * V * T, V * T * B + b
+            segs = shard.scene_kv_segments(b)
+            nat.attention(q_loc[r0:], k, v, ao[r0:], seq_q=V * T, seq_kv=shard.total_kv, kv_segments=segs, **kw)
+            nat.attention(q_loc[tok:], k, v, ao[tok:], seq_q=1, seq_kv=shard.total_kv, kv_segments=segs, **kw)
         nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y, **self._lnf(p["n2w"], p["n2b"], yn))
         nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
         nat.gemm(hbuf, p["fc2"], L, C, 4 * C, bias=p["fc2_b"], resid1=y, out_f32=y,
@@ -1107,13 +1139,14 @@ class MapaEngine:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
         B = scenes
-        if B > 1 and (shard is not None or (geo is not None and geo.scenes != B) or taps is not None or VB % B):
-            raise ValueError("batched scenes run unsharded, without taps, with VB a multiple of B and geometric "
-                             "inputs batched the same way (GeoInputs.scenes)")
+        if B > 1 and ((geo is not None and (geo.scenes != B or shard is not None)) or taps is not None or VB % B
+                      or (shard is not None and shard.scenes != B)):
+            raise ValueError("batched scenes run without taps, with VB a multiple of B, a shard plan of B scenes and "
+                             "geometric inputs batched the same way (GeoInputs.scenes; unsharded)")
         with torch.cuda.device(self.device):
             fused_lp, fused_f32, (hp, wp) = self.encode(imgs, taps, geo, scenes=B)
             T = hp * wp
-            if shard is not None and (shard.counts[shard.rank] != VB or shard.tokens_per_view != T):
+            if shard is not None and (shard.counts[shard.rank] * B != VB or shard.tokens_per_view != T):
                 raise AssertionError("shard plan does not match the local views")
             if self.info.nonref_pe and pe_idx is None:
                 raise ValueError("this info-sharing variant encodes every view's index: pass pe_idx")

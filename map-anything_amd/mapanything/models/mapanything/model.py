@@ -19,10 +19,10 @@ Differences that are by design:
     fp32-exact split-bf16 heads (the default of the fp16 recipe, amp_dtype="fp16", whose transformer rounds 8x finer
     than bf16: its tolerance is the reference's own fp16 spread measured with exact fp32 heads); `use_amp=False` (or precision="fp32") runs the exact-fp32 MFMA path;
     `head_precision="bf16"` is an opt-in fast mode with bf16 heads (not the reference's recipe),
-  * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687): image-only scenes run as ONE engine
-    call (encoder, frame layers and heads over all B x V images, global attention, scale token and scale head per
-    scene, as the reference's batched forward, model.py:687-721); scenes with geometric inputs or on a view-sharded
-    model run scene by scene.  The per-view outputs are concatenated on the batch dimension as the reference
+  * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687): the scenes run as ONE engine call
+    (encoder, geometric encoders, frame layers and heads over all B x V images, global attention, scale token and
+    scale head per scene, as the reference's batched forward, model.py:687-721); on a view-sharded model every rank
+    runs its views of all B scenes (image-only scenes; with geometric inputs a sharded model runs scene by scene).  The per-view outputs are concatenated on the batch dimension as the reference
     returns them.
 """
 
@@ -487,7 +487,7 @@ class MapAnything:
         dnt = views[0].get("data_norm_type", ["dinov2"])
         if (dnt[0] if isinstance(dnt, (list, tuple)) else dnt) != "dinov2":
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
-        local, plan = self._local_views(views)
+        local, plan = self._local_views(views, B)
         geo = self._geo_inputs(views, plan, self._metric_flags(views)) if B == 1 else \
             self._geo_inputs_scenes(views, B, [self._metric_flags(self._scene_views(views, b, B)) for b in range(B)])
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
@@ -498,6 +498,7 @@ class MapAnything:
 
     # entries a view may carry and still run in a batched-scene engine call: images and every geometric input
     # (raw as infer() takes them, and preprocessed as forward() takes them)
+    _IMAGE_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label"))
     _BATCHABLE_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label",
                                  "intrinsics", "ray_directions", "depth_z", "camera_poses", "ray_directions_cam",
                                  "depth_along_ray", "camera_pose_quats", "camera_pose_trans"))
@@ -505,8 +506,10 @@ class MapAnything:
     def _batchable(self, views) -> bool:
         """B > 1 scenes run as ONE engine call (encoder, geometric encoders, frame layers and heads over all B x V
         images; the global layers and the camera-translation normalisation per scene; the reference's batched
-        forward, model.py:687-721) unless the model is view-sharded; then scene by scene."""
-        return self._comm is None and all(set(v.keys()) <= self._BATCHABLE_KEYS for v in views)
+        forward, model.py:687-721).  A view-sharded model batches image-only scenes (every rank holds its views of
+        each scene, ShardPlan.scenes); with geometric inputs it runs scene by scene."""
+        keys = self._BATCHABLE_KEYS if self._comm is None else self._IMAGE_KEYS
+        return all(set(v.keys()) <= keys for v in views)
 
     @staticmethod
     def _scene_major(imgs, B: int):
@@ -727,7 +730,7 @@ class MapAnything:
                     v[k] = tuple(x.to(self._device, non_blocking=True) if isinstance(x, torch.Tensor) else x
                                  for x in v[k])
         processed = preprocess_input_views_for_inference(validated)
-        local, plan = self._local_views(processed)
+        local, plan = self._local_views(processed, B)
         use = dict(use_calibration=not ignore_calibration_inputs, use_depth=not ignore_depth_inputs,
                    use_pose=not ignore_pose_inputs, use_depth_scale=not ignore_depth_scale_inputs,
                    use_pose_scale=not ignore_pose_scale_inputs)
@@ -757,13 +760,13 @@ class MapAnything:
         per_view = 320 if self.heads_for(self.precision) == "bf16" else 420
         return max(1, int(0.95 * free / (per_view * 1024 * 1024)))
 
-    def _local_views(self, views):
+    def _local_views(self, views, scenes: int = 1):
         if self._comm is None:
             return views, None
         from ...parallel import ShardPlan
 
         H, W = views[0]["img"].shape[-2:]
-        plan = ShardPlan(len(views), self._comm.world, self._comm.rank, (H // 14) * (W // 14))
+        plan = ShardPlan(len(views), self._comm.world, self._comm.rank, (H // 14) * (W // 14), scenes)
         return [views[i] for i in plan.local_views], plan
 
     def _finish(self, batched, plan, V, with_post, scenes: int = 1):
@@ -772,15 +775,25 @@ class MapAnything:
         -> per view (B, ...) tensors."""
         if plan is None:
             return split_views(batched, V, with_post, scenes)
+        B = scenes
         if self._gather is not None and plan.world > 1:
             dst = 0 if self._gather == "rank0" else None
+            counts = [B * c for c in plan.counts]
+            # gathered rows are rank-major ([rank][scene][view]); scene-major order [scene][global view]
+            order = None if B == 1 else torch.tensor(
+                [sum(counts[:r]) + b * plan.counts[r] + i for b in range(B) for r in range(plan.world)
+                 for i in range(plan.counts[r])])
             full = {}
             for k, t in batched.items():
                 # metric_scaling_factor is already the same on every rank (rank 0's scale token, engine.aat)
-                full[k] = t if k == "metric_scaling_factor" else self._comm.gather_views(t, plan.counts, dst)
+                if k == "metric_scaling_factor":
+                    full[k] = t
+                    continue
+                g = self._comm.gather_views(t, counts, dst)
+                full[k] = g if g is None or order is None else g.index_select(0, order.to(g.device))
             if dst is None or plan.rank == dst:
-                return split_views(full, V, with_post)
-        local_out = split_views(batched, len(plan.local_views), with_post)
+                return split_views(full, V, with_post, scenes)
+        local_out = split_views(batched, len(plan.local_views), with_post, scenes)
         out = [None] * V
         for i, v in enumerate(plan.local_views):
             out[v] = local_out[i]

@@ -82,10 +82,14 @@ def init_distributed(backend: str = "nccl", device: Optional[torch.device] = Non
 
 @dataclass
 class ShardPlan:
+    """Views of one scene split over `world` ranks in contiguous runs (counts / starts).  scenes = B > 1: B batched
+    scenes share the split (rank r holds views starts[r] .. +counts[r] of every scene, scene-major: local image
+    b * counts[r] + i), and its K/V slot holds the B scenes' token rows then the B scale-token replicas."""
     num_views: int
     world: int
     rank: int
     tokens_per_view: int
+    scenes: int = 1
     counts: List[int] = field(init=False)
     starts: List[int] = field(init=False)
 
@@ -93,6 +97,8 @@ class ShardPlan:
         V, P = self.num_views, self.world
         if V < P:
             raise ValueError(f"{V} views cannot be sharded over {P} ranks (need at least one view per rank)")
+        if self.scenes < 1:
+            raise ValueError(f"scenes must be >= 1, got {self.scenes}")
         self.counts = [V // P + (1 if r < V % P else 0) for r in range(P)]
         self.starts = [sum(self.counts[:r]) for r in range(P)]
 
@@ -101,12 +107,12 @@ class ShardPlan:
         return range(self.starts[self.rank], self.starts[self.rank] + self.counts[self.rank])
 
     def local_rows(self, r: Optional[int] = None) -> int:
-        """AAT rows held by rank r: its views' tokens + the scale-token replica."""
+        """AAT rows held by rank r: its views' tokens + the scale-token replica (of every scene)."""
         r = self.rank if r is None else r
-        return self.counts[r] * self.tokens_per_view + 1
+        return self.scenes * (self.counts[r] * self.tokens_per_view + 1)
 
     def kv_valid_rows(self, r: int) -> int:
-        """K/V rows rank r contributes to the global set (scale token only from rank 0)."""
+        """K/V rows rank r contributes to the global set (scale token only from rank 0); one scene."""
         return self.counts[r] * self.tokens_per_view + (1 if r == 0 else 0)
 
     @property
@@ -115,10 +121,22 @@ class ShardPlan:
 
     @property
     def total_kv(self) -> int:
+        """Keys one global-attention query sees: its scene's tokens + its scale token."""
         return self.num_views * self.tokens_per_view + 1
 
     def kv_segments(self) -> List[Tuple[int, int]]:
+        if self.scenes != 1:
+            raise ValueError("kv_segments: one scene; use scene_kv_segments(b)")
         return [(r * self.max_rows, self.kv_valid_rows(r)) for r in range(self.world)]
+
+    def scene_kv_segments(self, b: int) -> List[Tuple[int, int]]:
+        """Scene b's keys in the gathered [world][max_rows] K/V: each rank's run of the scene's token rows, then the
+        scene's scale token from rank 0's slot (one segment with rank 0's tokens when they are adjacent: B = 1)."""
+        if self.scenes == 1:
+            return self.kv_segments()
+        T, B = self.tokens_per_view, self.scenes
+        segs = [(r * self.max_rows + b * self.counts[r] * T, self.counts[r] * T) for r in range(self.world)]
+        return segs + [(B * self.counts[0] * T + b, 1)]
 
 
 class DistComm:

@@ -51,25 +51,30 @@ def main():
     V = 3
     views = [{"img": torch.from_numpy(i), "data_norm_type": ["dinov2"]}
              for i in synthetic.synthetic_images(V, 224, 224, 41)]
+    # two scenes per view (batch_size_per_view 2): the batched-scene sharded global layers (one gather, per-scene
+    # segment tables over the gathered slots)
+    views2 = [{"img": torch.cat([v["img"], torch.from_numpy(i)], 0), "data_norm_type": ["dinov2"]}
+              for v, i in zip(views, synthetic.synthetic_images(V, 224, 224, 43))]
     res = {}
-    for mode in ("gather", "overlap"):
+    for mode in ("gather", "overlap", "scenes2"):
         os.environ["MAPA_FORCE_OVERLAP"] = "1" if mode == "overlap" else "0"
+        vw = views2 if mode == "scenes2" else views
         for prec in ("fp32", "bf16"):
             model = MapAnything(**released_config(), precision=prec).load_synthetic_weights().to("cuda")
             kw = dict(use_amp=prec == "bf16", apply_mask=False)
-            single = model.infer(views, **kw)  # unsharded (graph-replayed on one GPU)
+            single = model.infer(vw, **kw)  # unsharded (graph-replayed on one GPU)
             model.enable_view_sharding(dist.group.WORLD)
             direct = isinstance(model._comm, RcclComm)
             model.hip_graphs = False
             merges[0] = 0
-            eager = model.infer(views, **kw)
+            eager = model.infer(vw, **kw)
             eager_merges = merges[0]
             model.hip_graphs = True
             with warnings.catch_warnings(record=True) as caught:  # a failed capture warns and falls back to eager
                 warnings.simplefilter("always")
-                g1 = model.infer(views, **kw)  # captures the sharded forward (RCCL collectives inside the graph)
+                g1 = model.infer(vw, **kw)  # captures the sharded forward (RCCL collectives inside the graph)
             merges[0] = 0
-            g2 = model.infer(views, **kw)  # replays it (no Python-side launches)
+            g2 = model.infer(vw, **kw)  # replays it (no Python-side launches)
             replay_merges = merges[0]
             torch.cuda.synchronize()
             res[f"{mode}_{prec}"] = {

@@ -53,7 +53,8 @@ def test_one_rank_rccl_sharded_graph(tmp_path):
     MAPA_FORCE_OVERLAP=1, in the overlapped form every N > 1 global layer takes (side-stream all-gather forked and
     joined inside the capture, local / remote attention, LSE merge).  Graph-replayed == eager bitwise; sharded ==
     unsharded (fp32 within 2e-5: the sharded global layers project Q and K/V in two GEMMs, attend through the segment
-    table, and in the overlapped form merge two partials)."""
+    table, and in the overlapped form merge two partials).  Mode "scenes2": two batched scenes per view through the
+    batched-scene sharded layers (ShardPlan.scenes = 2), against the unsharded batched forward."""
     out = str(tmp_path / "nccl1.json")
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
@@ -62,7 +63,7 @@ def test_one_rank_rccl_sharded_graph(tmp_path):
     assert r.returncode == 0, _rank_errors(r)
     res = json.load(open(out))
     print("\n[one-rank RCCL sharded forward]", json.dumps(res, indent=1))
-    for mode in ("gather", "overlap"):
+    for mode in ("gather", "overlap", "scenes2"):
         for prec in ("fp32", "bf16"):
             d = res[f"{mode}_{prec}"]
             assert d["direct_rccl"] and d["sharded_graph_keys"] == 1, d

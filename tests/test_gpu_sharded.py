@@ -88,6 +88,43 @@ def test_sharded_equals_single(precision, tol, world, V):
     _scale_equal_across_ranks(outs)
 
 
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 8e-3)])
+@pytest.mark.parametrize("world,V", [(2, 3), (3, 4)])
+def test_sharded_batched_scenes_equal_single(precision, tol, world, V):
+    """B = 2 scenes per view on a view-sharded model: one engine call per rank over its views of both scenes
+    (ShardPlan.scenes, per-scene segment tables over the gathered K/V), equal to the unsharded batched forward; the
+    outputs gathered to every rank (gather_outputs="all") come back per view as (B, ...) in scene order."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ThreadComm
+    from tests_helpers import released_config
+
+    a, b = _views(V, 224, 224, seed=17), _views(V, 224, 224, seed=19)
+    views = [{"img": torch.cat([x["img"], y["img"]], 0), "data_norm_type": ["dinov2"]} for x, y in zip(a, b)]
+    ref_model = MapAnything(**released_config(), precision=precision).load_synthetic_weights().to("cuda")
+    ref = ref_model.forward(views)
+    assert ref[0]["pts3d"].shape[0] == 2
+    comm = ThreadComm(world)
+    model = MapAnything(**released_config(), precision=precision).to("cuda")
+    model._sd = ref_model._sd
+    model.enable_view_sharding(comm=comm, gather_outputs="all")
+    model.engine()
+    calls = []
+    real = model._run_engine
+    model._run_engine = lambda *a_, **k: calls.append(k.get("scenes")) or real(*a_, **k)
+    outs = _run_ranks(comm, world, lambda rank: model.forward(views))
+    assert calls == [2] * world  # one batched call per rank, not one per scene
+    worst = 0.0
+    for r in range(world):
+        assert all(o is not None for o in outs[r])
+        for v, o in enumerate(outs[r]):
+            for k in ("pts3d", "conf", "cam_quats", "cam_trans", "metric_scaling_factor"):
+                assert o[k].shape == ref[v][k].shape, (k, o[k].shape, ref[v][k].shape)
+                e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
+                worst = max(worst, e)
+                assert e < tol, (r, v, k, e)
+    print(f"\n[{precision} world {world} B=2] worst rel-L2 sharded vs single: {worst:.2e}")
+
+
 def test_sharded_gather_outputs_to_rank0():
     """enable_view_sharding(gather_outputs="rank0"): rank 0 returns every view (the reference's infer contract,
     model.py:2266-2282), equal to what the owning ranks computed; other ranks keep their own views."""

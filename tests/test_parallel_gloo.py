@@ -28,6 +28,33 @@ def test_shard_plan_layout():
         ShardPlan(3, 4, 0, 10)
 
 
+def test_shard_plan_batched_scenes():
+    """B scenes share the view split; each rank's slot holds [scene][view][token] rows then the B scale-token
+    replicas, and scene b's segments select exactly its tokens on every rank plus its scale token from rank 0."""
+    V, world, T, B = 7, 3, 5, 4
+    plans = [ShardPlan(V, world, r, T, scenes=B) for r in range(world)]
+    p = plans[0]
+    assert p.counts == [3, 2, 2] and p.max_rows == B * (3 * T + 1) and p.total_kv == V * T + 1
+    # global K/V laid out as the engine writes it: rank r's slot row of (scene b, local view i, token t)
+    full = -torch.ones(world * p.max_rows, dtype=torch.int64)
+    for r, pr in enumerate(plans):
+        c = pr.counts[r]
+        for b in range(B):
+            for i in range(c):
+                for t in range(T):
+                    full[r * p.max_rows + (b * c + i) * T + t] = b * 1000 + (pr.starts[r] + i) * T + t
+            full[r * p.max_rows + B * c * T + b] = b * 1000 + V * T  # scale-token replica
+    for b in range(B):
+        segs = p.scene_kv_segments(b)
+        assert len(segs) == world + 1 and sum(n for _, n in segs) == p.total_kv
+        got = torch.cat([full[st:st + n] for st, n in segs]).tolist()
+        assert sorted(got) == [b * 1000 + k for k in range(V * T + 1)]
+    # one scene: the B = 1 layout and segments
+    assert ShardPlan(V, world, 0, T, scenes=1).scene_kv_segments(0) == ShardPlan(V, world, 0, T).kv_segments()
+    with pytest.raises(ValueError):
+        p.kv_segments()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -148,6 +175,17 @@ def _gather_worker(rank, world, port, q):
             got = [None if o is None else float(o["pts3d"].flatten()[0]) for o in out]
             masks = [None if o is None else bool(o["non_ambiguous_mask"].flatten()[0]) for o in out]
             res[mode] = (got, masks)
+        # B = 2 batched scenes: local rows scene-major (scene b, local view i), value 100 b + global view
+        B = 2
+        plan2 = ShardPlan(V, world, rank, 4, scenes=B)
+        lv = list(plan2.local_views)
+        vals = [100 * b + v for b in range(B) for v in lv]
+        local2 = {"pts3d": torch.tensor(vals, dtype=torch.float32).view(-1, 1, 1, 1).expand(-1, 2, 2, 3).contiguous(),
+                  "metric_scaling_factor": torch.ones(B, 1)}
+        for mode in ("rank0", "all", None):
+            m._gather = mode
+            out = m._finish(dict(local2), plan2, V, with_post=False, scenes=B)
+            res[("b2", mode)] = [None if o is None else o["pts3d"][:, 0, 0, 0].tolist() for o in out]
         q.put((rank, ok_bcast, res))
     finally:
         dist.destroy_process_group()
@@ -175,6 +213,11 @@ def test_scale_token_broadcast_and_output_gather_gloo(world):
         assert r["all"] == (every, every_mask)
         assert r["rank0"][0] == (every if rank == 0 else own)
         assert r[None][0] == own
+        every2 = [[float(v), float(100 + v)] for v in range(V)]  # per view: its (B,) values, scene order
+        own2 = [e if v in plan.local_views else None for v, e in enumerate(every2)]
+        assert r[("b2", "all")] == every2
+        assert r[("b2", "rank0")] == (every2 if rank == 0 else own2)
+        assert r[("b2", None)] == own2
 
 
 class _FakeRccl:
