@@ -66,8 +66,9 @@ class GeoInputs:
     cam_mask: List[bool] = field(default_factory=list)       # (V,)
     pose_metric: List[bool] = field(default_factory=list)    # (V,) is_metric_scale & use_pose_scale
     local_start: int = 0
-    # B > 1 batched scenes (no shard): every list / tensor above holds the B scenes' views scene-major (image b*V + v);
-    # the camera translations are normalised per scene (pose inputs over each scene's V views, model.py:792-896)
+    # B > 1 batched scenes: every list / tensor above holds the B scenes' views scene-major (dense inputs: local image
+    # b*n_local + i; camera arrays: view b*V + v); the camera translations are normalised per scene (pose inputs over
+    # each scene's V views, model.py:792-896)
     scenes: int = 1
 
     def empty(self) -> bool:
@@ -606,15 +607,22 @@ class MapaEngine:
             for b in range(geo.scenes):  # camera inputs in each scene's view-0 frame, translations normalised per scene
                 sl = slice(b * V, (b + 1) * V)
                 nat.pose_inputs(cq[sl], ct[sl], mask[sl], V, q[sl], t[sl], lnf[sl])
-            s0 = geo.local_start
-            cm = [1.0 if geo.cam_mask[s0 + v] else 0.0 for v in range(VB)]
-            pm = [cm[v] if geo.pose_metric[s0 + v] else 0.0 for v in range(VB)]
-            vecs.append(self._global_rep(q[s0:s0 + VB], VB, 4, g["cam_rot_encoder"]))
+            # this rank's images among all views: scene b's local view i (image b*c + i) is view b*V + s0 + i
+            s0, c = geo.local_start, VB // geo.scenes
+            loc = [b * V + s0 + i for b in range(geo.scenes) for i in range(c)]
+            if loc == list(range(s0, s0 + VB)):  # one contiguous run (one scene, or B scenes unsharded)
+                pick = lambda a: a[s0:s0 + VB]  # noqa: E731
+            else:  # B scenes on a view shard
+                li = self._const(loc, torch.long)
+                pick = lambda a: a.index_select(0, li)  # noqa: E731
+            cm = [1.0 if geo.cam_mask[j] else 0.0 for j in loc]
+            pm = [cm[v] if geo.pose_metric[j] else 0.0 for v, j in enumerate(loc)]
+            vecs.append(self._global_rep(pick(q), VB, 4, g["cam_rot_encoder"]))
             scales.append(cm)
-            vecs.append(self._global_rep(t[s0:s0 + VB], VB, 3, g["cam_trans_encoder"]))
+            vecs.append(self._global_rep(pick(t), VB, 3, g["cam_trans_encoder"]))
             scales.append(cm)
             if any(pm):
-                vecs.append(self._global_rep(lnf[s0:s0 + VB].view(VB, 1), VB, 1, g["cam_trans_scale_encoder"]))
+                vecs.append(self._global_rep(pick(lnf).view(VB, 1), VB, 1, g["cam_trans_scale_encoder"]))
                 scales.append(pm)
         if vecs:
             vb = torch.stack(vecs, 0).contiguous()
@@ -1139,10 +1147,10 @@ class MapaEngine:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
         B = scenes
-        if B > 1 and ((geo is not None and (geo.scenes != B or shard is not None)) or taps is not None or VB % B
+        if B > 1 and ((geo is not None and geo.scenes != B) or taps is not None or VB % B
                       or (shard is not None and shard.scenes != B)):
             raise ValueError("batched scenes run without taps, with VB a multiple of B, a shard plan of B scenes and "
-                             "geometric inputs batched the same way (GeoInputs.scenes; unsharded)")
+                             "geometric inputs batched the same way (GeoInputs.scenes)")
         with torch.cuda.device(self.device):
             fused_lp, fused_f32, (hp, wp) = self.encode(imgs, taps, geo, scenes=B)
             T = hp * wp

@@ -22,7 +22,7 @@ Differences that are by design:
   * B > 1 scenes per view (the reference's batch_size_per_view, model.py:687): the scenes run as ONE engine call
     (encoder, geometric encoders, frame layers and heads over all B x V images, global attention, scale token and
     scale head per scene, as the reference's batched forward, model.py:687-721); on a view-sharded model every rank
-    runs its views of all B scenes (image-only scenes; with geometric inputs a sharded model runs scene by scene).  The per-view outputs are concatenated on the batch dimension as the reference
+    runs its views of all B scenes.  The per-view outputs are concatenated on the batch dimension as the reference
     returns them.
 """
 
@@ -441,29 +441,33 @@ class MapAnything:
                                      else torch.zeros(1, 3, device=dev, dtype=f32) for v in range(V)], 0)
         return None if g.empty() else g
 
-    def _geo_inputs_scenes(self, views, B, metrics, **use):
-        """GeoInputs of B batched scenes (unsharded): each scene's inputs as _geo_inputs builds them (its own metric
-        flags, its own camera normalisation frame), concatenated scene-major (image b*V + v) with GeoInputs.scenes =
-        B; scenes without an input kind get the reference's zero / identity fill and a cleared mask.  metrics[b]:
-        scene b's per-view is_metric_scale flags (read on the host before the inputs moved to the device)."""
+    def _geo_inputs_scenes(self, views, B, metrics, plan=None, **use):
+        """GeoInputs of B batched scenes: each scene's inputs as _geo_inputs builds them (its own metric flags, its
+        own camera normalisation frame), concatenated scene-major with GeoInputs.scenes = B — dense inputs over this
+        rank's images (image b*n + i, n = local views per scene; n = V unsharded), camera arrays over every view
+        (b*V + v); scenes without an input kind get the reference's zero / identity fill and a cleared mask.
+        metrics[b]: scene b's per-view is_metric_scale flags (read on the host before the inputs moved to the
+        device)."""
         from .engine import GeoInputs
 
-        per = [self._geo_inputs(self._scene_views(views, b, B), None, metrics[b], **use) for b in range(B)]
+        per = [self._geo_inputs(self._scene_views(views, b, B), plan, metrics[b], **use) for b in range(B)]
         if all(g is None for g in per):
             return None
         V = len(views)
+        n = V if plan is None else len(plan.local_views)
+        s0 = 0 if plan is None else plan.local_views[0]
         H, W = views[0]["img"].shape[-2:]
         dev, f32 = self._device, torch.float32
-        g = GeoInputs(local_start=0, scenes=B)
+        g = GeoInputs(local_start=s0, scenes=B)
         if any(p is not None and p.ray_views for p in per):
-            g.rays = torch.cat([p.rays if p is not None and p.ray_views else torch.zeros(V, H, W, 3, device=dev, dtype=f32)
+            g.rays = torch.cat([p.rays if p is not None and p.ray_views else torch.zeros(n, H, W, 3, device=dev, dtype=f32)
                                 for p in per], 0).contiguous()
-            g.ray_views = [b * V + i for b, p in enumerate(per) if p is not None for i in p.ray_views]
+            g.ray_views = [b * n + i for b, p in enumerate(per) if p is not None for i in p.ray_views]
         if any(p is not None and p.depth_views for p in per):
-            g.depth = torch.cat([p.depth if p is not None and p.depth_views else torch.zeros(V, H, W, device=dev, dtype=f32)
+            g.depth = torch.cat([p.depth if p is not None and p.depth_views else torch.zeros(n, H, W, device=dev, dtype=f32)
                                  for p in per], 0).contiguous()
-            g.depth_views = [b * V + i for b, p in enumerate(per) if p is not None for i in p.depth_views]
-            g.depth_metric = [bool(p is not None and p.depth_views and p.depth_metric[i]) for p in per for i in range(V)]
+            g.depth_views = [b * n + i for b, p in enumerate(per) if p is not None for i in p.depth_views]
+            g.depth_metric = [bool(p is not None and p.depth_views and p.depth_metric[i]) for p in per for i in range(n)]
         if any(p is not None and any(p.cam_mask) for p in per):
             ident_q = torch.tensor([[0.0, 0.0, 0.0, 1.0]], device=dev, dtype=f32).expand(V, 4)
             has = [p is not None and any(p.cam_mask) for p in per]
@@ -489,7 +493,8 @@ class MapAnything:
             raise AssertionError(f"Input data norm type {dnt} does not match encoder norm type dinov2")
         local, plan = self._local_views(views, B)
         geo = self._geo_inputs(views, plan, self._metric_flags(views)) if B == 1 else \
-            self._geo_inputs_scenes(views, B, [self._metric_flags(self._scene_views(views, b, B)) for b in range(B)])
+            self._geo_inputs_scenes(views, B, [self._metric_flags(self._scene_views(views, b, B)) for b in range(B)],
+                                    plan)
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference),
                                scenes=B)
@@ -498,7 +503,6 @@ class MapAnything:
 
     # entries a view may carry and still run in a batched-scene engine call: images and every geometric input
     # (raw as infer() takes them, and preprocessed as forward() takes them)
-    _IMAGE_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label"))
     _BATCHABLE_KEYS = frozenset(("img", "data_norm_type", "instance", "idx", "true_shape", "is_metric_scale", "label",
                                  "intrinsics", "ray_directions", "depth_z", "camera_poses", "ray_directions_cam",
                                  "depth_along_ray", "camera_pose_quats", "camera_pose_trans"))
@@ -506,10 +510,9 @@ class MapAnything:
     def _batchable(self, views) -> bool:
         """B > 1 scenes run as ONE engine call (encoder, geometric encoders, frame layers and heads over all B x V
         images; the global layers and the camera-translation normalisation per scene; the reference's batched
-        forward, model.py:687-721).  A view-sharded model batches image-only scenes (every rank holds its views of
-        each scene, ShardPlan.scenes); with geometric inputs it runs scene by scene."""
-        keys = self._BATCHABLE_KEYS if self._comm is None else self._IMAGE_KEYS
-        return all(set(v.keys()) <= keys for v in views)
+        forward, model.py:687-721).  On a view-sharded model every rank holds its views of each scene
+        (ShardPlan.scenes)."""
+        return all(set(v.keys()) <= self._BATCHABLE_KEYS for v in views)
 
     @staticmethod
     def _scene_major(imgs, B: int):
@@ -737,7 +740,7 @@ class MapAnything:
         if B == 1:
             geo = self._geo_inputs(processed, plan, metric, **use)
         else:
-            geo = self._geo_inputs_scenes(processed, B, metric, **use)
+            geo = self._geo_inputs_scenes(processed, B, metric, plan, **use)
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         eng = self.engine(precision)
         raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)

@@ -258,6 +258,39 @@ def test_sharded_geometric_inputs_equal_single(precision, tol):
                 assert e < tol, (r, v, k, e)
 
 
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5)])
+def test_sharded_batched_geometric_scenes_equal_single(precision, tol):
+    """B = 2 scenes x 3 views with mixed geometric inputs (b2_224) on a 2-rank shard, one engine call per rank: the
+    dense encoders over each rank's images of both scenes, the camera inputs normalised per scene over ALL its views
+    and picked per local image — against the unsharded batched infer, outputs gathered to every rank."""
+    from mapanything.models import MapAnything
+    from mapanything.parallel import ThreadComm
+    from tests_helpers import CASES, make_views, released_config
+
+    case = CASES["b2_224"]
+    kw = dict(use_amp=False, apply_mask=False)
+    ref_model = MapAnything(**released_config(), precision=precision).load_synthetic_weights().to("cuda")
+    ref = ref_model.infer(make_views(case), **kw)
+    assert ref[0]["pts3d"].shape[0] == 2
+    world = 2
+    comm = ThreadComm(world)
+    model = MapAnything(**released_config(), precision=precision).to("cuda")
+    model._sd = ref_model._sd
+    model.enable_view_sharding(comm=comm, gather_outputs="all")
+    model.engine("fp32")
+    calls = []
+    real = model._run_engine
+    model._run_engine = lambda *a_, **k: calls.append((k.get("scenes"), a_[3] is not None)) or real(*a_, **k)
+    per_rank_views = [make_views(case) for _ in range(world)]
+    outs = _run_ranks(comm, world, lambda rank: model.infer(per_rank_views[rank], **kw))
+    assert calls == [(2, True)] * world  # one batched geometric call per rank
+    for r in range(world):
+        for v, o in enumerate(outs[r]):
+            for k in ("pts3d", "conf", "depth_along_ray", "cam_quats", "cam_trans", "metric_scaling_factor"):
+                e = rel_l2(o[k].float().cpu(), ref[v][k].float().cpu())
+                assert e < tol, (r, v, k, e)
+
+
 @pytest.mark.parametrize("variant", ["gat_224", "aatpe_224", "aat48_224"])
 def test_sharded_variants_equal_single(variant):
     """Info-sharing variants on the sharded path: GAT (every block global, view PE on every view: each rank adds
