@@ -573,10 +573,12 @@ int conv_halo_flat_split(const GemmArgs& a, int slots, int force) {
   const int64_t tiles = flat_blocks(a) * (a.N / 128);
   const int nslice = a.K / 288;
   if (force > 0) return force < nslice ? force : nslice;
-  // fill the resident slots (2 per CU) once, with at least two slices (18 K steps) per part and at most 8 parts:
-  // the last arriver sums the parts' 128-KiB slabs alone (flat_sweep.py, 8 views: l4rn@19 83.6 us on stream-K,
-  // 93.4 with 19 parts, 55.8 with 8; rn4@19 51.9 / 54.6 with 12 / 34.7 with 8; rn3@37 93.5 -> 59.2 with 5)
-  int64_t s = slots / (tiles > 0 ? tiles : 1);
+  // one block per CU (slots = 2 per CU), with at least two slices (18 K steps) per part and at most 8 parts: the
+  // last arriver sums the parts' 128-KiB slabs alone, and a second, partly filled round of blocks costs more than
+  // the extra parts win (flat_sweep.py, 8 views, round 5: the 37^2 convs' 92 tiles take 2 parts — binary16 rn3@37
+  // 41.2 -> 32.3 us, l3rn@37 48.9 -> 39.2 against 4 / 5 parts; split bf16 rn3@37 59.5 -> 57.3, l3rn@37 74.0 -> 78.6;
+  // the 19^2 convs' 26 tiles keep 8 / 4 parts: l4rn@19 83.6 us on stream-K, 55.8 with 8 parts)
+  int64_t s = (slots / 2) / (tiles > 0 ? tiles : 1);
   int cap = nslice / 2 > 1 ? nslice / 2 : 1;
   if (cap > 8) cap = 8;
   if (s > cap) s = cap;

@@ -1,6 +1,7 @@
 """Flat-raster split-K halo conv (variant 2589) against the stream-K implicit GEMM (2580/2581) on the DPT's small-map
 head convs at 8 views, with a sweep of the K part count (mapa_gemm_tune(MAPA_TUNE_HALO_SPLIT)).  Interleaved in one
-process (tools/kbench.py's rule).  Usage: python tools/flat_sweep.py [reps]"""
+process (tools/kbench.py's rule).  FS_F16=1: the TF32-equivalent heads' plain binary16 operands (logical channel
+widths).  Usage: python tools/flat_sweep.py [reps]"""
 import os
 import sys
 
@@ -13,6 +14,11 @@ V = 8
 # name, H, W, C (per-pixel operand width: 3x the logical channels of the split-precision convs), Co
 CONVS = [("l3rn@37", 37, 37, 1152, 256), ("l4rn@19", 19, 19, 2304, 256), ("rn4@19", 19, 19, 768, 256),
          ("rn3@37", 37, 37, 768, 256)]
+DT = torch.bfloat16
+if os.environ.get("FS_F16"):
+    CONVS = [("l3rn@37", 37, 37, 384, 256), ("l4rn@19", 19, 19, 768, 256), ("rn4@19", 19, 19, 256, 256),
+             ("rn3@37", 37, 37, 256, 256)]
+    DT = torch.float16
 SPLITS = [int(s) for s in os.environ.get("FS_SPLITS", "0,2,3,4,6,8").split(",")]
 ROUNDS = 3
 
@@ -34,12 +40,12 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
     nat.lib()
     for name, H, W, C, Co in CONVS:
-        x = (torch.randn(V, H, W, C, device="cuda") * 0.5).to(torch.bfloat16)
-        w = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(torch.bfloat16)
+        x = (torch.randn(V, H, W, C, device="cuda") * 0.5).to(DT)
+        w = (torch.randn(Co, 9 * C, device="cuda") * (9 * C) ** -0.5).to(DT)
         w = w.view(Co, 9, C // 32, 32).permute(0, 2, 1, 3).contiguous().reshape(Co, -1)
         w._mapa_kblock = 32
         b = torch.randn(Co, device="cuda")
-        o = torch.empty(V * H * W, Co, device="cuda", dtype=torch.bfloat16)
+        o = torch.empty(V * H * W, Co, device="cuda", dtype=DT)
         M = V * H * W
         sk = 2581 if Co >= 512 and M >= 2048 else 2580
 
