@@ -73,7 +73,7 @@ def timeit(fn, reps):
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-    dt = torch.bfloat16
+    dt = torch.float16 if os.environ.get("KB_F16") else torch.bfloat16  # KB_F16=1: binary16 operands (the TF32 heads)
     if what in ("gemm", "all"):
         for name, M, N, K in GEMMS:
             A = (torch.randn(M, K, device="cuda") * 0.5).to(dt)
