@@ -10,13 +10,21 @@
   python bench.py --gpus 2 --dry-run     # launcher rehearsal on CPU: gloo ranks, no GPU, a placeholder step
 
 One step = one full `MapAnything.infer(views)` (validation, forward, post-processing with edge masks) over
-synthetic images with inputs already resident in HBM, in the reference's own precision recipe (bf16 encoder and
-transformer, fp32-exact geometric encoders and heads).  The same JSON line carries, as nested objects, the opt-in
-bf16-heads fast mode (N=1; not the reference's recipe, never the headline) and the configs[2] strong-scaling job
-(a fixed 100 views over the N ranks: `strong_scaling`, measured at every N so the curve can be read off the
-driver's per-N lines).  On one GPU the engine's launches are replayed from a captured
-HIP graph (MapAnything.hip_graphs); per-kernel timing for the roofline comes from a second, eager pass of the same
-steps with an event pair around every native call.  Prints ONE JSON line on rank 0.
+synthetic images with inputs already resident in HBM, in the reference's own GPU precision recipe: bf16 autocast
+encoder and transformer; geometric encoders and heads with autocast disabled (model.py:1377 / 1774), i.e. at the
+TF32 precision the reference's fp32 convs / linears run at on its GPUs (cudnn's default, matmul.allow_tf32 at
+model.py:93) — here binary16 operands at TF32's 11 significant bits with fp32 accumulation (--head-precision tf32, the
+default), with the binary16 range closed by power-of-two weight scales and an automatic fp32-exact re-run of a call
+whose head activations leave binary16's range (`range_fallbacks` counts them; expect 0).  The same JSON line carries,
+as nested objects: the fp32-exact heads (`fp32_exact_heads`, split-precision bf16 x3), the opt-in bf16-heads fast
+mode (N=1; not the reference's recipe, never the headline), the forward-only time (`forward_only`: the raw
+MapAnything.forward without input validation / pre- and post-processing), and the configs[2] strong-scaling job (a
+fixed 100 views over the N ranks: `strong_scaling`, measured at every N so the curve can be read off the driver's
+per-N lines).  At N > 1 (or --shard-rehearsal on one GPU) `kv_overlap` reports each global layer's K/V all-gather
+time on the communicator's stream beside the local- and remote-key attention and the join's exposed wait.  On one GPU
+the engine's launches are replayed from a captured HIP graph (MapAnything.hip_graphs); per-kernel timing for the
+roofline comes from a second, eager pass of the same steps with an event pair around every native call.  Prints ONE
+JSON line on rank 0.
 """
 
 import argparse
@@ -57,7 +65,16 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp16", "fp32"],
                     help="autocast operand dtype of the encoder / transformer (infer(amp_dtype=...)); fp32 = use_amp off")
     ap.add_argument("--head-precision", default="tf32", choices=["tf32", "tf32x2", "fp32", "bf16"],
-                    help="fp32 = the reference's recipe (autocast disabled for the heads); bf16 = fast mode")
+                    help="tf32 (default) = the reference's GPU recipe for its autocast-disabled heads (TF32-equivalent "
+                         "binary16 operands, fp32 accumulation); tf32x2 = 22-bit activations; fp32 = fp32-exact "
+                         "split-bf16 heads; bf16 = fast mode (not the reference's recipe)")
+    ap.add_argument("--shard-rehearsal", action="store_true",
+                    help="N=1 only: run the view-sharded path on a one-rank RCCL group with MAPA_FORCE_OVERLAP=1 (the "
+                         "N > 1 global layers' overlapped all-gather branch) and report kv_overlap")
+    ap.add_argument("--no-forward-only", action="store_true", help="skip the forward-only timing")
+    ap.add_argument("--from-files-src", type=int, default=1024,
+                    help="N=1: also time infer from JPEG files (this many pixels a side, resized to 518 on the host "
+                         "by the reference's pipeline, prefetched one scene ahead); 0 = skip")
     ap.add_argument("--no-fast-mode", action="store_true", help="skip the bf16-heads fast-mode measurement")
     ap.add_argument("--strong-views", type=int, default=100,
                     help="also time a fixed job of this many views over the N ranks (configs[2]); 0 = skip")
@@ -100,11 +117,20 @@ def main():
         _native.load_library(args.lib)
 
     observed_world = 1
-    if world > 1:
+    sharded = world > 1 or args.shard_rehearsal
+    if sharded:
         import torch.distributed as dist
 
         from mapanything.parallel import init_distributed
 
+        if args.shard_rehearsal:
+            if world != 1:
+                raise SystemExit("bench.py: --shard-rehearsal is a one-GPU rehearsal of the N > 1 path")
+            os.environ["MAPA_FORCE_OVERLAP"] = "1"  # parallel.force_overlap: the overlapped multi-rank branch
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local_rank)
         _, observed_world = init_distributed("nccl", torch.device("cuda", local_rank))
         assert observed_world == args.gpus, (observed_world, args.gpus)
@@ -121,7 +147,7 @@ def main():
     H = W = args.res
     model = MapAnything(**released_config(), precision=args.precision,
                         head_precision=args.head_precision).load_synthetic_weights().to(dev).eval()
-    if world > 1:
+    if sharded:
         model.enable_view_sharding(dist.group.WORLD)
     imgs = synthetic.synthetic_images(V_total, H, W, seed=2)
     views = [{"img": torch.from_numpy(i).to(dev), "data_norm_type": ["dinov2"]} for i in imgs]
@@ -141,7 +167,7 @@ def main():
         step()
     torch.cuda.synchronize()
     eng = model.engine()
-    shard_check = shard_graph_self_check(model, step, dist, dev) if world > 1 else None
+    shard_check = shard_graph_self_check(model, step, dist, dev) if sharded else None
 
     def timed(k):
         return timed_fn(step, k)
@@ -175,6 +201,22 @@ def main():
         ktimes = eng.collect_kernel_timing()
     ms = dt / args.steps * 1e3
     value = V_total * args.steps / dt
+
+    fwd = None
+    if not args.no_forward_only:
+        # the raw forward (model.py:1657-2152) on the same views, preprocessed once outside the timed region: the
+        # infer() time minus input validation / preprocessing and the post-processing masks
+        from mapanything.utils.inference import preprocess_input_views_for_inference, validate_input_views_for_inference
+
+        pre = preprocess_input_views_for_inference(validate_input_views_for_inference(
+            [dict(v) for v in views]))
+        fprec = args.precision
+        model.forward(pre, precision=fprec)
+        fdt = timed_fn(lambda: model.forward(pre, precision=fprec), args.steps)
+        fwd = {"ms_per_step": fdt / args.steps * 1e3, "value": V_total * args.steps / fdt, "unit": "views/s",
+               "steps": args.steps, "what": "MapAnything.forward on preprocessed views (no validation / "
+                                            "preprocessing / post-processing masks), same HIP-graph path"}
+        del pre
 
     def other_heads(hp):
         fm = MapAnything(**released_config(), precision=args.precision, head_precision=hp).to(dev).eval()
@@ -219,6 +261,10 @@ def main():
                    "vs_single_scene": (B * V_total * args.steps / bdt) / value}
         del b_views
         torch.cuda.empty_cache()
+
+    files = None
+    if world == 1 and args.from_files_src and not args.geometric and not args.total_views and H == 518:
+        files = bench_from_files(model, amp, V_total, args, timed_fn)
 
     cfg4 = None
     if world == 1 and args.cfg4_views and not args.geometric and not args.total_views:
@@ -287,6 +333,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.geometric:
             cpu = cpu_baseline(model, imgs, H, W)
+        kvo = kv_overlap(ktimes) if ktimes else None
         L = V_total * T + 1
         gf_view = (1870.9e9 + 36864.0 * L * L / V_total + (165.6e9 if args.geometric else 0.0)) / 1e12 \
             if H == 518 else None
@@ -313,7 +360,8 @@ def main():
                             "image-only MapAnything.infer (configs[1] at N=1)")),
                        "views": V_total, "views_per_gpu": V_total / world, "height": H, "width": W,
                        "batch_per_view": 1,
-                       "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else "single"},
+                       "parallelism": f"view-sharded x{world} + RCCL K/V all-gather" if world > 1 else
+                       ("one-rank RCCL shard rehearsal (MAPA_FORCE_OVERLAP=1)" if sharded else "single")},
             # algorithmic TFLOP/s of the whole job (global attention grows as (V*1369)^2: per-view work rises with
             # the total view count, so weak-scaling views/s alone understates the per-GPU throughput at N > 1)
             "tflops_effective": (gf_view * value) if gf_view else None,
@@ -327,15 +375,77 @@ def main():
             "fast_mode_bf16_heads": fast,
             "fp32_exact_heads": exact,
             "strong_scaling": strong,
+            "forward_only": fwd,
+            "from_files": files,
+            "kv_overlap": kvo,
+            "range_fallbacks": MapAnything.range_fallbacks,
             # one GPU, or a view shard over RCCL (kernels and collectives captured together; MAPA_SHARD_GRAPHS=0 or a
             # failed capture on any rank: eager, with the reason)
-            "hip_graphs": bool(model.hip_graphs and (world == 1 or model._shard_graphs)),
-            "hip_graph_fallback": None if world == 1 else model.shard_graph_fallback,
+            "hip_graphs": bool(model.hip_graphs and (not sharded or model._shard_graphs)),
+            "hip_graph_fallback": None if not sharded else model.shard_graph_fallback,
             "shard_graph_check": shard_check,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bench_from_files(model, amp, V, args, timed_fn):
+    """End to end from image files: V square JPEGs of --from-files-src pixels a side per scene, decoded, Lanczos-
+    resized to 518x518 and normalised by the input pipeline (utils/image.py, the reference's load_images), then
+    infer().  Sequential (load_images then infer, per scene) and prefetched (iter_load_images: the next scene's host
+    decode / resize runs on host threads under this scene's GPU work).  Not the headline: the host's decode rate."""
+    import tempfile
+
+    import PIL.Image
+
+    from mapanything.utils.image import iter_load_images, load_images
+    from tests_helpers import synthetic_image
+
+    S = args.from_files_src
+    tmp = tempfile.mkdtemp(prefix="mapa_bench_")
+    paths = []
+    for i in range(V):  # smooth seeded photographs-like images (gradients, discs, mild noise)
+        p = os.path.join(tmp, f"view_{i:03d}.jpg")
+        PIL.Image.fromarray(synthetic_image(S, S, 100 + i)).save(p, quality=95)
+        paths.append(p)
+    steps = max(2, args.steps // 2)
+    model.infer(load_images(paths), **amp)  # warm-up
+    seq = timed_fn(lambda: model.infer(load_images(paths), **amp), steps)
+    t_load = timed_fn(lambda: load_images(paths), steps)
+
+    def prefetched():
+        for views in iter_load_images([paths] * steps, prefetch=1):
+            model.infer(views, **amp)
+    pre = timed_fn(prefetched, 1)
+    for p in paths:
+        os.remove(p)
+    os.rmdir(tmp)
+    threads = min(16, os.cpu_count() or 1)
+    return {"views": V, "src": f"{S}x{S} JPEG (q95) -> 518x518 Lanczos (fixed_mapping)", "steps": steps,
+            "sequential": {"value": V * steps / seq, "unit": "views/s", "ms_per_step": seq / steps * 1e3},
+            "prefetched": {"value": V * steps / pre, "unit": "views/s", "ms_per_step": pre / steps * 1e3},
+            "host_load_only": {"value": V * steps / t_load, "unit": "views/s", "ms_per_step": t_load / steps * 1e3},
+            "host_threads": threads,
+            "note": "host decode / resize with PIL (bit-identical to the reference); the in-HBM headline excludes it"}
+
+
+def kv_overlap(ktimes):
+    """The overlapped global layer of the view-sharded path (engine._block_global_sharded), per layer, from the eager
+    timing pass: the K/V all-gather on the communicator's stream, the local- and remote-key attention on the compute
+    stream, and the join's exposed wait (local attention done -> gathered slots visible).  overlap_frac = 1 - wait /
+    all-gather: the share of the all-gather hidden under the local-key attention.  None without a sharded run."""
+    g, la = ktimes.get("kv_allgather"), ktimes.get("kv_local_attention")
+    ra, wt = ktimes.get("kv_remote_attention"), ktimes.get("kv_gather_wait")
+    if not (g and la and ra and wt):
+        return None
+    ag = g["ms"] / g["count"]
+    wait = wt["ms"] / wt["count"]
+    return {"allgather_ms_per_layer": ag, "local_attn_ms": la["ms"] / la["count"],
+            "remote_attn_ms": ra["ms"] / ra["count"], "gather_wait_ms": wait,
+            "overlap_frac": max(0.0, min(1.0, 1.0 - wait / ag)) if ag > 0 else None, "layers_timed": g["count"],
+            "source": "eager timing pass: HIP events on the communicator's stream (all-gather) and the compute "
+                      "stream (attention, join)"}
 
 
 def bench_cfg4(model, amp, dev, H, W, args, timed_fn):
@@ -442,12 +552,24 @@ def dry_run(args, world, rank):
     comm = DistComm() if world > 1 else None
     x = torch.ones(64, 64)
 
+    phases = {"kv_allgather": [], "kv_local_attention": [], "kv_remote_attention": [], "kv_gather_wait": []}
+
     def step():
+        # placeholder of one overlapped global layer: "local" product, the slot all-gather, "remote" product (CPU:
+        # sequential, so the gather is fully exposed)
+        t0 = time.perf_counter()
         y = x @ x
+        t1 = time.perf_counter()
         if comm is not None:
             t = torch.zeros(world * 4, 4)
             t[rank * 4:(rank + 1) * 4] = y[:4, :4]
             comm.allgather_slots(t, 4)
+        t2 = time.perf_counter()
+        y = y @ x
+        t3 = time.perf_counter()
+        for k, v in (("kv_local_attention", t1 - t0), ("kv_allgather", t2 - t1), ("kv_gather_wait", t2 - t1),
+                     ("kv_remote_attention", t3 - t2)):
+            phases[k].append(v * 1e3)
         return y
 
     try:
@@ -468,9 +590,10 @@ def dry_run(args, world, rank):
     except CommError as e:
         raise SystemExit(f"rank {rank}: {e}")
     if rank == 0:
+        kvo = kv_overlap({k: {"ms": sum(v), "count": len(v)} for k, v in phases.items()}) if world > 1 else None
         print(json.dumps({"metric": "dry-run (launcher rehearsal, no GPU)", "value": args.steps / dt, "unit": "steps/s",
                           "n_gpus": world, "world_size_observed": observed, "steps": args.steps,
-                          "warmup": args.warmup, "dry_run": True}), flush=True)
+                          "warmup": args.warmup, "dry_run": True, "kv_overlap": kvo}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

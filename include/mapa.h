@@ -61,14 +61,21 @@ int mapa_stream_check(mapa_stream_t stream, const char* what);
  *     every earlier launch on the stream has completed (graph-capturable).  The host zeroes slot[0], enqueues the
  *     work and the publish, and polls slot[0] != 0 — no stream synchronisation, so the GPU keeps running the work
  *     queued after the publish (MapAnything.infer publishes after the transformer and checks before returning).
+ *   mapa_fault_reset: enqueue on `stream` a kernel that clears the fault word once every earlier launch on the
+ *     stream has completed (graph-capturable); MapAnything.infer / forward start every call with it, so a publish
+ *     reports only faults of its own call.
  *   mapa_fault_status: synchronous read of the fault word (and reset to 0 when `reset`); -1 on a HIP error.
- *   mapa_stream_check also reports and clears it. */
-/* MAPA_FAULT_F16_RANGE: a MAPA_F16X2 producer met a value outside binary16's range (the TF32-equivalent heads'
- * operands); the outputs of that forward are not trustworthy and MapAnything.infer raises. */
+ *   mapa_stream_check also reports and clears it.
+ * The word is per device; the library's cached device properties (CU counts, co-resident slot counts of the
+ * LayerNorm-fused GEMM) are kept per device too, so one process may drive several devices. */
+/* MAPA_FAULT_F16_RANGE: a MAPA_F16 / MAPA_F16X2 producer met a value outside binary16's range (the TF32-equivalent
+ * heads' operands); the outputs of that forward are not trustworthy: MapAnything.infer / forward re-run the call with
+ * the fp32-exact split-precision heads (MapAnything._range_fallback) instead of returning them. */
 enum { MAPA_FAULT_LN_BARRIER = 1, MAPA_FAULT_F16_RANGE = 2 };
 int mapa_fault_slot_create(uint32_t** host, uint32_t** dev);
 int mapa_fault_slot_destroy(uint32_t* host);
 int mapa_fault_publish(uint32_t* dev_slot, mapa_stream_t stream);
+int mapa_fault_reset(mapa_stream_t stream);
 int mapa_fault_status(int reset);
 
 /* ---------------------------------------------------------------------------------------------------------
@@ -159,7 +166,9 @@ int64_t mapa_gemm_workspace_bytes(const mapa_gemm_desc* d);
  * the default; env MAPA_GEMM_VARIANT sets the initial value).  Codes: 643/644/1282/1283 = 128x128 tiles,
  * 2560..2574 = 256-row tiles, 2580/2581 = stream-K, 2582 = tail-only stream-K (these need a workspace; without one
  * the automatic choice runs), 2584..2586 / 2588 = LDS halo-window conv, 2589 = the same on flat-raster blocks with
- * split K (needs a workspace when it splits), 2587 = 192x192 tiles.  (The round-2 opt-in
+ * split K (needs a workspace when it splits), 2587 = 192x192 tiles; timing diagnostics with wrong results (dense A):
+ * 2591 / 2592 / 2593 = the 256x128 2-per-CU kernel compute-only / loads-only / without its epilogue, 2594 / 2595 /
+ * 2596 = the same for the 192x256 kernel.  (The round-2 opt-in
  * main-loop experiments — phase-interleaved and four-wave tiles — measured slower on every path shape and were
  * removed from the library) */
 int mapa_gemm_set_variant(int variant);
@@ -192,9 +201,19 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *     only N % 256 == 0 (the 192x256-tile form); 0 = always as a separate mapa_layernorm launch (A/B).
  *   MAPA_TUNE_LN_SPIN (default 0 = 2^22): polls of the fused LayerNorm's band barrier before it gives up.
  *   MAPA_TUNE_LN_TEST_SKIP (test hook, default 0): the next `value` LayerNorm-fused launches each have one tile
- *     (band 0, column tile 0) skip its statistics publish, so band 0 times out and raises MAPA_FAULT_LN_BARRIER. */
+ *     (band 0, column tile 0) skip its statistics publish, so band 0 times out and raises MAPA_FAULT_LN_BARRIER.
+ *   MAPA_TUNE_PERS (default 1, or the environment's MAPA_GEMM_PERS): the dense 16-bit linears with a transformer
+ *     epilogue (act -> 16-bit output, or the in-place fp32 residual update) and no ln_out run on the persistent
+ *     register-epilogue kernel; 1 = its automatic tile shape, 2..5 = tile shape 0..3 (256x128, 192x256, 256x256,
+ *     192x128), 0 = off (the data-parallel tile kernels).  Variants 2600..2603 force a shape.
+ *   MAPA_TUNE_PERS_LN (default 1, or the environment's MAPA_GEMM_PERS_LN): ln_out requests that the LayerNorm-fused
+ *     kernel takes run on the persistent register-epilogue form (192x128 tiles, 2 per CU, whole 192-row bands per
+ *     round, all co-resident); 0 = the 192-row LNF tile kernel.
+ *   MAPA_TUNE_DIAG_GRID (timing diagnostic, default 0): the data-parallel 256-row / 192-row tile kernels launch only
+ *     their first `value` workgroups (0 = every tile); outputs of the other tiles are left unwritten. */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,
-       MAPA_TUNE_LN_FUSE = 4, MAPA_TUNE_LN_SPIN = 5, MAPA_TUNE_LN_TEST_SKIP = 6 };
+       MAPA_TUNE_LN_FUSE = 4, MAPA_TUNE_LN_SPIN = 5, MAPA_TUNE_LN_TEST_SKIP = 6, MAPA_TUNE_DIAG_GRID = 7,
+       MAPA_TUNE_PERS = 8, MAPA_TUNE_PERS_LN = 9 };
 int mapa_gemm_tune(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------------------
@@ -397,6 +416,29 @@ int mapa_rope2d(void* tokens, int dtype, int B, int H, int N, int D, int64_t sb,
 
 /* dst[i] += src[i] (n % 4 == 0) */
 int mapa_add_f32(float* dst, const float* src, int64_t n, mapa_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Collectives of the view-sharded forward (csrc/comm.cpp): one process per GPU, RCCL over xGMI.
+ * Replaces the reference's torch.distributed setup for multi-GPU runs (mapanything/utils/train_tools.py:389-402) for
+ * the two exchanges the sharded path has — each global-attention layer's K/V slot all-gather
+ * (alternating_attention_transformer.py:657-661 attends over every view's tokens) and the scale-token broadcast.
+ * RCCL is dlopen'ed at first use (/opt/rocm/lib/librccl.so.1, or env MAPA_RCCL_LIB): no link-time dependency.
+ *   mapa_comm_unique_id_bytes / mapa_comm_get_unique_id: rank 0 makes the id; the host hands it to every rank by its
+ *     own channel (a TCP store, MPI, a file).
+ *   mapa_comm_init: non-blocking communicator set-up polled against timeout_s (<= 0: 600 s) on `device`; a peer that
+ *     never arrives or fails returns an error (the half-built communicator is aborted), never a hang.
+ *   mapa_comm_allgather_kv: in place, slot `rank` of `full` ([world][slot_bytes]) goes to every rank (enqueued on
+ *     `stream`, graph-capturable).  mapa_comm_broadcast: in place from `root`.
+ *   mapa_comm_check: 0, or -1 after an asynchronous error (the communicator is then aborted).
+ *   mapa_comm_destroy: finalize + destroy (abort != 0: ncclCommAbort, for a failed or timed-out peer). */
+typedef struct mapa_comm mapa_comm;
+int mapa_comm_unique_id_bytes(void);
+int mapa_comm_get_unique_id(void* id_out);
+int mapa_comm_init(mapa_comm** comm, int world, int rank, const void* id, int device, double timeout_s);
+int mapa_comm_allgather_kv(mapa_comm* comm, void* full, int64_t slot_bytes, mapa_stream_t stream);
+int mapa_comm_broadcast(mapa_comm* comm, void* buf, int64_t bytes, int root, mapa_stream_t stream);
+int mapa_comm_check(mapa_comm* comm);
+int mapa_comm_destroy(mapa_comm* comm, int abort);
 
 #ifdef __cplusplus
 }

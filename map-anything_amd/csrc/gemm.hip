@@ -348,6 +348,22 @@ static int pick_flat(const GemmArgs& a) {
   return conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split);
 }
 
+// Persistent register-epilogue kernel (gemm_pers.hip) for the dense transformer linears: mapa_gemm_tune(MAPA_TUNE_PERS,
+// .) / env MAPA_GEMM_PERS: 0 = off, 1 = on with the automatic tile shape, 2 + s = tile shape s; -1: env not read.
+static int g_pers = -1;
+static int pers_mode() {
+  if (g_pers < 0) g_pers = getenv("MAPA_GEMM_PERS") ? atoi(getenv("MAPA_GEMM_PERS")) : 1;
+  return g_pers;
+}
+
+// The LayerNorm-fused residual linears on the persistent kernel (launch_gemm_pers_ln) instead of gemm_big's LNF tiles:
+// mapa_gemm_tune(MAPA_TUNE_PERS_LN, .) / env MAPA_GEMM_PERS_LN, 1 = on (default), 0 = off; -1: env not read.
+static int g_pers_ln = -1;
+static int pers_ln_mode() {
+  if (g_pers_ln < 0) g_pers_ln = getenv("MAPA_GEMM_PERS_LN") ? atoi(getenv("MAPA_GEMM_PERS_LN")) : 1;
+  return g_pers_ln;
+}
+
 static int g_forced = -1;  // -1: not read yet; 0: automatic; else a kernel variant code (tuning / tests)
 
 static int forced_variant() {
@@ -490,20 +506,33 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
                    : forced ? (forced == 2589 ? conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split) : 0)
                             : pick_flat(a);
   const int lnf = pick_ln_fused(d, variant, sk);
+  if (lnf && pers_ln_mode() && !forced &&
+      launch_gemm_pers_ln(a, d->workspace, d->workspace_bytes, gemm_streamk_slots(1), stream)) {
+    MAPA_CHECK_LAUNCH("mapa_gemm (LayerNorm fused, persistent)");
+    return 0;
+  }
   if (lnf && launch_gemm_big_ln(a, lnf, d->workspace, d->workspace_bytes, stream)) {
     MAPA_CHECK_LAUNCH("mapa_gemm (LayerNorm fused)");
     return 0;  // launched (residual linear + the LayerNorm of its output rows)
   }
+  const bool pers_forced = forced >= 2600 && forced <= 2606;
+  const bool pers_auto = !forced && pers_mode() && !sk && ((variant >= 2560 && variant <= 2574) || variant == 2587);
   if (flat && launch_conv_halo_flat(a, flat, d->workspace, d->workspace_bytes, GEMM_TICKET_BYTES, stream)) {
     // launched (flat-raster halo conv, split K)
+  } else if (!conv && lp16 && !d->ln_out && (pers_forced || pers_auto) &&
+             launch_gemm_pers(a, pers_forced ? forced - 2600 : pers_mode() >= 2 ? pers_mode() - 2 : -1,
+                              gemm_streamk_slots(1), stream)) {
+    // launched (persistent register-epilogue kernel)
   } else if (sk && launch_gemm_streamk(a, conv, sk - 2580, d->workspace, d->workspace_bytes, stream)) {
     // launched (persistent stream-K grid)
   } else if (halo && (forced ? launch_conv_halo(a, forced == 2585 || forced == 2588 ? 256 : 128, stream,
                                                 forced == 2588 ? 8 : 16)
                               : launch_conv_halo(a, halo_rows8(a) ? 256 : 128, stream, halo_rows8(a) ? 8 : 16))) {
     // launched (LDS halo-window conv)
-  } else if (d->dtype != MAPA_F32 && ((variant >= 2560 && variant <= 2574) || variant == 2587) &&
-             launch_gemm_big(a, conv, variant == 2587 ? 15 : variant - 2560, stream)) {
+  } else if (d->dtype != MAPA_F32 && ((variant >= 2560 && variant <= 2574) || variant == 2587 ||
+                                      (variant >= 2591 && variant <= 2596)) &&
+             launch_gemm_big(a, conv, variant == 2587 ? 15 : variant >= 2591 ? variant - 2575 : variant - 2560,
+                             stream)) {
     // launched (bf16, or f16 for the tile kernels that carry an fp16 instantiation)
   } else if (d->dtype == MAPA_F16) {
     if (conv) launch_variant<TraitsF16, 1>(variant >= 2560 ? 643 : variant, nblk, stream, a);
@@ -546,7 +575,8 @@ extern "C" int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6,
 extern "C" int mapa_gemm_tune(int key, int value) {
   MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK || key == MAPA_TUNE_HALO_SPLIT ||
                      key == MAPA_TUNE_TILE_GROUP || key == MAPA_TUNE_LN_FUSE || key == MAPA_TUNE_LN_SPIN ||
-                     key == MAPA_TUNE_LN_TEST_SKIP,
+                     key == MAPA_TUNE_LN_TEST_SKIP || key == MAPA_TUNE_DIAG_GRID || key == MAPA_TUNE_PERS ||
+                     key == MAPA_TUNE_PERS_LN,
                  "mapa_gemm_tune: unknown key %d", key);
   MAPA_CHECK_ARG((key != MAPA_TUNE_LN_SPIN && key != MAPA_TUNE_LN_TEST_SKIP) || value >= 0,
                  "mapa_gemm_tune: negative value %d", value);
@@ -556,6 +586,20 @@ extern "C" int mapa_gemm_tune(int key, int value) {
   }
   if (key == MAPA_TUNE_LN_TEST_SKIP) {
     ln_arm_test_skip(value);
+    return 0;
+  }
+  if (key == MAPA_TUNE_PERS_LN) {
+    g_pers_ln = value ? 1 : 0;
+    return 0;
+  }
+  if (key == MAPA_TUNE_PERS) {
+    MAPA_CHECK_ARG(value >= 0 && value <= 8, "mapa_gemm_tune: persistent mode %d", value);
+    g_pers = value;
+    return 0;
+  }
+  if (key == MAPA_TUNE_DIAG_GRID) {
+    MAPA_CHECK_ARG(value >= 0, "mapa_gemm_tune: grid %d", value);
+    diag_set_grid(value);
     return 0;
   }
   MAPA_CHECK_ARG(key != MAPA_TUNE_HALO_SPLIT || (value >= 0 && value <= 64), "mapa_gemm_tune: split %d", value);
@@ -571,7 +615,8 @@ extern "C" int mapa_gemm_tune(int key, int value) {
 extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
                      (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582) ||
-                     (variant >= 2584 && variant <= 2589),
+                     (variant >= 2584 && variant <= 2589) || (variant >= 2591 && variant <= 2596) ||
+                     (variant >= 2600 && variant <= 2606),
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;

@@ -332,7 +332,7 @@ __device__ __forceinline__ void epi_store_row8(const GemmArgs& p, const EpiCol8&
 // Epilogue patterns of the transformer blocks, fixed once per tile so the per-row calls carry no output-set checks:
 // 1 = act(acc + bias) -> 16-bit out_lp only (qkv, fc1 + GELU); 2 = resid1 + gamma * (acc + bias) -> out_f32 only, in
 // place (attn proj, fc2); 0 = anything else (epi_store_row8).
-__device__ __forceinline__ int epi_mode(const GemmArgs& p) {
+__host__ __device__ __forceinline__ int epi_mode(const GemmArgs& p) {
   const bool lp_outs = p.out_lp_relu || p.out_s3 || p.out_s3_relu;
   if (p.out_mode != 0 || p.resid2 || lp_outs || p.ldo % 8 != 0 || !p.vec_ok) return 0;
   if (p.out_lp && !p.out_f32 && !p.resid1 && !p.gamma && (p.act == MAPA_ACT_NONE || p.act == MAPA_ACT_GELU)) return 1;
@@ -398,6 +398,22 @@ __device__ __forceinline__ void epi_store_row8_mode(const GemmArgs& p, const Epi
 // 256-row bf16 kernel (gemm_big.hip): variant 0 = 256x256 tile, 1 = 256x128 tile.  Returns false if it does not
 // take this shape.
 bool launch_gemm_big(const GemmArgs& a, bool conv, int variant, hipStream_t stream);
+// The 256-row tile kernels' instantiations, one translation unit each (parallel build): nullptr = no such variant.
+using GemmKernel = void (*)(GemmArgs);
+GemmKernel big_kernel_bf16_dense(int variant);       // gemm_big_dense.hip
+GemmKernel big_kernel_lnf(int variant);              // gemm_big_dense.hip (LayerNorm-fused: 14 / 15)
+GemmKernel big_kernel_bf16_conv(int variant);        // gemm_big_conv.hip
+GemmKernel big_kernel_f16(int variant, bool conv);   // gemm_big_f16.hip
+GemmKernel big_kernel_diag(int variant, bool conv);  // gemm_big_diag.hip
+int gemm_device_cus();                               // CUs of the current device (cached per device)
+void diag_set_grid(int blocks);  // timing diagnostic: launch only the first `blocks` tiles (0 = all)
+
+// Persistent data-parallel kernel for the transformer linears (gemm_pers.hip): dense 16-bit A, epi_mode 1 or 2,
+// register epilogue, the next tile's DMA prologue under the epilogue.  shape: 0 = 256x128 (2 / CU), 1 = 192x256,
+// 2 = 256x256, 3 = 192x128 (2 / CU); -1 = pers_pick_shape.  cus: the device's CU count.  false if the problem or its
+// epilogue does not qualify.
+bool launch_gemm_pers(const GemmArgs& a, int shape, int cus, hipStream_t stream);
+int pers_pick_shape(int M, int N, int K, int cus);
 
 // The in-place residual linear (epi_mode 2: out_f32 = resid1 + gamma * (acc + bias)) with the LayerNorm of its output
 // rows fused (gemm_big.hip, LNF): the row statistics combine across a band's column tiles inside the launch (band
@@ -413,6 +429,11 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
 // Tuning / test state of the LayerNorm-fused launches (mapa_gemm_tune MAPA_TUNE_LN_SPIN / MAPA_TUNE_LN_TEST_SKIP).
 void ln_set_spin(unsigned spins);
 void ln_arm_test_skip(int n);
+int ln_take_test_skip();    // 1 if an armed test skip is consumed by this launch
+unsigned ln_spin_value();   // the band barrier's poll bound
+// The LayerNorm-fused residual linear on the persistent register-epilogue kernel (gemm_pers.hip): 192x128 tiles at 2
+// workgroups per CU, N = 768 / 1024, the workspace of launch_gemm_big_ln.  false if it does not qualify.
+bool launch_gemm_pers_ln(const GemmArgs& a, void* ws, int64_t ws_bytes, int cus, hipStream_t stream);
 
 // Stride-1 3x3 conv with its A operand read from an LDS halo window (conv_halo.hip); bn = 256 / 128 / 0 (auto).
 // Returns false unless the conv is in the 32-channel-slice K order (conv_kblock == 32).

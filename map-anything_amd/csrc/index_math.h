@@ -49,6 +49,17 @@ MAPA_HD void tile_coords_rt(int b, int gm, int ntm, int ntn, int& tm, int& tn) {
   group_coords_rt(xcd_remap(b, ntm * ntn), gm, ntm, ntn, tm, tn);
 }
 
+// ---- persistent data-parallel GEMM (gemm_pers.hip): round r holds tiles [r*G, min((r+1)*G, tiles)); block b takes
+// the round's xcd_remap(b, n_r)-th tile (n_r = that round's tile count; blocks b >= n_r sit the round out), so in every
+// round — the last, partial one included — each XCD's blocks walk one contiguous range of the GM-row tile order.
+MAPA_HD bool pers_tile(int b, int G, int r, int tiles, int gm, int ntm, int ntn, int& tm, int& tn) {
+  const int base = r * G;
+  const int n = imin(G, tiles - base);
+  if (b >= n) return false;
+  group_coords_rt(base + xcd_remap(b, n), gm, ntm, ntn, tm, tn);
+  return true;
+}
+
 // ---- LayerNorm-fused residual GEMM (gemm_big.hip, LNF): the row statistics of a LayerNorm over N combine across the
 // ntn column tiles of a tile row ("band") inside the launch, so every band's tiles must run together.  The bands are
 // dealt to the 8 XCDs in contiguous ranges and each XCD walks its bands band-major (a band's ntn tiles consecutive in

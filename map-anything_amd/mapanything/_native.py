@@ -31,7 +31,9 @@ EXPORTED = (
     "mapa_split_bf16x3", "mapa_split_rows", "mapa_view_rays", "mapa_apply_mask", "mapa_confidence_mask", "mapa_attn_merge", "mapa_dense_adaptor",
     "mapa_normalize_image", "mapa_normal_cos_threshold", "mapa_rope2d", "mapa_gemm_tune",
     "mapa_regressor_head_out", "mapa_stream_check", "mapa_fault_slot_create", "mapa_fault_slot_destroy",
-    "mapa_fault_publish", "mapa_fault_status",
+    "mapa_fault_publish", "mapa_fault_status", "mapa_fault_reset",
+    "mapa_comm_unique_id_bytes", "mapa_comm_get_unique_id", "mapa_comm_init", "mapa_comm_allgather_kv",
+    "mapa_comm_broadcast", "mapa_comm_check", "mapa_comm_destroy",
 )
 FAULT_LN_BARRIER = 1  # include/mapa.h MAPA_FAULT_LN_BARRIER
 FAULT_F16_RANGE = 2  # include/mapa.h MAPA_FAULT_F16_RANGE
@@ -69,6 +71,19 @@ class AttnDesc(ctypes.Structure):
 
 class NativeError(RuntimeError):
     pass
+
+
+class DeviceFault(NativeError):
+    """A kernel set the library's device fault word (include/mapa.h MAPA_FAULT_*); `bits` holds the word."""
+
+    def __init__(self, bits: int):
+        super().__init__(_fault_message(bits))
+        self.bits = int(bits)
+
+    @property
+    def range_only(self) -> bool:
+        """Only MAPA_FAULT_F16_RANGE: a binary16 operand left binary16's range (the run is valid in another recipe)."""
+        return self.bits == FAULT_F16_RANGE
 
 
 def lib_path() -> str:
@@ -134,6 +149,13 @@ def load_library(path: Optional[str] = None):
     L.mapa_fault_slot_destroy.argtypes = [pu32]
     L.mapa_fault_publish.argtypes = [pu32, vp]
     L.mapa_fault_status.argtypes = [i]
+    L.mapa_fault_reset.argtypes = [vp]
+    L.mapa_comm_get_unique_id.argtypes = [vp]
+    L.mapa_comm_init.argtypes = [ctypes.POINTER(vp), i, i, vp, i, ctypes.c_double]
+    L.mapa_comm_allgather_kv.argtypes = [vp, vp, i64, vp]
+    L.mapa_comm_broadcast.argtypes = [vp, vp, i64, i, vp]
+    L.mapa_comm_check.argtypes = [vp]
+    L.mapa_comm_destroy.argtypes = [vp, i]
     _lib = L
     return L
 
@@ -219,7 +241,7 @@ def check_faults():
     """Raise NativeError if a kernel set the device fault word since the last check (synchronises the device)."""
     v = fault_status(reset=True)
     if v:
-        raise NativeError(_fault_message(v))
+        raise DeviceFault(v)
 
 
 class FaultTimeout(NativeError):
@@ -248,6 +270,11 @@ class FaultSlot:
     def publish(self):
         """Enqueue the publish on the current stream (also inside a graph capture)."""
         check(lib().mapa_fault_publish(self._d, stream()), "mapa_fault_publish")
+
+    @staticmethod
+    def reset():
+        """Enqueue the fault word's reset on the current stream (the start of a call; also inside a capture)."""
+        check(lib().mapa_fault_reset(stream()), "mapa_fault_reset")
 
     def wait(self, timeout_s: float = 600.0, poll=None):
         """Poll until the armed publish has run; raise NativeError if it carried a fault (the device word is reset).
@@ -279,7 +306,7 @@ class FaultSlot:
         bits = v >> 1
         if bits:
             fault_status(reset=True)
-            raise NativeError(_fault_message(bits))
+            raise DeviceFault(bits)
 
     def __del__(self):
         try:
@@ -287,6 +314,46 @@ class FaultSlot:
                 _lib.mapa_fault_slot_destroy(self._h)
         except Exception:  # noqa: BLE001 -- interpreter shutdown
             pass
+
+
+class CComm:
+    """The library's own RCCL communicator (include/mapa.h mapa_comm_*): what a non-Python host of libmapa.so uses for
+    the sharded forward's K/V all-gather and scale-token broadcast.  `uid` = rank 0's mapa_comm_get_unique_id bytes
+    (CComm.unique_id()), handed to every rank by the caller."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = lib()
+        buf = ctypes.create_string_buffer(int(L.mapa_comm_unique_id_bytes()))
+        if L.mapa_comm_get_unique_id(buf) != 0:
+            raise NativeError(L.mapa_last_error().decode())
+        return buf.raw
+
+    def __init__(self, world: int, rank: int, uid: bytes, device: int, timeout_s: float = 600.0):
+        L = lib()
+        self._c = ctypes.c_void_p()
+        if L.mapa_comm_init(ctypes.byref(self._c), world, rank, uid, device, float(timeout_s)) != 0:
+            raise NativeError(L.mapa_last_error().decode())
+        self.world, self.rank = world, rank
+
+    def allgather_slots(self, full: torch.Tensor, rows_per_slot: int):
+        slot = rows_per_slot * full[0].numel() * full.element_size()
+        check(lib().mapa_comm_allgather_kv(self._c, ctypes.c_void_p(full.data_ptr()), slot, stream()),
+              "mapa_comm_allgather_kv")
+
+    def broadcast_(self, t: torch.Tensor, src: int = 0):
+        check(lib().mapa_comm_broadcast(self._c, ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(), src,
+                                        stream()), "mapa_comm_broadcast")
+
+    def check_async(self):
+        check(lib().mapa_comm_check(self._c), "mapa_comm_check")
+
+    def close(self, abort: bool = False):
+        if self._c:
+            rc = lib().mapa_comm_destroy(self._c, 1 if abort else 0)
+            self._c = ctypes.c_void_p()
+            if rc != 0:
+                raise NativeError(lib().mapa_last_error().decode())
 
 
 # --------------------------------------------------------------------------------------- kernel timing
@@ -312,6 +379,21 @@ def timing_stop():
         ms = sum(a.elapsed_time(b) for a, b, _ in recs)
         out[kind] = {"ms": ms, "count": len(recs), "flops": float(sum(f for _, _, f in recs))}
     return out
+
+
+def mark(stream=None):
+    """An event recorded now on `stream` (default: the current stream) while kernel timing is on, else None."""
+    if _timing is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record(stream)
+    return e
+
+
+def span(kind, start, end):
+    """Record the interval between two mark() events under `kind` (no flops: a phase, not a kernel)."""
+    if _timing is not None and start is not None and end is not None:
+        _timing.setdefault(kind, []).append((start, end, 0.0))
 
 
 def _tic():
@@ -379,7 +461,7 @@ def attention_workspace(d) -> torch.Tensor:
 
 
 TUNE_CONV_HALO, TUNE_TAIL_STREAMK, TUNE_HALO_SPLIT, TUNE_TILE_GROUP, TUNE_LN_FUSE = 0, 1, 2, 3, 4
-TUNE_LN_SPIN, TUNE_LN_TEST_SKIP = 5, 6
+TUNE_LN_SPIN, TUNE_LN_TEST_SKIP, TUNE_DIAG_GRID, TUNE_PERS, TUNE_PERS_LN = 5, 6, 7, 8, 9
 
 
 def gemm_tune(key: int, value: int):
@@ -400,6 +482,38 @@ def gemm_set_variant(variant: int = 0):
     _WS_NEED.clear()
 
 
+def _wscale_epilogue(W, N, bias, gamma, act, head_out):
+    """Epilogue operands for a weight stored as 2^s x w (W._mapa_wscale = s, engine._f16_pack: a binary16 head weight
+    whose largest element sits outside [2^-4, 2^12] is rescaled by a power of two so that its small elements stay
+    normal binary16 numbers, as TF32 — fp32's exponent — keeps them).  The accumulator is then exactly 2^s x the
+    unscaled one, so the epilogue takes bias x 2^s and gamma x 2^-s (or a gamma of 2^-s), and the fused regressor
+    tail's 1x1 weights x 2^-s: all exact powers of two through a positively homogeneous activation (none or ReLU),
+    so every output bit equals the unscaled arithmetic's.  The scaled copies are made once per (weight, bias, gamma)
+    and kept on the weight tensor (before any graph capture: the engine's eager warm-up)."""
+    s = W._mapa_wscale
+    if act not in (ACT_NONE, ACT_RELU):
+        raise NativeError("a power-of-two scaled weight needs a linear or ReLU epilogue")
+    cache = W.__dict__.setdefault("_mapa_wsc_cache", [])
+    w6 = head_out[0] if head_out is not None else None
+    for b0, g0, w60, ent in cache:
+        if b0 is bias and g0 is gamma and w60 is w6:
+            b2, g2, w62 = ent
+            break
+    else:
+        up, dn = 2.0 ** s, 2.0 ** -s
+        b2 = None if bias is None else (bias.float() * up).contiguous()
+        if head_out is not None:  # the fused regressor tail applies no gamma: its 1x1 weights take the 2^-s
+            g2, w62 = None, (w6.float() * dn).contiguous()
+        else:
+            g2 = (gamma.float() * dn).contiguous() if gamma is not None else \
+                torch.full((N,), dn, dtype=torch.float32, device=W.device)
+            w62 = None
+        cache.append((bias, gamma, w6, (b2, g2, w62)))
+    if head_out is not None:
+        return b2, gamma, (w62,) + tuple(head_out[1:])
+    return b2, g2, head_out
+
+
 def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_NONE, resid1=None, resid2=None,
          out_f32=None, out_lp=None, out_lp_relu=None, out_s3=None, out_s3_relu=None, ldo=None, conv=None,
          pixshuf=None, head_out=None, ln=None):
@@ -413,6 +527,8 @@ def gemm(A, W, M, N, K, *, lda=None, bias=None, bias_mod=0, gamma=None, act=ACT_
     outputs; image i uses scale[i // views_per_scale]).
     ln=(w, b, eps, out): the LayerNorm of out_f32's rows into out (the GEMM's 16-bit dtype; mapa_gemm_desc.ln_*), fused
     into the residual linear where the library can (include/mapa.h)."""
+    if getattr(W, "_mapa_wscale", 0):
+        bias, gamma, head_out = _wscale_epilogue(W, N, bias, gamma, act, head_out)
     d = GemmDesc()
     d.dtype = dt_code(A.dtype)
     assert W.dtype == A.dtype

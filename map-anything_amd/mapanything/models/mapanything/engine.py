@@ -105,12 +105,31 @@ class GeoInputs:
 KBLOCK = 32  # channel block of the head convs' K order (include/mapa.h conv_kblock)
 
 
-def _f16_pack(w: np.ndarray, dev) -> torch.Tensor:
+# A binary16 head weight whose largest magnitude lies in [2^WS_LO, 2^WS_HI] is stored as is; otherwise it is stored
+# as 2^s x w with s putting that magnitude in [2^8, 2^9) (_f16_wscale), and the GEMM epilogue takes the power of two
+# back out exactly (_native._wscale_epilogue).  TF32 has fp32's 8-bit exponent: a weight tensor of tiny (or huge)
+# values keeps its 11 significant bits there, and keeps them here too.
+WS_LO, WS_HI = -4, 12
+
+
+def _f16_wscale(wt: torch.Tensor) -> int:
+    """Power-of-two exponent s of a binary16 weight's storage scale (0 = stored as is)."""
+    m = float(wt.abs().max()) if wt.numel() else 0.0
+    if m == 0.0 or 2.0 ** WS_LO <= m <= 2.0 ** WS_HI:
+        return 0
+    return 8 - math.floor(math.log2(m))
+
+
+def _f16_pack(w: np.ndarray, dev, scaled: bool = False) -> torch.Tensor:
     """[out][taps][cin] fp32 -> binary16 [out][taps * ceil8(cin)]: the weight side of the TF32-equivalent heads
     (activations binary16 too, include/mapa.h MAPA_F16): both operands at TF32's 11 significant bits, fp32
-    accumulation, on the f16 MFMA pipe at the bf16 rate."""
+    accumulation, on the f16 MFMA pipe at the bf16 rate.  scaled: store 2^s x w for a weight outside binary16's
+    comfortable range (WS_LO / WS_HI; the tensor carries _mapa_wscale = s for nat.gemm's epilogue)."""
     o, taps, cin = w.shape
     wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+    s = _f16_wscale(wt) if scaled else 0
+    if s:
+        wt = wt * (2.0 ** s)
     if bool((wt.abs() > 65504).any()):
         raise ValueError("a head weight exceeds binary16's range: use head_precision='fp32'")
     cp = _ceil8(cin)
@@ -118,15 +137,20 @@ def _f16_pack(w: np.ndarray, dev) -> torch.Tensor:
     out[:, :, :cin] = wt.to(torch.float16)
     out = out.reshape(o, -1)
     out._mapa_split = True  # timed with the fp32-recipe heads (nat.gemm: "gemm_split" / "conv3x3_split")
+    out._mapa_wscale = s
     return out
 
 
-def _f16x2_pack(w: np.ndarray, dev) -> torch.Tensor:
+def _f16x2_pack(w: np.ndarray, dev, scaled: bool = False) -> torch.Tensor:
     """[out][taps][cin] fp32 -> binary16 [out][taps * 2 * ceil8(cin)] = [w | w] per tap: the weight side of the
     TF32-equivalent heads (activations stored [hi | lo] of binary16, include/mapa.h MAPA_F16X2), a plain f16 GEMM over
-    K = 2C that accumulates w*(x_hi + x_lo): the weight at 11 significant bits as TF32 rounds it, the activation at 22."""
+    K = 2C that accumulates w*(x_hi + x_lo): the weight at 11 significant bits as TF32 rounds it, the activation at 22.
+    scaled: as _f16_pack."""
     o, taps, cin = w.shape
     wt = torch.from_numpy(np.ascontiguousarray(w)).to(dev)
+    s = _f16_wscale(wt) if scaled else 0
+    if s:
+        wt = wt * (2.0 ** s)
     if bool((wt.abs() > 65504).any()):
         raise ValueError("a head weight exceeds binary16's range: use head_precision='fp32'")
     h = wt.to(torch.float16)
@@ -135,6 +159,7 @@ def _f16x2_pack(w: np.ndarray, dev) -> torch.Tensor:
     out[:, :, 0, :cin], out[:, :, 1, :cin] = h, h
     out = out.reshape(o, -1)
     out._mapa_split = True  # timed with the split heads (nat.gemm: "gemm_split" / "conv3x3_split")
+    out._mapa_wscale = s
     return out
 
 
@@ -187,8 +212,10 @@ class PackedWeights:
                 dev, self.lp)
 
         def hpack(w):  # head weights [out][taps][cin]: lp (or fp32) [out][taps*cin], or split-packed
-            if head_split:
-                return {"f16": _f16_pack, "f16x2": _f16x2_pack}.get(head_fmt, _split_pack)(w, dev)
+            if head_split:  # (binary16 head weights with a power-of-two storage scale where their range needs one)
+                if head_fmt in ("f16", "f16x2"):
+                    return (_f16_pack if head_fmt == "f16" else _f16x2_pack)(w, dev, scaled=True)
+                return _split_pack(w, dev)
             return torch.from_numpy(np.ascontiguousarray(w.reshape(w.shape[0], -1))).to(dev, self.lp)
 
         def hlin(name):
@@ -206,6 +233,7 @@ class PackedWeights:
                 return t
             r = t.view(o, 9, c // KBLOCK, KBLOCK).permute(0, 2, 1, 3).contiguous().reshape(o, -1)
             r._mapa_split = getattr(t, "_mapa_split", False)
+            r._mapa_wscale = getattr(t, "_mapa_wscale", 0)
             r._mapa_kblock = KBLOCK
             return r
 
@@ -872,13 +900,22 @@ class MapaEngine:
                 own = segs[shard.rank]
                 rest = [sg for r, sg in enumerate(segs) if r != shard.rank]
             lse_l = self._empty(NH, L, dtype=torch.float32)
+            # eager timing pass (bench.py kv_overlap): local- and remote-key attention and the join's exposed wait on
+            # this stream; the all-gather itself is timed on the communicator's stream (RcclComm)
+            t0 = nat.mark()
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao, seq_kv=own[1], kv_segments=[own], lse=lse_l,
                           kind="attention_global", **strides)
+            t1 = nat.mark()
             handle.wait()
+            t2 = nat.mark()
             ao_r = self._empty(L, C)
             lse_r = self._empty(NH, L, dtype=torch.float32)
             nat.attention(q_loc, kv_full, kv_full[:, C:], ao_r, seq_kv=sum(sg[1] for sg in rest), kv_segments=rest,
                           lse=lse_r, kind="attention_global", **strides)
+            t3 = nat.mark()
+            nat.span("kv_local_attention", t0, t1)
+            nat.span("kv_gather_wait", t1, t2)
+            nat.span("kv_remote_attention", t2, t3)
             nat.attn_merge(ao, lse_l, ao_r, lse_r, ao, L, NH, C)
         nat.gemm(ao, p["proj"], L, C, C, bias=p["proj_b"], resid1=y, out_f32=y, **self._lnf(p["n2w"], p["n2b"], yn))
         nat.gemm(yn, p["fc1"], L, 4 * C, C, bias=p["fc1_b"], act=nat.ACT_GELU, out_lp=hbuf)
@@ -1146,6 +1183,9 @@ class MapaEngine:
         if H % PATCH or W % PATCH:
             raise AssertionError(f"Input shape must be divisible by patch size: {PATCH}")
         imgs = imgs.to(self.device, torch.float32).contiguous()
+        if fault is not None:  # the call's publish reports only the faults raised since here (stream order)
+            with torch.cuda.device(self.device):
+                fault.reset()
         B = scenes
         if B > 1 and ((geo is not None and geo.scenes != B) or taps is not None or VB % B
                       or (shard is not None and shard.scenes != B)):

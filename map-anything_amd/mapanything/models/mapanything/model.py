@@ -300,14 +300,16 @@ class MapAnything:
             return self.head_precision
         return "fp32" if precision == "fp16" else "tf32"
 
-    def engine(self, precision: Optional[str] = None):
+    def engine(self, precision: Optional[str] = None, heads: Optional[str] = None):
+        """The engine of a run at `precision` (heads: override heads_for(precision), e.g. the fp32-exact heads of the
+        binary16 range fallback)."""
         prec = precision or self.precision
         if self._sd is None:
             raise RuntimeError("no weights loaded: use from_pretrained(local_dir), load_state_dict() or "
                                "load_synthetic_weights()")
         if self._device.type != "cuda":
             raise nat.NativeError("MapAnything (MI355X engine) runs on a gfx950 device only: call .to('cuda')")
-        heads = self.heads_for(prec)
+        heads = heads if heads is not None and prec != "fp32" else self.heads_for(prec)
         key = (str(self._device), prec, heads)
         if key not in self._engines:
             from .engine import MapaEngine
@@ -353,6 +355,7 @@ class MapAnything:
                 old.close()
         self._comm = comm
         self._gather = gather_outputs
+        self._comm_dead = None
         return self
 
     # ------------------------------------------------------------------------------------------ forward
@@ -496,9 +499,12 @@ class MapAnything:
             self._geo_inputs_scenes(views, B, [self._metric_flags(self._scene_views(views, b, B)) for b in range(B)],
                                     plan)
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
-        raw = self._run_engine(self.engine(precision), imgs, plan, geo, self._dpt_chunk(memory_efficient_inference),
-                               scenes=B)
-        self._await_faults(plan)
+        eng = self.engine(precision)
+        raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)
+        if self._await_faults(plan, eng):  # binary16 range left: this call again with the fp32-exact heads
+            eng = self._range_fallback(precision)
+            raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)
+            self._await_faults(plan)
         return self._finish(raw, plan, len(views), with_post=False, scenes=B)
 
     # entries a view may carry and still run in a batched-scene engine call: images and every geometric input
@@ -570,7 +576,14 @@ class MapAnything:
                 with torch.cuda.stream(side):  # eager warm-up: lazy packing, pos-embed caches
                     eng.run(static_in, shard=plan, comm=comm, geo=static_geo, pe_idx=static_pe, scenes=scenes,
                             fault=self._arm_fault())
-                    self._await_local_fault()
+                    try:
+                        self._await_local_fault()
+                    except nat.DeviceFault as e:
+                        # binary16 range left in the warm-up: capture anyway (every rank captures the same
+                        # collectives); the replay below reports it again and the caller re-runs with the fp32-exact
+                        # heads (_await_faults -> _range_fallback)
+                        if not (e.range_only and eng.hsplit and eng.hfmt in ("f16", "f16x2")):
+                            raise
                 torch.cuda.current_stream(imgs.device).wait_stream(side)
                 graph = torch.cuda.CUDAGraph()
                 gslot = nat.FaultSlot()  # the graph's own publish slot (its address is baked into the graph)
@@ -657,39 +670,81 @@ class MapAnything:
         if slot is not None:
             slot.wait()
 
-    def _await_faults(self, plan):
+    # binary16 range fallbacks taken (MAPA_FAULT_F16_RANGE under the TF32-equivalent heads; bench.py reports it)
+    range_fallbacks = 0
+
+    def _range_fallback(self, precision):
+        """The engine a call re-runs on after its TF32-equivalent (binary16) heads or geometric encoders left
+        binary16's range: the fp32-exact split-precision heads (head_precision='fp32'), whose operands cover fp32's
+        range as the reference's TF32 does (model.py:89-93, 1774).  Counted in range_fallbacks; warned once."""
+        MapAnything.range_fallbacks += 1
+        if MapAnything.range_fallbacks == 1:
+            warnings.warn("a binary16 head operand left binary16's range (MAPA_FAULT_F16_RANGE): the call was re-run "
+                          "with the fp32-exact heads (head_precision='fp32'); later calls do the same when needed")
+        return self.engine(precision, heads="fp32")
+
+    def _comm_failed(self, comm, why: str):
+        """The communicator was aborted (a hung or failed collective): graphs captured against it hold its freed RCCL
+        state, so they are dropped and the model refuses sharded calls until enable_view_sharding() installs a new
+        communicator (a replay on an aborted communicator faults instead of raising)."""
+        for k in [k for k in self._graphs if k[-1] is not None]:
+            del self._graphs[k]
+        if hasattr(comm, "graph_safe"):
+            comm.graph_safe = False
+        self._shard_graphs = False
+        self.shard_graph_fallback = f"communicator aborted: {why}"
+        self._comm_dead = why
+
+    def _await_faults(self, plan, eng=None) -> bool:
         """Wait for this call's fault publish (the GPU is past the transformer then and still has the heads queued,
         so the wait costs no GPU time) and raise NativeError if a kernel set the device fault word — a LayerNorm-
-        fused band barrier that timed out (include/mapa.h fault channel): the outputs are then never returned.  A
-        sharded model that gathers outputs agrees first, so every rank raises together instead of one rank leaving
-        the others in the gather."""
+        fused band barrier that timed out (include/mapa.h fault channel): the outputs are then never returned.
+        Returns True instead when the only fault is MAPA_FAULT_F16_RANGE and `eng` runs binary16 ("tf32") heads /
+        geometric encoders: the caller re-runs the call with the fp32-exact heads (_range_fallback).  A sharded
+        model agrees across ranks first — whenever it gathers outputs or a range fallback is possible — so every rank
+        raises, or re-runs its collectives, together instead of one rank leaving the others in a collective."""
         err = None
         st = self._fault_state()
         slot, st.pending = st.pending, None
         if slot is not None and os.environ.get("MAPA_FAULT_WAIT", "1") == "0":  # A/B switch: publish, never wait
             slot.armed = False
             slot = None
+        comm = self._comm if plan is not None else None
         if slot is not None:
-            comm = self._comm if plan is not None else None
+            from ...parallel import CommError
+
             try:
                 if comm is None:
                     slot.wait()
                 else:  # sharded: a hung collective never lets the forward reach its publish
                     slot.wait(timeout_s=comm_timeout().total_seconds(), poll=getattr(comm, "check_async", None))
             except nat.FaultTimeout as e:
-                from ...parallel import CommError
-
+                if comm is None:
+                    raise
                 if hasattr(comm, "abort"):
                     comm.abort()  # RCCL's kernels stop on the abort flag; the stream can drain
+                self._comm_failed(comm, f"rank {plan.rank}: forward not complete ({e})")
                 raise CommError(f"sharded forward on rank {plan.rank} did not complete: {e} (RCCL communicator "
                                 "aborted)") from e
+            except CommError as e:  # check_async: the communicator reported an error (and was aborted)
+                self._comm_failed(comm, str(e))
+                raise
             except nat.NativeError as e:
                 err = e
-        if plan is not None and self._gather is not None and plan.world > 1 and hasattr(self._comm, "all_agree"):
-            if not self._comm.all_agree(err is None, self._device):
-                raise err or nat.NativeError("a device fault on another rank (include/mapa.h fault channel)")
-        elif err is not None:
+        range_ok = eng is not None and eng.hsplit and eng.hfmt in ("f16", "f16x2")
+        retry = range_ok and isinstance(err, nat.DeviceFault) and err.range_only
+        if plan is not None and plan.world > 1 and hasattr(self._comm, "all_agree") and \
+                (self._gather is not None or range_ok):
+            # host-side agreement where the communicator has one (a gloo group: the GPU keeps running the heads)
+            agree = getattr(self._comm, "all_agree_host", None) or (lambda ok: self._comm.all_agree(ok, self._device))
+            if agree(err is None):
+                return False
+            if range_ok and agree(err is None or retry):
+                return True  # every rank re-runs (their collectives pair up again)
+            raise err or nat.NativeError("a device fault on another rank (include/mapa.h fault channel)")
+        if err is not None and not retry:
             raise err
+        return retry
 
     @torch.inference_mode()
     def infer(self, views: List[Dict[str, Any]], memory_efficient_inference: bool = False, use_amp: bool = True,
@@ -743,13 +798,18 @@ class MapAnything:
             geo = self._geo_inputs_scenes(processed, B, metric, plan, **use)
         imgs = self._scene_major(torch.cat([v["img"] for v in local], 0).to(self._device, torch.float32), B)
         eng = self.engine(precision)
-        raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)
-        post = postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
-                                   mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
-                                   edge_depth_threshold=edge_depth_threshold,
-                                   apply_confidence_mask=apply_confidence_mask,
-                                   confidence_percentile=confidence_percentile)
-        self._await_faults(plan)
+
+        def run(eng):
+            raw = self._run_engine(eng, imgs, plan, geo, self._dpt_chunk(memory_efficient_inference), scenes=B)
+            return postprocess_outputs(raw, imgs, eng.w.norm_mean, eng.w.norm_std, apply_mask=apply_mask,
+                                       mask_edges=mask_edges, edge_normal_threshold=edge_normal_threshold,
+                                       edge_depth_threshold=edge_depth_threshold,
+                                       apply_confidence_mask=apply_confidence_mask,
+                                       confidence_percentile=confidence_percentile)
+        post = run(eng)
+        if self._await_faults(plan, eng):  # binary16 range left: this call again with the fp32-exact heads
+            post = run(self._range_fallback(precision))
+            self._await_faults(plan)
         return self._finish(post, plan, len(views), with_post=True, scenes=B)
 
     def _dpt_chunk(self, memory_efficient: bool):
@@ -766,6 +826,11 @@ class MapAnything:
     def _local_views(self, views, scenes: int = 1):
         if self._comm is None:
             return views, None
+        if getattr(self, "_comm_dead", None):
+            from ...parallel import CommError
+
+            raise CommError(f"the view-sharding communicator was aborted ({self._comm_dead}); call "
+                            "enable_view_sharding() again")
         from ...parallel import ShardPlan
 
         H, W = views[0]["img"].shape[-2:]

@@ -198,6 +198,18 @@ class DistComm:
         self._call("agreement all-reduce", self.dist.all_reduce, flag, op=self.dist.ReduceOp.MIN, group=self.group)
         return bool(flag.item())
 
+    def all_agree_host(self, ok: bool) -> bool:
+        """all_agree over a gloo group of the same ranks on a CPU tensor: no device work and no stream
+        synchronisation (the per-call fault agreement, MapAnything._await_faults, while the GPU still runs the heads).
+        The group is made on first use — every rank reaches that call at the same point of the same call."""
+        if getattr(self, "_host_group", None) is None:
+            ranks = None if self.group is None else self.dist.get_process_group_ranks(self.group)
+            self._host_group = self.dist.new_group(ranks=ranks, backend="gloo")
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        self._call("agreement all-reduce (host)", self.dist.all_reduce, flag, op=self.dist.ReduceOp.MIN,
+                   group=self._host_group)
+        return bool(flag.item())
+
     def gather_views(self, local: torch.Tensor, counts: List[int], dst: Optional[int]) -> Optional[torch.Tensor]:
         """View-major local rows [counts[rank], ...] -> [sum(counts), ...] in rank order on rank dst (None: on
         every rank); other ranks get None.  Slots are padded to max(counts) so one collective moves them."""
@@ -250,10 +262,16 @@ class RcclComm(DistComm):
             raise CommError(f"{what} failed on rank {self.rank} of {self.world}: {e}") from e
 
     def check_async(self):
-        self._rc("RCCL", self._nccl.check_async)
+        try:
+            self._rc("RCCL", self._nccl.check_async)
+        except CommError:
+            self.graph_safe = False  # check_async aborted the communicator
+            raise
 
     def abort(self):
+        """ncclCommAbort; the communicator is unusable afterwards (graphs captured against it must not replay)."""
         self._nccl.abort()
+        self.graph_safe = False
 
     def close(self, abort: bool = False):
         """Release the RCCL communicator (ncclCommFinalize + ncclCommDestroy, or ncclCommAbort after an error)."""
@@ -263,10 +281,14 @@ class RcclComm(DistComm):
         self._rc("K/V all-gather", self._nccl.all_gather_, full, rows_per_slot, torch.cuda.current_stream())
 
     def allgather_slots_async(self, full: torch.Tensor, rows_per_slot: int):
+        from . import _native as nat
+
         cur = torch.cuda.current_stream()
         side = self._side
         side.wait_stream(cur)  # the K/V projection into this rank's slot is done
+        g0 = nat.mark(side)  # eager timing pass only (bench.py kv_overlap): the gather on the communicator's stream
         self._rc("K/V all-gather", self._nccl.all_gather_, full, rows_per_slot, side)
+        nat.span("kv_allgather", g0, nat.mark(side))
 
         class _Handle:
             def wait(self_inner):
@@ -322,6 +344,9 @@ class ThreadComm:
             if t.is_cuda:
                 torch.cuda.current_stream().synchronize()
         self._barrier.wait()
+
+    def all_agree_host(self, ok: bool) -> bool:
+        return self.all_agree(ok)
 
     def all_agree(self, ok: bool, device=None) -> bool:
         """True on every rank thread iff ok on every one (barrier-exchanged flags)."""

@@ -158,6 +158,31 @@ def load_images(folder_or_list, resize_mode="fixed_mapping", size=None, norm_typ
                  data_norm_type=[norm_type]) for i in range(len(resized))]
 
 
+def iter_load_images(scenes, prefetch=1, **kwargs):
+    """Yield load_images(scene, **kwargs) for every scene (a folder or a file list) in order, with the host part of
+    the next `prefetch` scenes (decode + Lanczos / bicubic resize + crop: load_resized_images, PIL on host threads,
+    GIL released) running while the caller works on the current one — so a stream of scenes fed to
+    MapAnything.infer keeps the GPU busy instead of alternating host decode and GPU inference.  Each scene's uint8
+    images go to the GPU and are normalised when the scene is yielded (stream-ordered behind the previous scene's
+    work).  Results are exactly load_images' (the same functions, only overlapped)."""
+    from concurrent.futures import ThreadPoolExecutor as _TPE
+
+    scenes = list(scenes)
+    device = kwargs.pop("device", None)
+    norm_type = kwargs.get("norm_type", "dinov2")
+    host_kw = {k: v for k, v in kwargs.items() if k != "device"}
+    prefetch = max(1, int(prefetch))
+    with _TPE(max_workers=prefetch) as ahead:
+        pending = [ahead.submit(load_resized_images, sc, **host_kw) for sc in scenes[:prefetch]]
+        for k in range(len(scenes)):
+            resized = pending.pop(0).result()
+            if k + prefetch < len(scenes):
+                pending.append(ahead.submit(load_resized_images, scenes[k + prefetch], **host_kw))
+            imgs = normalize_images(resized, norm_type, device)
+            yield [dict(img=imgs[i:i + 1], true_shape=np.int32([resized[i].size[::-1]]), idx=i, instance=str(i),
+                        data_norm_type=[norm_type]) for i in range(len(resized))]
+
+
 def _to_pil(img, view_idx):
     """image.py:468-497."""
     if isinstance(img, torch.Tensor):

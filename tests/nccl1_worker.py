@@ -55,10 +55,16 @@ def main():
     # segment tables over the gathered slots)
     views2 = [{"img": torch.cat([v["img"], torch.from_numpy(i)], 0), "data_norm_type": ["dinov2"]}
               for v, i in zip(views, synthetic.synthetic_images(V, 224, 224, 43))]
+    # two batched scenes with mixed geometric inputs (b2_224: rays / depth / poses per view; the camera inputs
+    # normalised per scene and picked per local image under the capture)
+    from tests_helpers import CASES, make_views
+
+    geo2 = make_views(CASES["b2_224"])
     res = {}
-    for mode in ("gather", "overlap", "scenes2"):
+    for mode in ("gather", "overlap", "scenes2", "geoscenes2"):
         os.environ["MAPA_FORCE_OVERLAP"] = "1" if mode == "overlap" else "0"
-        vw = views2 if mode == "scenes2" else views
+        vw = {"scenes2": views2, "geoscenes2": geo2}.get(mode, views)
+        nv = len(vw)
         for prec in ("fp32", "bf16"):
             model = MapAnything(**released_config(), precision=prec).load_synthetic_weights().to("cuda")
             kw = dict(use_amp=prec == "bf16", apply_mask=False)
@@ -85,7 +91,7 @@ def main():
                 "graph_eq_eager": all(torch.equal(a[k], b[k]) for a, b in zip(g1, eager) for k in KEYS),
                 "replay_eq_eager": all(torch.equal(a[k], b[k]) for a, b in zip(g2, eager) for k in KEYS),
                 "eager_eq_single": all(torch.equal(a[k], b[k]) for a, b in zip(eager, single) for k in KEYS),
-                "err_vs_single": {k: max(rel(eager[v][k], single[v][k]) for v in range(V)) for k in KEYS},
+                "err_vs_single": {k: max(rel(eager[v][k], single[v][k]) for v in range(nv)) for k in KEYS},
                 "warnings": [str(w.message)[:500] for w in caught],
             }
             model._comm.close()

@@ -32,6 +32,10 @@ def test_bench_gpus_n_launches_n_ranks():
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["world_size_observed"] == 2 and line["dry_run"]
+    # the N > 1 line explains its own overlap: per-layer all-gather vs local / remote attention (bench.kv_overlap)
+    kvo = line["kv_overlap"]
+    for k in ("allgather_ms_per_layer", "local_attn_ms", "remote_attn_ms", "gather_wait_ms", "overlap_frac"):
+        assert k in kvo and kvo[k] is not None and kvo[k] >= 0, (k, kvo)
 
 
 def test_bench_failing_rank_fails_the_job():

@@ -150,6 +150,51 @@ def test_gemm_big_and_streamk_variants(nat, variant, M, N, K):
         assert ws.numel() > 0 and int(ws[: 4 * 65536].count_nonzero()) == 0
 
 
+@pytest.mark.parametrize("variant", [0, 2600, 2601, 2602, 2603])
+@pytest.mark.parametrize("M,N,K", [(10960, 3072, 1024), (10953, 768, 768), (3001, 200, 264), (513, 136, 72),
+                                   (700, 4100, 128), (5, 12, 8)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_gemm_persistent_register_epilogue(nat, variant, M, N, K, dtype):
+    """The persistent register-epilogue kernel (gemm_pers.hip; 0 = the automatic choice, which takes it for these
+    epilogues; 2600..2603 = each tile shape) on both transformer patterns — act(acc + bias) -> 16-bit (GELU and
+    plain) and the in-place fp32 residual x += gamma * (acc + bias) — on ragged M / N / K, with more tiles than
+    resident workgroups (several rounds) and fewer; deterministic, and bitwise equal to the data-parallel tile kernels
+    (same MFMA products and K order, only the operand order and the store path differ)."""
+    A = _rand(M, K, seed=31).to(dtype)
+    W = _rand(N, K, scale=K ** -0.5, seed=32).to(dtype)
+    b, g, r = _rand(N, seed=33), _rand(N, seed=34), _rand(M, N, seed=35)
+    acc = A.float() @ W.float().t() + b
+    outs = {}
+    for tag, var, pers in (("pers", variant, 1), ("tiles", 0, 0)):
+        nat.gemm_set_variant(var)
+        nat.gemm_tune(nat.TUNE_PERS, pers)
+        try:
+            o = torch.empty(M, N, device="cuda", dtype=dtype)
+            og = torch.empty(M, N, device="cuda", dtype=dtype)
+            x = r.clone()
+            nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
+            nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=og)
+            nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=x, out_f32=x)
+            og2 = torch.empty_like(og)
+            nat.gemm(A, W, M, N, K, bias=b, act=nat.ACT_GELU, out_lp=og2)
+            torch.cuda.synchronize()
+        finally:
+            nat.gemm_set_variant(0)
+            nat.gemm_tune(nat.TUNE_PERS, 1)
+        outs[tag] = (o, og, x)
+        assert torch.equal(og, og2)
+    o, og, x = outs["pers"]
+    assert rel_l2(o.float().cpu(), acc.cpu()) < 5e-3
+    assert rel_l2(og.float().cpu(), F.gelu(acc).cpu()) < 5e-3
+    assert rel_l2(x.cpu(), (r + g * acc).cpu()) < 1e-4
+    # the plain and residual outputs bitwise; the GELU one bitwise where both use the bf16 GELU epilogue (the 128x128
+    # kernels of small problems evaluate the fp32 erf form: rounding flips only)
+    assert torch.equal(outs["pers"][0], outs["tiles"][0]) and torch.equal(outs["pers"][2], outs["tiles"][2])
+    assert rel_l2(outs["pers"][1].float().cpu(), outs["tiles"][1].float().cpu()) < 5e-3
+    if M >= 10000:  # the path shapes: both on the 16-bit GELU epilogue
+        assert torch.equal(outs["pers"][1], outs["tiles"][1])
+
+
 def _ln_flag(nat):
     """The library's device fault word (include/mapa.h fault channel): MAPA_FAULT_LN_BARRIER if a band barrier of a
     LayerNorm-fused launch gave up."""

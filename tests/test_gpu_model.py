@@ -677,12 +677,14 @@ def test_infer_raises_on_layernorm_barrier_timeout(model, graphs):
 
 
 @pytest.mark.parametrize("graphs", [False, True])
-def test_infer_raises_on_f16_range_fault(model, graphs):
-    """The TF32-equivalent heads' binary16 operands (include/mapa.h MAPA_F16X2): a head activation outside binary16's
+def test_infer_falls_back_on_f16_range_fault(model, graphs):
+    """The TF32-equivalent heads' binary16 operands (include/mapa.h MAPA_F16): a head activation outside binary16's
     range (here forced by scaling one packed head weight by 2^20) sets MAPA_FAULT_F16_RANGE, published before the
-    last conv, and infer() raises instead of returning outputs — eager and graph-replayed; restored weights give
-    bit-identical outputs again."""
+    last conv; infer() does not raise but re-runs the call with the fp32-exact heads (MapAnything._range_fallback,
+    counted in range_fallbacks) — eager and graph-replayed — and returns exactly what head_precision='fp32' returns;
+    restored weights give bit-identical TF32-recipe outputs again without a fallback."""
     from mapanything import _native as nat
+    from mapanything.models import MapAnything
 
     views = _views(CASES["cfg1_224"])
     kw = dict(use_amp=True, apply_mask=False)
@@ -694,22 +696,36 @@ def test_infer_raises_on_f16_range_fault(model, graphs):
     try:
         model._graphs.clear()
         before = model.infer(views, **kw)
+        model.head_precision = "fp32"
+        ref = model.infer(views, **kw)  # the fp32-exact heads (their own packed weights: untouched below)
+        model.head_precision = None
         with torch.inference_mode():  # the packed weights are inference tensors
             w.mul_(2.0 ** 20)  # f16: saturates to inf where |w| > 65504 / 2^20 — the conv output leaves the range
-        with pytest.raises(nat.NativeError, match="F16_RANGE"):
-            model.infer(views, **kw)
+        n0 = MapAnything.range_fallbacks
+        with pytest.warns(UserWarning) if n0 == 0 else _nullcontext():
+            fell = model.infer(views, **kw)
+        assert MapAnything.range_fallbacks == n0 + 1
         assert nat.fault_status(reset=False) == 0
         with torch.inference_mode():
             w.copy_(keep)
         after = model.infer(views, **kw)
+        assert MapAnything.range_fallbacks == n0 + 1
     finally:
+        model.head_precision = None
         with torch.inference_mode():
             w.copy_(keep)
         model.hip_graphs = True
         model._graphs.clear()
-    for a, b in zip(before, after):
+    for a, b, r, f in zip(before, after, ref, fell):
         for k in ("pts3d", "conf", "cam_quats", "metric_scaling_factor"):
             assert torch.equal(a[k], b[k]), k
+            assert torch.equal(f[k], r[k]), k
+
+
+def _nullcontext():
+    import contextlib
+
+    return contextlib.nullcontext()
 
 
 FP16_CASES = ["cfg1_224", "mm_224", "v2_518", "cfg2_518"]

@@ -258,7 +258,7 @@ def test_sharded_geometric_inputs_equal_single(precision, tol):
                 assert e < tol, (r, v, k, e)
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5)])
+@pytest.mark.parametrize("precision,tol", [("fp32", 2e-5), ("bf16", 8e-3)])
 def test_sharded_batched_geometric_scenes_equal_single(precision, tol):
     """B = 2 scenes x 3 views with mixed geometric inputs (b2_224) on a 2-rank shard, one engine call per rank: the
     dense encoders over each rank's images of both scenes, the camera inputs normalised per scene over ALL its views
@@ -268,7 +268,7 @@ def test_sharded_batched_geometric_scenes_equal_single(precision, tol):
     from tests_helpers import CASES, make_views, released_config
 
     case = CASES["b2_224"]
-    kw = dict(use_amp=False, apply_mask=False)
+    kw = dict(use_amp=precision != "fp32", apply_mask=False)  # bf16: the default TF32-equivalent heads
     ref_model = MapAnything(**released_config(), precision=precision).load_synthetic_weights().to("cuda")
     ref = ref_model.infer(make_views(case), **kw)
     assert ref[0]["pts3d"].shape[0] == 2
@@ -277,7 +277,7 @@ def test_sharded_batched_geometric_scenes_equal_single(precision, tol):
     model = MapAnything(**released_config(), precision=precision).to("cuda")
     model._sd = ref_model._sd
     model.enable_view_sharding(comm=comm, gather_outputs="all")
-    model.engine("fp32")
+    model.engine(precision)
     calls = []
     real = model._run_engine
     model._run_engine = lambda *a_, **k: calls.append((k.get("scenes"), a_[3] is not None)) or real(*a_, **k)

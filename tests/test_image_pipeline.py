@@ -144,6 +144,30 @@ def test_load_images_matches_reference(fx, files, case):
 
 
 @pytest.mark.gpu
+def test_iter_load_images_prefetch_matches_load_images(fx, files):
+    """The prefetching scene iterator (host decode / resize of scene k+1 under the caller's work on scene k) yields
+    exactly load_images' views for every scene, in order — the reference fixtures included."""
+    from mapanything.utils.image import iter_load_images, load_images
+
+    d, names = files
+    scenes = [_source(c, d, names) for c in CASES]
+    kws = [CASES[c] for c in CASES]
+    # one keyword set per stream: the iterator takes the same arguments as load_images
+    for prefetch in (1, 2):
+        for sc, kw, c, got in zip(scenes, kws, CASES, (next(iter_load_images([s], prefetch=prefetch, **k))
+                                                       for s, k in zip(scenes, kws))):
+            ref = load_images(sc, **kw)
+            assert len(got) == len(ref)
+            for a, b in zip(got, ref):
+                assert torch.equal(a["img"], b["img"]) and np.array_equal(a["true_shape"], b["true_shape"])
+    seq = list(iter_load_images([scenes[0]] * 3, prefetch=2))
+    step = int(fx["fixed__step"])
+    for views in seq:
+        imgs = torch.cat([r["img"] for r in views], 0)
+        assert np.array_equal(imgs.cpu().numpy()[:, :, ::step, ::step], fx["fixed__norm"])
+
+
+@pytest.mark.gpu
 def test_preprocess_inputs_matches_reference(fx):
     from mapanything.utils.image import preprocess_inputs
 
