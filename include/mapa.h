@@ -206,9 +206,9 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *     epilogue (act -> 16-bit output, or the in-place fp32 residual update) and no ln_out run on the persistent
  *     register-epilogue kernel; 1 = its automatic tile shape, 2..5 = tile shape 0..3 (256x128, 192x256, 256x256,
  *     192x128), 0 = off (the data-parallel tile kernels).  Variants 2600..2603 force a shape.
- *   MAPA_TUNE_PERS_LN (default 1, or the environment's MAPA_GEMM_PERS_LN): ln_out requests that the LayerNorm-fused
- *     kernel takes run on the persistent register-epilogue form (192x128 tiles, 2 per CU, whole 192-row bands per
- *     round, all co-resident); 0 = the 192-row LNF tile kernel.
+ *   MAPA_TUNE_PERS_LN (default 0, or the environment's MAPA_GEMM_PERS_LN): 1 = ln_out requests that the LayerNorm-
+ *     fused kernel takes run on the persistent register-epilogue form (192x128 tiles, 2 per CU, whole 192-row bands
+ *     per round, all co-resident); 0 = the 192-row LNF tile kernel (measured faster on the path shapes).
  *   MAPA_TUNE_DIAG_GRID (timing diagnostic, default 0): the data-parallel 256-row / 192-row tile kernels launch only
  *     their first `value` workgroups (0 = every tile); outputs of the other tiles are left unwritten. */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,

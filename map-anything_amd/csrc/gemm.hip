@@ -357,10 +357,11 @@ static int pers_mode() {
 }
 
 // The LayerNorm-fused residual linears on the persistent kernel (launch_gemm_pers_ln) instead of gemm_big's LNF tiles:
-// mapa_gemm_tune(MAPA_TUNE_PERS_LN, .) / env MAPA_GEMM_PERS_LN, 1 = on (default), 0 = off; -1: env not read.
+// mapa_gemm_tune(MAPA_TUNE_PERS_LN, .) / env MAPA_GEMM_PERS_LN, 1 = on, 0 = off (default: 1-4 us slower per launch
+// than the LNF tiles on the path shapes, tools/pers_ab.py, profiles/r6/pers_ab.json); -1: env not read.
 static int g_pers_ln = -1;
 static int pers_ln_mode() {
-  if (g_pers_ln < 0) g_pers_ln = getenv("MAPA_GEMM_PERS_LN") ? atoi(getenv("MAPA_GEMM_PERS_LN")) : 1;
+  if (g_pers_ln < 0) g_pers_ln = getenv("MAPA_GEMM_PERS_LN") ? atoi(getenv("MAPA_GEMM_PERS_LN")) : 0;
   return g_pers_ln;
 }
 

@@ -256,6 +256,9 @@ class FaultSlot:
 
     def __init__(self):
         L = lib()
+        if _DEFERRED_SLOTS and not torch.cuda.is_current_stream_capturing():
+            while _DEFERRED_SLOTS:
+                L.mapa_fault_slot_destroy(_DEFERRED_SLOTS.pop())
         h, d = ctypes.POINTER(ctypes.c_uint32)(), ctypes.POINTER(ctypes.c_uint32)()
         if L.mapa_fault_slot_create(ctypes.byref(h), ctypes.byref(d)) != 0:
             raise NativeError(L.mapa_last_error().decode())
@@ -309,11 +312,20 @@ class FaultSlot:
             raise DeviceFault(bits)
 
     def __del__(self):
+        # a slot can be collected at any allocation — also while a HIP graph is being captured on this thread (a
+        # cyclic reference freed by the garbage collector), where a host free would invalidate the capture: then the
+        # free waits for the next slot made outside a capture
         try:
             if _lib is not None and getattr(self, "_h", None):
-                _lib.mapa_fault_slot_destroy(self._h)
+                if torch.cuda.is_current_stream_capturing():
+                    _DEFERRED_SLOTS.append(self._h)
+                else:
+                    _lib.mapa_fault_slot_destroy(self._h)
         except Exception:  # noqa: BLE001 -- interpreter shutdown
             pass
+
+
+_DEFERRED_SLOTS = []  # FaultSlot host words collected during a capture, freed by the next FaultSlot()
 
 
 class CComm:

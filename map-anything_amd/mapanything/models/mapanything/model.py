@@ -740,10 +740,12 @@ class MapAnything:
             if agree(err is None):
                 return False
             if range_ok and agree(err is None or retry):
+                err = None
                 return True  # every rank re-runs (their collectives pair up again)
             raise err or nat.NativeError("a device fault on another rank (include/mapa.h fault channel)")
         if err is not None and not retry:
             raise err
+        err = None  # (the exception's traceback holds this frame: drop the cycle so the fault slot is freed now)
         return retry
 
     @torch.inference_mode()

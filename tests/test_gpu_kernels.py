@@ -208,12 +208,14 @@ def _ln_flag(nat):
                                          (10953, 768, 3072, False), (150, 768, 768, False), (4001, 1024, 1024, True),
                                          (21905, 768, 3072, False), (80001, 1024, 1024, True),
                                          (136901, 768, 768, False)])
-def test_gemm_layernorm_fused(nat, M, N, K, gamma):
+@pytest.mark.parametrize("pers_ln", [0, 1])
+def test_gemm_layernorm_fused(nat, M, N, K, gamma, pers_ln):
     """mapa_gemm with ln_out (the next sub-block's LayerNorm fused into the residual linear): the fp32 residual
     stream bitwise equal to the plain GEMM's, the bf16 normalised rows within one bf16 rounding of the standalone
     two-pass LayerNorm of that stream (mapa_layernorm) and of torch's fp32 LayerNorm, repeatable bit for bit, and no
     band barrier timed out.  MAPA_TUNE_LN_FUSE=0 (GEMM, then LayerNorm) is the A side, 1 fuses only where the tile
-    choice is the 192-row kernel, 2 (the default) whatever it is."""
+    choice is the 192-row kernel, 2 (the default) whatever it is.  pers_ln = 1: the fused forms on the persistent
+    register-epilogue kernel (MAPA_TUNE_PERS_LN; whole 192-row bands per round)."""
     A = _rand(M, K, seed=61).to(torch.bfloat16)
     W = _rand(N, K, scale=K ** -0.5, seed=62).to(torch.bfloat16)
     b = _rand(N, seed=63)
@@ -223,6 +225,7 @@ def test_gemm_layernorm_fused(nat, M, N, K, gamma):
 
     def run(fuse):
         nat.gemm_tune(nat.TUNE_LN_FUSE, fuse)
+        nat.gemm_tune(nat.TUNE_PERS_LN, pers_ln)
         x = x0.clone()
         y = torch.full((M, N), float("nan"), device="cuda", dtype=torch.bfloat16)
         nat.gemm(A, W, M, N, K, bias=b, gamma=g, resid1=x, out_f32=x, ln=(lw, lb, 1e-6, y))
@@ -235,6 +238,7 @@ def test_gemm_layernorm_fused(nat, M, N, K, gamma):
         xa, ya = run(2)  # the default: the fused kernel whatever the tile choice (B = 2: more tiles than CUs)
     finally:
         nat.gemm_tune(nat.TUNE_LN_FUSE, 2)  # the default
+        nat.gemm_tune(nat.TUNE_PERS_LN, 0)
     assert _ln_flag(nat) == 0
     assert torch.equal(xf, xs) and torch.equal(xf2, xf) and torch.equal(yf2, yf)
     assert not torch.isnan(yf.float()).any() and not torch.isnan(ya.float()).any()
@@ -248,7 +252,8 @@ def test_gemm_layernorm_fused(nat, M, N, K, gamma):
     assert rel_l2(xa.cpu(), xs.cpu()) < 1e-6  # another tile kernel for the residual when the choice differed
 
 
-def test_gemm_layernorm_barrier_timeout_is_reported(nat):
+@pytest.mark.parametrize("pers_ln", [0, 1])
+def test_gemm_layernorm_barrier_timeout_is_reported(nat, pers_ln):
     """A band that never completes (the test hook drops tile (0, 0)'s statistics publish; MAPA_TUNE_LN_SPIN shortens
     the bounded wait) must not hang and must not pass silently: the fault word carries MAPA_FAULT_LN_BARRIER, a
     FaultSlot published after the launch raises, check_faults raises and resets, and the next call is clean — its
@@ -265,6 +270,7 @@ def test_gemm_layernorm_barrier_timeout_is_reported(nat):
         nat.gemm(A, W, M, N, K, bias=b, resid1=x, out_f32=x, ln=(lw, lb, 1e-6, y))
         return x, y
 
+    nat.gemm_tune(nat.TUNE_PERS_LN, pers_ln)
     assert nat.fault_status(reset=True) == 0
     x_ok, y_ok = run()
     slot = nat.FaultSlot()
@@ -297,6 +303,7 @@ def test_gemm_layernorm_barrier_timeout_is_reported(nat):
     assert torch.equal(y_bad[192:], y_ok[192:])  # only band 0's normalised rows are invalid
     x2, y2 = run()
     torch.cuda.synchronize()
+    nat.gemm_tune(nat.TUNE_PERS_LN, 0)
     assert nat.fault_status(reset=False) == 0
     assert torch.equal(x2, x_ok) and torch.equal(y2, y_ok)
 

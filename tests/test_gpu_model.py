@@ -679,7 +679,7 @@ def test_infer_raises_on_layernorm_barrier_timeout(model, graphs):
 @pytest.mark.parametrize("graphs", [False, True])
 def test_infer_falls_back_on_f16_range_fault(model, graphs):
     """The TF32-equivalent heads' binary16 operands (include/mapa.h MAPA_F16): a head activation outside binary16's
-    range (here forced by scaling one packed head weight by 2^20) sets MAPA_FAULT_F16_RANGE, published before the
+    range (here forced by scaling one head conv's effective weights by 2^20) sets MAPA_FAULT_F16_RANGE, published before the
     last conv; infer() does not raise but re-runs the call with the fp32-exact heads (MapAnything._range_fallback,
     counted in range_fallbacks) — eager and graph-replayed — and returns exactly what head_precision='fp32' returns;
     restored weights give bit-identical TF32-recipe outputs again without a fallback."""
@@ -691,7 +691,7 @@ def test_infer_falls_back_on_f16_range_fault(model, graphs):
     eng = model.engine("bf16")
     assert eng.hfmt == "f16"
     w = eng.w.refine[4]["resConfUnit2"]["c1"]
-    keep = w.clone()
+    s0 = w._mapa_wscale
     model.hip_graphs = graphs
     try:
         model._graphs.clear()
@@ -699,21 +699,25 @@ def test_infer_falls_back_on_f16_range_fault(model, graphs):
         model.head_precision = "fp32"
         ref = model.infer(views, **kw)  # the fp32-exact heads (their own packed weights: untouched below)
         model.head_precision = None
-        with torch.inference_mode():  # the packed weights are inference tensors
-            w.mul_(2.0 ** 20)  # f16: saturates to inf where |w| > 65504 / 2^20 — the conv output leaves the range
+        # the conv's effective weights x 2^20: its stored power-of-two scale lowered by 20 (engine._f16_wscale; the
+        # epilogue then multiplies by 2^20 more), so its outputs leave binary16's range
+        w._mapa_wscale = s0 - 20
+        w.__dict__.pop("_mapa_wsc_cache", None)
+        model._graphs.clear()  # captured graphs hold the epilogue's scaled bias / gamma copies: capture afresh
         n0 = MapAnything.range_fallbacks
         with pytest.warns(UserWarning) if n0 == 0 else _nullcontext():
             fell = model.infer(views, **kw)
         assert MapAnything.range_fallbacks == n0 + 1
         assert nat.fault_status(reset=False) == 0
-        with torch.inference_mode():
-            w.copy_(keep)
+        w._mapa_wscale = s0
+        w.__dict__.pop("_mapa_wsc_cache", None)
+        model._graphs.clear()
         after = model.infer(views, **kw)
         assert MapAnything.range_fallbacks == n0 + 1
     finally:
         model.head_precision = None
-        with torch.inference_mode():
-            w.copy_(keep)
+        w._mapa_wscale = s0
+        w.__dict__.pop("_mapa_wsc_cache", None)
         model.hip_graphs = True
         model._graphs.clear()
     for a, b, r, f in zip(before, after, ref, fell):
