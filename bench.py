@@ -43,7 +43,7 @@ import torch  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
 PEAK_HBM_GBS = 8000.0
-PROFILE_ROUND = "r5"          # profiles/<round>/: the rocprofv3 PMC summaries the roofline / attention objects cite
+PROFILE_ROUND = "r6"          # profiles/<round>/: the rocprofv3 PMC summaries the roofline / attention objects cite
 
 
 def enc_linear_flops_per_view(T):

@@ -29,6 +29,8 @@ from collections import defaultdict
 def group(name: str) -> str:
     if "conv_halo_kernel" in name:
         return "conv3x3"
+    if "gemm_pers" in name:  # gemm_pers.hip: dense A only (the transformer linears, persistent register epilogue)
+        return "gemm"
     m = re.search(r"gemm_(?:big|8p|w4|sk)_kernel<(?:[^,<>]*P8Cfg<[^>]*>, )?(\d)", name)
     if m:
         return "conv3x3" if m.group(1) == "1" else "gemm"
@@ -44,7 +46,7 @@ def group(name: str) -> str:
 
 def _is_gemm(name):
     return "gemm_big_kernel" in name or "gemm_kernel<" in name or "gemm_sk_kernel" in name or \
-        "gemm_pp_kernel" in name or "conv_halo_kernel" in name
+        "gemm_pp_kernel" in name or "conv_halo_kernel" in name or "gemm_pers" in name
 
 
 def dispatch_kinds(names, log_path, keep_shape=False):
