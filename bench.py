@@ -394,7 +394,8 @@ def bench_from_files(model, amp, V, args, timed_fn):
     """End to end from image files: V square JPEGs of --from-files-src pixels a side per scene, decoded, Lanczos-
     resized to 518x518 and normalised by the input pipeline (utils/image.py, the reference's load_images), then
     infer().  Sequential (load_images then infer, per scene) and prefetched (iter_load_images: the next scene's host
-    decode / resize runs on host threads under this scene's GPU work).  Not the headline: the host's decode rate."""
+    decode runs on host threads under this scene's GPU work), for the GPU resize (default) and the host PIL resize.
+    Not the headline: it includes the host's JPEG decode rate."""
     import tempfile
 
     import PIL.Image
@@ -410,24 +411,32 @@ def bench_from_files(model, amp, V, args, timed_fn):
         PIL.Image.fromarray(synthetic_image(S, S, 100 + i)).save(p, quality=95)
         paths.append(p)
     steps = max(2, args.steps // 2)
-    model.infer(load_images(paths), **amp)  # warm-up
-    seq = timed_fn(lambda: model.infer(load_images(paths), **amp), steps)
-    t_load = timed_fn(lambda: load_images(paths), steps)
 
-    def prefetched():
-        for views in iter_load_images([paths] * steps, prefetch=1):
-            model.infer(views, **amp)
-    pre = timed_fn(prefetched, 1)
+    def leg(gpu_resize):
+        model.infer(load_images(paths, gpu_resize=gpu_resize), **amp)  # warm-up
+        seq = timed_fn(lambda: model.infer(load_images(paths, gpu_resize=gpu_resize), **amp), steps)
+        t_load = timed_fn(lambda: load_images(paths, gpu_resize=gpu_resize), steps)
+
+        def prefetched():
+            for views in iter_load_images([paths] * steps, prefetch=1, gpu_resize=gpu_resize):
+                model.infer(views, **amp)
+        pre = timed_fn(prefetched, 1)
+        return {"sequential": {"value": V * steps / seq, "unit": "views/s", "ms_per_step": seq / steps * 1e3},
+                "prefetched": {"value": V * steps / pre, "unit": "views/s", "ms_per_step": pre / steps * 1e3},
+                "load_only": {"value": V * steps / t_load, "unit": "views/s", "ms_per_step": t_load / steps * 1e3}}
+    gpu = leg(True)
+    pil = leg(False)
     for p in paths:
         os.remove(p)
     os.rmdir(tmp)
     threads = min(16, os.cpu_count() or 1)
     return {"views": V, "src": f"{S}x{S} JPEG (q95) -> 518x518 Lanczos (fixed_mapping)", "steps": steps,
-            "sequential": {"value": V * steps / seq, "unit": "views/s", "ms_per_step": seq / steps * 1e3},
-            "prefetched": {"value": V * steps / pre, "unit": "views/s", "ms_per_step": pre / steps * 1e3},
-            "host_load_only": {"value": V * steps / t_load, "unit": "views/s", "ms_per_step": t_load / steps * 1e3},
-            "host_threads": threads,
-            "note": "host decode / resize with PIL (bit-identical to the reference); the in-HBM headline excludes it"}
+            **gpu, "host_threads": threads,
+            "pil_resize": pil,
+            "note": "default loader: host JPEG decode (PIL, thread pool) + GPU resize / crop / normalise "
+                    "(mapa_resize_normalize, bit-identical with PIL's Image.resize); pil_resize: the host PIL resize "
+                    "path.  load_only = the loader alone (decode + H2D + resize, synchronised).  The in-HBM "
+                    "headline excludes the loader"}
 
 
 def kv_overlap(ktimes):

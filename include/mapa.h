@@ -317,6 +317,37 @@ int mapa_dense_head_out(const void* hidden, int dtype, int n, int HW, const floa
 int mapa_normalize_image(const uint8_t* hwc, int n, int H, int W, const float* mean3, const float* std3, float* out,
                          mapa_stream_t stream);
 
+/* GPU resize of the input pipeline, bit-exact with PIL's Image.resize on 8-bit RGB (the reference's
+ * crop_resize_if_necessary: cropping.py:188-280 / 385-465, called from image.py:283-303), fused with the crop and
+ * ToTensor + Normalize.  Replaces the host Image.resize(LANCZOS | BICUBIC) + crop + mapa_normalize_image chain.
+ * Two steps, so a host can place the weights where it wants:
+ *  1. mapa_resize_plan_build (HOST only, no device): Pillow's float64 window weights -> 22-bit fixed point
+ *     (Resample.c precompute_coeffs + normalize_coeffs_8bpc, Pillow 12.2.0) for an in_w x in_h -> rs_w x rs_h
+ *     resize followed by the crop box (crop_left, crop_top, +out_w, +out_h) of the resized image, into `plan`
+ *     (mapa_resize_plan_bytes bytes: a mapa_resize_plan header + int32 tables);
+ *  2. copy the plan to device memory, then mapa_resize_normalize: src u8 [in_h][src_row_bytes] (HWC RGB, device)
+ *     -> out f32 [3][out_h][out_w] = (u8 / 255 - mean) / std (torchvision's order, like mapa_normalize_image) and/or
+ *     out_u8 [out_h][out_w][3] (either may be NULL).  plan_host: the host plan (launch geometry), plan_dev: its device
+ *     copy (weights); workspace: mapa_resize_workspace_bytes(plan_host) bytes of device scratch (the 8-bit
+ *     intermediate image of the horizontal pass).
+ * filter: MAPA_RESAMPLE_* (PIL.Image.Resampling numbering). */
+enum { MAPA_RESAMPLE_LANCZOS = 1, MAPA_RESAMPLE_BILINEAR = 2, MAPA_RESAMPLE_BICUBIC = 3 };
+typedef struct mapa_resize_plan {
+  int32_t in_w, in_h, rs_w, rs_h, crop_left, crop_top, out_w, out_h, filter;
+  int32_t need_h, need_v;      /* a pass runs only when its size changes (Resample.c need_horizontal / need_vertical) */
+  int32_t kh, kv;              /* window sizes (fixed-point weights per output column / row) */
+  int32_t row0, nrows;         /* input rows the kept output rows read */
+  int32_t off_hb, off_hk, off_vb, off_vk;  /* int32 offsets of the bounds {xmin, count} / weight tables */
+  int32_t int32s;              /* plan size in int32s */
+} mapa_resize_plan;
+int64_t mapa_resize_plan_bytes(int in_w, int in_h, int rs_w, int rs_h, int filter);
+int mapa_resize_plan_build(int in_w, int in_h, int rs_w, int rs_h, int crop_left, int crop_top, int out_w, int out_h,
+                           int filter, void* plan, int64_t plan_bytes);
+int64_t mapa_resize_workspace_bytes(const void* plan_host);
+int mapa_resize_normalize(const uint8_t* src, int64_t src_row_bytes, const void* plan_host, const void* plan_dev,
+                          const float* mean3, const float* std3, float* out, uint8_t* out_u8, void* workspace,
+                          int64_t workspace_bytes, mapa_stream_t stream);
+
 /* Dense adaptor on its own (RayDirectionsPlusDepthWithConfidenceAndMaskAdaptor, adaptors.py:1898-1951 ->
  * 1740-1796, 393-523, 1012-1073, 1114-1133), for the module-level API (model.dense_adaptor): raw [n][HW][6] f32
  * (the regressor's conv1x1 output rows) -> NCHW f32 planes value [n][4][HW] = (ray / max(|ray|, 1e-8), exp(depth)),

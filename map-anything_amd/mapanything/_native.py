@@ -34,9 +34,18 @@ EXPORTED = (
     "mapa_fault_publish", "mapa_fault_status", "mapa_fault_reset",
     "mapa_comm_unique_id_bytes", "mapa_comm_get_unique_id", "mapa_comm_init", "mapa_comm_allgather_kv",
     "mapa_comm_broadcast", "mapa_comm_check", "mapa_comm_destroy",
+    "mapa_resize_plan_bytes", "mapa_resize_plan_build", "mapa_resize_workspace_bytes", "mapa_resize_normalize",
 )
 FAULT_LN_BARRIER = 1  # include/mapa.h MAPA_FAULT_LN_BARRIER
 FAULT_F16_RANGE = 2  # include/mapa.h MAPA_FAULT_F16_RANGE
+RESAMPLE_LANCZOS, RESAMPLE_BILINEAR, RESAMPLE_BICUBIC = 1, 2, 3  # include/mapa.h MAPA_RESAMPLE_* (PIL numbering)
+
+
+class ResizePlan(ctypes.Structure):
+    """include/mapa.h mapa_resize_plan (the header of a resize plan blob)."""
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "in_w", "in_h", "rs_w", "rs_h", "crop_left", "crop_top", "out_w", "out_h", "filter", "need_h", "need_v",
+        "kh", "kv", "row0", "nrows", "off_hb", "off_hk", "off_vb", "off_vk", "int32s")]
 
 
 class GemmDesc(ctypes.Structure):
@@ -156,6 +165,12 @@ def load_library(path: Optional[str] = None):
     L.mapa_comm_broadcast.argtypes = [vp, vp, i64, i, vp]
     L.mapa_comm_check.argtypes = [vp]
     L.mapa_comm_destroy.argtypes = [vp, i]
+    L.mapa_resize_plan_bytes.argtypes = [i, i, i, i, i]
+    L.mapa_resize_plan_bytes.restype = i64
+    L.mapa_resize_plan_build.argtypes = [i, i, i, i, i, i, i, i, i, vp, i64]
+    L.mapa_resize_workspace_bytes.argtypes = [vp]
+    L.mapa_resize_workspace_bytes.restype = i64
+    L.mapa_resize_normalize.argtypes = [vp, i64, vp, vp, vp, vp, vp, vp, vp, i64, vp]
     _lib = L
     return L
 
@@ -726,6 +741,46 @@ def postprocess_mask(pts3d, pts3d_cam, mask_in, mask_out, n, H, W, normal_cos_th
     check(lib().mapa_postprocess_mask(ptr(pts3d), ptr(pts3d_cam), ptr(mask_in), ptr(mask_out), n, H, W,
                                       float(normal_cos_thr), depth_rtol, int(use_edges), ptr(work), stream()),
           "mapa_postprocess_mask")
+
+
+def resize_plan(in_w, in_h, rs_w, rs_h, crop_left, crop_top, out_w, out_h, filter_):
+    """Host-only (no device): PIL's fixed-point resampling plan for an in_w x in_h -> rs_w x rs_h resize followed by
+    the crop (crop_left, crop_top, +out_w, +out_h), as an int32 numpy blob (include/mapa.h mapa_resize_plan_build)."""
+    import numpy as np
+    L = load_library()
+    nb = L.mapa_resize_plan_bytes(in_w, in_h, rs_w, rs_h, filter_)
+    if nb < 0:
+        raise NativeError(L.mapa_last_error().decode())
+    blob = np.zeros(nb // 4, np.int32)
+    check(L.mapa_resize_plan_build(in_w, in_h, rs_w, rs_h, crop_left, crop_top, out_w, out_h, filter_,
+                                   blob.ctypes.data, nb), "mapa_resize_plan_build")
+    return blob
+
+
+def resize_plan_header(blob) -> ResizePlan:
+    return ResizePlan.from_buffer_copy(blob[:ctypes.sizeof(ResizePlan) // 4].tobytes())
+
+
+def resize_workspace_bytes(blob) -> int:
+    return int(load_library().mapa_resize_workspace_bytes(blob.ctypes.data))
+
+
+def resize_normalize(src_u8, src_row_bytes, blob, plan_dev, mean=None, std=None, out=None, out_u8=None,
+                     workspace=None):
+    """src_u8 (device, HWC RGB rows of src_row_bytes) -> out [3][out_h][out_w] f32 normalised and / or out_u8
+    [out_h][out_w][3]; blob: the host plan, plan_dev: its device copy (include/mapa.h mapa_resize_normalize)."""
+    m = s = None
+    if out is not None:
+        m = (ctypes.c_float * 3)(*[float(x) for x in mean])
+        s = (ctypes.c_float * 3)(*[float(x) for x in std])
+    ws = resize_workspace_bytes(blob)
+    if ws and (workspace is None or workspace.numel() * workspace.element_size() < ws):
+        raise NativeError(f"resize_normalize: workspace of {ws} bytes needed")
+    check(lib().mapa_resize_normalize(ptr(src_u8), int(src_row_bytes), blob.ctypes.data, ptr(plan_dev),
+                                      ctypes.cast(m, ctypes.c_void_p) if m is not None else None,
+                                      ctypes.cast(s, ctypes.c_void_p) if s is not None else None, ptr(out),
+                                      ptr(out_u8), ptr(workspace) if ws else None, ws, stream()),
+          "mapa_resize_normalize")
 
 
 def normal_cos_threshold(tol_deg: float) -> float:

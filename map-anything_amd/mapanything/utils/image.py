@@ -104,10 +104,10 @@ def normalize_images(pil_images: List[PIL.Image.Image], norm_type="dinov2", devi
     return out
 
 
-def load_resized_images(folder_or_list, resize_mode="fixed_mapping", size=None, norm_type="dinov2", patch_size=14,
-                        verbose=False, bayer_format=False, resolution_set=518, stride=1, num_workers=None):
-    """Host part of load_images (image.py:163-303): decode (EXIF-transposed RGB), choose the common target size,
-    Lanczos / bicubic resize + crop.  Returns the resized PIL images."""
+def _decode_scene(folder_or_list, resize_mode, size, norm_type, patch_size, verbose, bayer_format, resolution_set,
+                  stride, pool):
+    """image.py:163-275: decode every image (EXIF-transposed RGB; unreadable files skipped) and choose the common
+    target size.  Returns (decoded PIL images, (width, height))."""
     _check_resize_args(resize_mode, size)
     if bayer_format:
         raise NotImplementedError("bayer_format needs OpenCV's demosaicing, which this image does not ship")
@@ -128,59 +128,153 @@ def load_resized_images(folder_or_list, resize_mode="fixed_mapping", size=None, 
                 print(f"Warning: Could not load {path}: {e}")
             return None
 
+    loaded = [im for im in pool.map(decode, paths) if im is not None]
+    if not loaded:
+        raise ValueError("No valid images found")
+    target = target_size_for([im.size[0] / im.size[1] for im in loaded], resize_mode, size, patch_size,
+                             resolution_set)
+    if verbose:
+        print(f"Using target resolution {target[0]}x{target[1]} (W x H) for all images")
+    return loaded, target
+
+
+def load_resized_images(folder_or_list, resize_mode="fixed_mapping", size=None, norm_type="dinov2", patch_size=14,
+                        verbose=False, bayer_format=False, resolution_set=518, stride=1, num_workers=None):
+    """Host part of load_images (image.py:163-303) on PIL: decode, choose the common target size, Lanczos / bicubic
+    resize + crop.  Returns the resized PIL images (the host reference of the GPU resize)."""
+    n_hint = len(folder_or_list) if isinstance(folder_or_list, list) else None
     # PIL decodes and resamples with the GIL released: a thread pool keeps every host core busy (file order kept)
-    with ThreadPoolExecutor(max_workers=_workers(num_workers, len(paths))) as pool:
-        loaded = [im for im in pool.map(decode, paths) if im is not None]
-        if not loaded:
-            raise ValueError("No valid images found")
-        target = target_size_for([im.size[0] / im.size[1] for im in loaded], resize_mode, size, patch_size,
-                                 resolution_set)
-        if verbose:
-            print(f"Using target resolution {target[0]}x{target[1]} (W x H) for all images")
+    with ThreadPoolExecutor(max_workers=_workers(num_workers, n_hint)) as pool:
+        loaded, target = _decode_scene(folder_or_list, resize_mode, size, norm_type, patch_size, verbose,
+                                       bayer_format, resolution_set, stride, pool)
         return list(pool.map(lambda im: crop_resize_if_necessary(im, resolution=target)[0], loaded))
+
+
+def resize_geometry(in_wh, target_wh):
+    """rescale_image_and_other_optional_info + the centred crop of crop_resize_if_necessary without intrinsics
+    (cropping.py:188-280 / 385-465, numpy float64 like the reference): (resized (w, h), PIL filter, crop (left, top))."""
+    input_resolution = np.array(in_wh)
+    output_resolution = np.array(target_wh)
+    scale_final = max(output_resolution / input_resolution) + 1e-8
+    rs = np.floor(input_resolution * scale_final).astype(int)
+    filt = nat.RESAMPLE_LANCZOS if scale_final < 1 else nat.RESAMPLE_BICUBIC
+    w, h = int(rs[0]), int(rs[1])
+    return (w, h), filt, ((w - int(target_wh[0])) // 2, (h - int(target_wh[1])) // 2)
+
+
+class _DecodedScene:
+    """Host stage of the GPU-resize loader: decoded uint8 images in pinned memory + their fixed-point resize plans
+    (one pinned int32 blob), ready for one H2D copy each and the resize kernels."""
+
+    def __init__(self, images, target, plans, offsets):
+        self.images, self.target, self.plans, self.offsets = images, target, plans, offsets
+
+
+def _decode_scene_for_gpu(folder_or_list, resize_mode="fixed_mapping", size=None, norm_type="dinov2", patch_size=14,
+                          verbose=False, bayer_format=False, resolution_set=518, stride=1, num_workers=None):
+    n_hint = len(folder_or_list) if isinstance(folder_or_list, list) else None
+    with ThreadPoolExecutor(max_workers=_workers(num_workers, n_hint)) as pool:
+        loaded, target = _decode_scene(folder_or_list, resize_mode, size, norm_type, patch_size, verbose,
+                                       bayer_format, resolution_set, stride, pool)
+        pin = torch.cuda.is_available()  # (the host stage alone also runs on a CPU-only machine: tests)
+
+        def host_copy(im):  # the RGB bytes into pinned host memory, on the pool's threads
+            t = torch.empty((im.size[1], im.size[0], 3), dtype=torch.uint8, pin_memory=pin)
+            np.copyto(t.numpy(), np.asarray(im, dtype=np.uint8))
+            return t
+        pinned = list(pool.map(host_copy, loaded))
+    blobs, offsets, off = [], [], 0
+    for im in loaded:
+        (rw, rh), filt, (left, top) = resize_geometry(im.size, target)
+        b = nat.resize_plan(im.size[0], im.size[1], rw, rh, left, top, int(target[0]), int(target[1]), filt)
+        blobs.append(b)
+        offsets.append(off)
+        off += (b.size + 63) // 64 * 64  # 256-B aligned plans
+    plans = torch.zeros(off, dtype=torch.int32, pin_memory=pin)
+    pn = plans.numpy()
+    for b, o in zip(blobs, offsets):
+        pn[o:o + b.size] = b
+    return _DecodedScene(list(zip(pinned, blobs)), target, plans, offsets)
+
+
+def _resize_on_gpu(scene: _DecodedScene, norm_type, device):
+    """Device stage: H2D of the pinned images + plans (stream-ordered), PIL-exact resize + crop + normalise
+    (mapa_resize_normalize) into one (n, 3, H, W) float32 batch."""
+    mean, std = _norm_consts(norm_type)
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    tw, th = int(scene.target[0]), int(scene.target[1])
+    with torch.cuda.device(dev):
+        plans = scene.plans.to(dev, non_blocking=True)
+        ws_bytes = max(nat.resize_workspace_bytes(b) for _, b in scene.images)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        out = torch.empty(len(scene.images), 3, th, tw, dtype=torch.float32, device=dev)
+        for i, ((src, blob), off) in enumerate(zip(scene.images, scene.offsets)):
+            d = src.to(dev, non_blocking=True)
+            nat.resize_normalize(d, d.shape[1] * 3, blob, plans[off:], mean, std, out=out[i], workspace=ws)
+    return out
+
+
+def _views(imgs, shapes, norm_type):
+    return [dict(img=imgs[i:i + 1], true_shape=np.int32([shapes[i]]), idx=i, instance=str(i),
+                 data_norm_type=[norm_type]) for i in range(imgs.shape[0])]
 
 
 def _workers(num_workers, n):
     if num_workers is None:
         num_workers = min(16, os.cpu_count() or 1)
-    return max(1, min(int(num_workers), max(n, 1)))
+    return max(1, min(int(num_workers), max(n or num_workers, 1)))
+
+
+def _host_stage(folder_or_list, gpu_resize, **kw):
+    if gpu_resize:
+        return _decode_scene_for_gpu(folder_or_list, **kw)
+    return load_resized_images(folder_or_list, **kw)
+
+
+def _device_stage(host, norm_type, device):
+    if isinstance(host, _DecodedScene):
+        imgs = _resize_on_gpu(host, norm_type, device)
+        return _views(imgs, [(int(host.target[1]), int(host.target[0]))] * imgs.shape[0], norm_type)
+    imgs = normalize_images(host, norm_type, device)
+    return _views(imgs, [im.size[::-1] for im in host], norm_type)
 
 
 def load_images(folder_or_list, resize_mode="fixed_mapping", size=None, norm_type="dinov2", patch_size=14,
-                verbose=False, bayer_format=False, resolution_set=518, stride=1, device=None, num_workers=None):
+                verbose=False, bayer_format=False, resolution_set=518, stride=1, device=None, num_workers=None,
+                gpu_resize=True):
     """image.py:134-333: open every image of a folder (sorted) or list, resize + crop all to one target size from
-    their mean aspect ratio, normalise (GPU).  Returns [{img (1,3,H,W), true_shape, idx, instance,
-    data_norm_type}] with img on `device` (default: the current GPU)."""
-    resized = load_resized_images(folder_or_list, resize_mode, size, norm_type, patch_size, verbose, bayer_format,
-                                  resolution_set, stride, num_workers)
-    imgs = normalize_images(resized, norm_type, device)
-    return [dict(img=imgs[i:i + 1], true_shape=np.int32([resized[i].size[::-1]]), idx=i, instance=str(i),
-                 data_norm_type=[norm_type]) for i in range(len(resized))]
+    their mean aspect ratio, normalise.  Returns [{img (1,3,H,W), true_shape, idx, instance, data_norm_type}] with
+    img on `device` (default: the current GPU).
+
+    gpu_resize=True (default): the host only decodes (PIL, thread pool); the Lanczos / bicubic resize, the crop and
+    ToTensor + Normalize run on the GPU (mapa_resize_normalize, bit-identical with PIL's Image.resize).
+    gpu_resize=False: PIL resizes on the host (load_resized_images), the GPU only normalises."""
+    kw = dict(resize_mode=resize_mode, size=size, norm_type=norm_type, patch_size=patch_size, verbose=verbose,
+              bayer_format=bayer_format, resolution_set=resolution_set, stride=stride, num_workers=num_workers)
+    return _device_stage(_host_stage(folder_or_list, gpu_resize, **kw), norm_type, device)
 
 
 def iter_load_images(scenes, prefetch=1, **kwargs):
     """Yield load_images(scene, **kwargs) for every scene (a folder or a file list) in order, with the host part of
-    the next `prefetch` scenes (decode + Lanczos / bicubic resize + crop: load_resized_images, PIL on host threads,
-    GIL released) running while the caller works on the current one — so a stream of scenes fed to
-    MapAnything.infer keeps the GPU busy instead of alternating host decode and GPU inference.  Each scene's uint8
-    images go to the GPU and are normalised when the scene is yielded (stream-ordered behind the previous scene's
-    work).  Results are exactly load_images' (the same functions, only overlapped)."""
+    the next `prefetch` scenes (decode, plus the PIL resize when gpu_resize=False; PIL on host threads, GIL
+    released) running while the caller works on the current one — so a stream of scenes fed to MapAnything.infer
+    keeps the GPU busy instead of alternating host decode and GPU inference.  Each scene's images go to the GPU and
+    are resized / normalised when the scene is yielded (stream-ordered behind the previous scene's work).  Results
+    are exactly load_images' (the same functions, only overlapped)."""
     from concurrent.futures import ThreadPoolExecutor as _TPE
 
     scenes = list(scenes)
     device = kwargs.pop("device", None)
+    gpu_resize = kwargs.pop("gpu_resize", True)
     norm_type = kwargs.get("norm_type", "dinov2")
-    host_kw = {k: v for k, v in kwargs.items() if k != "device"}
     prefetch = max(1, int(prefetch))
     with _TPE(max_workers=prefetch) as ahead:
-        pending = [ahead.submit(load_resized_images, sc, **host_kw) for sc in scenes[:prefetch]]
+        pending = [ahead.submit(_host_stage, sc, gpu_resize, **kwargs) for sc in scenes[:prefetch]]
         for k in range(len(scenes)):
-            resized = pending.pop(0).result()
+            host = pending.pop(0).result()
             if k + prefetch < len(scenes):
-                pending.append(ahead.submit(load_resized_images, scenes[k + prefetch], **host_kw))
-            imgs = normalize_images(resized, norm_type, device)
-            yield [dict(img=imgs[i:i + 1], true_shape=np.int32([resized[i].size[::-1]]), idx=i, instance=str(i),
-                        data_norm_type=[norm_type]) for i in range(len(resized))]
+                pending.append(ahead.submit(_host_stage, scenes[k + prefetch], gpu_resize, **kwargs))
+            yield _device_stage(host, norm_type, device)
 
 
 def _to_pil(img, view_idx):

@@ -128,12 +128,13 @@ def test_argument_errors_like_reference(files):
 
 # ------------------------------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
+@pytest.mark.parametrize("gpu_resize", [True, False], ids=["gpu_resize", "pil_resize"])
 @pytest.mark.parametrize("case", list(CASES))
-def test_load_images_matches_reference(fx, files, case):
+def test_load_images_matches_reference(fx, files, case, gpu_resize):
     from mapanything.utils.image import load_images
 
     d, names = files
-    res = load_images(_source(case, d, names), **CASES[case])
+    res = load_images(_source(case, d, names), gpu_resize=gpu_resize, **CASES[case])
     step = int(fx[f"{case}__step"])
     imgs = torch.cat([r["img"] for r in res], 0)
     assert imgs.is_cuda and imgs.dtype == torch.float32
@@ -153,10 +154,10 @@ def test_iter_load_images_prefetch_matches_load_images(fx, files):
     scenes = [_source(c, d, names) for c in CASES]
     kws = [CASES[c] for c in CASES]
     # one keyword set per stream: the iterator takes the same arguments as load_images
-    for prefetch in (1, 2):
-        for sc, kw, c, got in zip(scenes, kws, CASES, (next(iter_load_images([s], prefetch=prefetch, **k))
+    for prefetch, gr in ((1, True), (2, True), (1, False)):
+        for sc, kw, c, got in zip(scenes, kws, CASES, (next(iter_load_images([s], prefetch=prefetch, gpu_resize=gr, **k))
                                                        for s, k in zip(scenes, kws))):
-            ref = load_images(sc, **kw)
+            ref = load_images(sc, gpu_resize=gr, **kw)
             assert len(got) == len(ref)
             for a, b in zip(got, ref):
                 assert torch.equal(a["img"], b["img"]) and np.array_equal(a["true_shape"], b["true_shape"])
@@ -192,3 +193,20 @@ def test_preprocess_inputs_ray_directions_recover_intrinsics():
                           size=(224, 168))
     np.testing.assert_allclose(a[0]["intrinsics"].numpy(), b[0]["intrinsics"].numpy(), rtol=1e-4, atol=1e-3)
     assert torch.equal(a[0]["img"], b[0]["img"])
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_gpu_resize_host_stage_matches_pil(files, case):
+    """Host stage of the GPU-resize loader (decode + resize_geometry + the fixed-point plans), run through the
+    kernels' integer arithmetic in numpy (test_resample_plan.passes), equals the PIL path image for image."""
+    from mapanything.utils.image import _decode_scene_for_gpu, load_resized_images
+    from test_resample_plan import passes
+
+    d, names = files
+    kw = {k: v for k, v in CASES[case].items()}
+    ref = load_resized_images(_source(case, d, names), **kw)
+    scene = _decode_scene_for_gpu(_source(case, d, names), **kw)
+    assert len(scene.images) == len(ref)
+    for (src, blob), im in zip(scene.images, ref):
+        got = passes(src.numpy(), blob)
+        assert tuple(scene.target) == im.size and np.array_equal(got, np.asarray(im))
