@@ -205,15 +205,20 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *   MAPA_TUNE_PERS (default 1, or the environment's MAPA_GEMM_PERS): the dense 16-bit linears with a transformer
  *     epilogue (act -> 16-bit output, or the in-place fp32 residual update) and no ln_out run on the persistent
  *     register-epilogue kernel; 1 = its automatic tile shape, 2..5 = tile shape 0..3 (256x128, 192x256, 256x256,
- *     192x128), 0 = off (the data-parallel tile kernels).  Variants 2600..2603 force a shape.
+ *     192x128), 0 = off (the data-parallel tile kernels).  Variants 2600..2608 force a shape (4..6: diagnostics;
+ *     7, 8: 4-wave 192x128 / 256x128 forms, measured slower).
  *   MAPA_TUNE_PERS_LN (default 0, or the environment's MAPA_GEMM_PERS_LN): 1 = ln_out requests that the LayerNorm-
  *     fused kernel takes run on the persistent register-epilogue form (192x128 tiles, 2 per CU, whole 192-row bands
  *     per round, all co-resident); 0 = the 192-row LNF tile kernel (measured faster on the path shapes).
+ *   MAPA_TUNE_PERS_STAGGER (default -1 = automatic, or the environment's MAPA_GEMM_STAGGER): the persistent kernel's
+ *     workgroups that get one tile fewer start `value` 100-MHz ticks (10 ns) late, so the chip's epilogue store bursts
+ *     do not coincide (0 = off, up to 100000); automatic = half a tile's time where those workgroups are < 35 % of
+ *     the grid, else none.  Results are bitwise the same either way.
  *   MAPA_TUNE_DIAG_GRID (timing diagnostic, default 0): the data-parallel 256-row / 192-row tile kernels launch only
  *     their first `value` workgroups (0 = every tile); outputs of the other tiles are left unwritten. */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,
        MAPA_TUNE_LN_FUSE = 4, MAPA_TUNE_LN_SPIN = 5, MAPA_TUNE_LN_TEST_SKIP = 6, MAPA_TUNE_DIAG_GRID = 7,
-       MAPA_TUNE_PERS = 8, MAPA_TUNE_PERS_LN = 9 };
+       MAPA_TUNE_PERS = 8, MAPA_TUNE_PERS_LN = 9, MAPA_TUNE_PERS_STAGGER = 10 };
 int mapa_gemm_tune(int key, int value);
 
 /* ---------------------------------------------------------------------------------------------------------

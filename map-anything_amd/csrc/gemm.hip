@@ -484,6 +484,7 @@ static int gemm_args(const mapa_gemm_desc* d, GemmArgs& a) {
   }
   a.ln_w = d->ln_w; a.ln_b = d->ln_b; a.ln_eps = d->ln_eps; a.ln_out = d->ln_out; a.ln_ldo = d->ln_ldo;
   a.ln_ctr = nullptr; a.ln_stats = nullptr;
+  a.stagger = 0;
   MAPA_CHECK_ARG(a.vec_ok || d->out_mode == MAPA_OUT_ROWMAJOR, "mapa_gemm: pixel shuffle needs N %% 4 == 0");
   return 0;
 }
@@ -516,7 +517,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
     MAPA_CHECK_LAUNCH("mapa_gemm (LayerNorm fused)");
     return 0;  // launched (residual linear + the LayerNorm of its output rows)
   }
-  const bool pers_forced = forced >= 2600 && forced <= 2606;
+  const bool pers_forced = forced >= 2600 && forced <= 2608;
   const bool pers_auto = !forced && pers_mode() && !sk && ((variant >= 2560 && variant <= 2574) || variant == 2587);
   if (flat && launch_conv_halo_flat(a, flat, d->workspace, d->workspace_bytes, GEMM_TICKET_BYTES, stream)) {
     // launched (flat-raster halo conv, split K)
@@ -577,7 +578,7 @@ extern "C" int mapa_gemm_tune(int key, int value) {
   MAPA_CHECK_ARG(key == MAPA_TUNE_CONV_HALO || key == MAPA_TUNE_TAIL_STREAMK || key == MAPA_TUNE_HALO_SPLIT ||
                      key == MAPA_TUNE_TILE_GROUP || key == MAPA_TUNE_LN_FUSE || key == MAPA_TUNE_LN_SPIN ||
                      key == MAPA_TUNE_LN_TEST_SKIP || key == MAPA_TUNE_DIAG_GRID || key == MAPA_TUNE_PERS ||
-                     key == MAPA_TUNE_PERS_LN,
+                     key == MAPA_TUNE_PERS_LN || key == MAPA_TUNE_PERS_STAGGER,
                  "mapa_gemm_tune: unknown key %d", key);
   MAPA_CHECK_ARG((key != MAPA_TUNE_LN_SPIN && key != MAPA_TUNE_LN_TEST_SKIP) || value >= 0,
                  "mapa_gemm_tune: negative value %d", value);
@@ -587,6 +588,11 @@ extern "C" int mapa_gemm_tune(int key, int value) {
   }
   if (key == MAPA_TUNE_LN_TEST_SKIP) {
     ln_arm_test_skip(value);
+    return 0;
+  }
+  if (key == MAPA_TUNE_PERS_STAGGER) {
+    MAPA_CHECK_ARG(value >= -1 && value <= 100000, "mapa_gemm_tune: stagger %d", value);
+    pers_set_stagger(value);
     return 0;
   }
   if (key == MAPA_TUNE_PERS_LN) {
@@ -617,7 +623,7 @@ extern "C" int mapa_gemm_set_variant(int variant) {
   MAPA_CHECK_ARG(variant == 0 || variant == 643 || variant == 644 || variant == 1282 || variant == 1283 ||
                      (variant >= 2560 && variant <= 2574) || (variant >= 2580 && variant <= 2582) ||
                      (variant >= 2584 && variant <= 2589) || (variant >= 2591 && variant <= 2596) ||
-                     (variant >= 2600 && variant <= 2606),
+                     (variant >= 2600 && variant <= 2608),
                  "mapa_gemm_set_variant: unknown variant %d", variant);
   g_forced = variant;
   return 0;

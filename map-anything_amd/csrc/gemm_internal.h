@@ -47,6 +47,7 @@ struct GemmArgs {
   unsigned ln_spin;              // bounded wait: polls before the band barrier gives up and raises the fault word
   int ln_skip;                   // test hook: tile (band 0, column 0) skips its publish (mapa_gemm_tune LN_TEST_SKIP)
   unsigned* fault;               // the library's device fault word (f16 split outputs out of binary16 range)
+  int stagger;                   // gemm_pers_kernel: 100-MHz ticks the workgroups with one tile fewer start late
 };
 
 // Device address of the library's fault word on the current device (gemm_big.hip; other translation units pass it
@@ -414,6 +415,7 @@ void diag_set_grid(int blocks);  // timing diagnostic: launch only the first `bl
 // epilogue does not qualify.
 bool launch_gemm_pers(const GemmArgs& a, int shape, int cus, hipStream_t stream);
 int pers_pick_shape(int M, int N, int K, int cus);
+void pers_set_stagger(int ticks);  // MAPA_TUNE_PERS_STAGGER (100-MHz ticks, 0 = off)
 
 // The in-place residual linear (epi_mode 2: out_f32 = resid1 + gamma * (acc + bias)) with the LayerNorm of its output
 // rows fused (gemm_big.hip, LNF): the row statistics combine across a band's column tiles inside the launch (band

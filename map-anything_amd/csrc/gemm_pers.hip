@@ -18,6 +18,8 @@
 //    (e.g. 1032 tiles on 512 slots) is traded for a fuller one.
 // Main loop as gemm_big's: LDS-DMA (global_load_lds_dwordx4) into a ring of K tiles with the 16-B chunk XOR swizzle
 // on the source address, conflict-free ds_read_b128 fragments, counted vmcnt + raw s_barrier, 16x16x32 MFMA.
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "gemm_internal.h"
@@ -30,9 +32,9 @@ constexpr int LN_MAX_NTN_P = 8;  // column tiles per band the LayerNorm merge ho
                                  // workspace layout for both LayerNorm-fused kernels)
 typedef unsigned int u32x4p __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int RB, int WM>
+template <int BM, int BN, int RB, int WM, int NW = 8>
 struct PCfg {
-  static constexpr int WN = 8 / WM;
+  static constexpr int WN = NW / WM;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
   static constexpr int CPR = RB / 16;  // 16-B chunks per LDS row
@@ -40,8 +42,8 @@ struct PCfg {
   static constexpr int KG = CPR / 4;   // 32-deep MFMA k-groups per tile
   static constexpr int RPI = 1024 / RB;
   static constexpr int A_BYTES = BM * RB, B_BYTES = BN * RB, STAGE = A_BYTES + B_BYTES;
-  static constexpr int NLA = BM / (8 * RPI), NLB = BN / (8 * RPI);
-  static_assert(BM % (8 * RPI) == 0 && BN % (8 * RPI) == 0, "whole 1-KiB wave instructions per operand");
+  static constexpr int NLA = BM / (NW * RPI), NLB = BN / (NW * RPI);
+  static_assert(BM % (NW * RPI) == 0 && BN % (NW * RPI) == 0, "whole 1-KiB wave instructions per operand");
   static_assert(TM % 16 == 0 && TN % 16 == 0, "16x16 MFMA tiles");
 };
 
@@ -54,9 +56,9 @@ __device__ __forceinline__ int pswz(int row) {
 // Per-tile staging state: the per-lane source rows (clamped past M / N; their results are never stored).  TAG makes
 // every kernel instantiation use a Src type of its own: with two kernels sharing one Src instantiation, hipcc (ROCm
 // 7.2) emitted the host-side launch stubs of the first kernel only (the others' stayed undefined at link time).
-template <int BM, int BN, int RB, int WM, int TAG>
+template <int BM, int BN, int RB, int WM, int TAG, int NW = 8>
 struct Src {
-  using C = PCfg<BM, BN, RB, WM>;
+  using C = PCfg<BM, BN, RB, WM, NW>;
   const char* a[C::NLA];
   const char* w[C::NLB];
   int asc[C::NLA], wsc[C::NLB];
@@ -64,14 +66,14 @@ struct Src {
     const int lrow = lane / C::CPR, pos = lane % C::CPR;
 #pragma unroll
     for (int i = 0; i < C::NLA; ++i) {
-      const int r = (i * 8 + wave) * C::RPI + lrow;
+      const int r = (i * NW + wave) * C::RPI + lrow;
       asc[i] = pos ^ pswz<RB>(r);
       const int m = min(bm + r, p.M - 1);
       a[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + asc[i] * 8) * 2;
     }
 #pragma unroll
     for (int i = 0; i < C::NLB; ++i) {
-      const int r = (i * 8 + wave) * C::RPI + lrow;
+      const int r = (i * NW + wave) * C::RPI + lrow;
       wsc[i] = pos ^ pswz<RB>(r);
       const int n = min(bn + r, p.N - 1);
       w[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + wsc[i] * 8) * 2;
@@ -86,12 +88,12 @@ struct Src {
 #pragma unroll
     for (int i = 0; i < C::NLA; ++i) {
       const bool kin = k_exact || kt * C::BK + asc[i] * 8 < p.K;
-      __builtin_amdgcn_global_load_lds(kin ? a[i] + koff : zero, As + lds_wave + i * 8192, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(kin ? a[i] + koff : zero, As + lds_wave + i * NW * 1024, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < C::NLB; ++i) {
       const bool kin = k_exact || kt * C::BK + wsc[i] * 8 < p.K;
-      __builtin_amdgcn_global_load_lds(kin ? w[i] + koff : zero, Bs + lds_wave + i * 8192, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(kin ? w[i] + koff : zero, Bs + lds_wave + i * NW * 1024, 16, 0, 0);
     }
   }
 };
@@ -187,9 +189,10 @@ __device__ __forceinline__ void pers_epilogue(const GemmArgs& p, const f32x4 (&a
 }
 
 // PRIO: s_setprio 1 around each tile's MFMA burst.  DIAG (timing diagnostic, wrong results): 1 = no epilogue.
-template <int MODE, int BM, int BN, int RB, int WM, int STAGES, int MINB, bool F16, int PRIO = 0, int DIAG = 0>
-__global__ void __launch_bounds__(PTHREADS, MINB) gemm_pers_kernel(GemmArgs p) {
-  using C = PCfg<BM, BN, RB, WM>;
+template <int MODE, int BM, int BN, int RB, int WM, int STAGES, int MINB, bool F16, int PRIO = 0, int DIAG = 0,
+          int NW = 8>
+__global__ void __launch_bounds__(NW * 64, MINB) gemm_pers_kernel(GemmArgs p) {
+  using C = PCfg<BM, BN, RB, WM, NW>;
   constexpr int NPT = C::NLA + C::NLB;
   __shared__ __attribute__((aligned(1024))) char lds[STAGES * C::STAGE];
 
@@ -221,11 +224,21 @@ __global__ void __launch_bounds__(PTHREADS, MINB) gemm_pers_kernel(GemmArgs p) {
 
   int r = 0, tm, tn;
   if (!mapa_idx::pers_tile(blockIdx.x, G, r, tiles, p.tile_gm, ntm, ntn, tm, tn)) return;
-  Src<BM, BN, RB, WM, MODE * 2 + (F16 ? 1 : 0) + 4 * PRIO + 8 * DIAG> src;
+  Src<BM, BN, RB, WM, MODE * 2 + (F16 ? 1 : 0) + 4 * PRIO + 8 * DIAG + 32 * NW, NW> src;
   src.setup(p, tm * BM, tn * BN, wave, lane);
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, k_exact);
+  // Stagger: the workgroups with one tile fewer (no tile in the last, partial round) start p.stagger ticks late, so
+  // their tile boundaries fall mid-tile of the others' and the chip's epilogue store bursts no longer coincide; they
+  // still finish before the full-length workgroups as long as the delay is under one tile time.
+  if (p.stagger > 0) {
+    const int rem = tiles % G;
+    if (rem && (int)blockIdx.x >= rem) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)p.stagger) __builtin_amdgcn_s_sleep(8);
+    }
+  }
 
   f32x4 acc[C::FM][C::FN];
   for (;;) {
@@ -546,12 +559,31 @@ __global__ void __launch_bounds__(PTHREADS, MINB) gemm_pers_ln_kernel(GemmArgs p
 // Shapes: 0 = 256x128 (64-B rows, 3 stages, 2 workgroups / CU), 1 = 192x256 (128-B rows, 2 stages, 1 / CU),
 // 2 = 256x256 (128-B rows, 2 stages, 1 / CU), 3 = 192x128 (128-B rows, 2 stages, 2 / CU); 4 = 3 with s_setprio
 // around the MFMA bursts; 5 / 6 = 3 / 0 without the epilogue (timing diagnostics, wrong results).
-static void pers_shape(int s, int& bm, int& bn, int& per_cu) {
-  static const int BMs[7] = {256, 192, 256, 192, 192, 192, 256}, BNs[7] = {128, 256, 256, 128, 128, 128, 128},
-                   PCs[7] = {2, 1, 1, 2, 2, 2, 2};
+static void pers_shape(int s, int& bm, int& bn, int& per_cu, int& nw) {
+  static const int BMs[9] = {256, 192, 256, 192, 192, 192, 256, 192, 256},
+                   BNs[9] = {128, 256, 256, 128, 128, 128, 128, 128, 128}, PCs[9] = {2, 1, 1, 2, 2, 2, 2, 2, 2},
+                   NWs[9] = {8, 8, 8, 8, 8, 8, 8, 4, 4};
   bm = BMs[s];
   bn = BNs[s];
   per_cu = PCs[s];
+  nw = NWs[s];
+}
+
+// Start delay of the workgroups with one tile fewer (gemm_pers_kernel): mapa_gemm_tune(MAPA_TUNE_PERS_STAGGER, .) /
+// env MAPA_GEMM_STAGGER = 100-MHz ticks, 0 = off, -1 = automatic (pers_auto_stagger); -2: env not read yet.
+static int g_pers_stagger = -2;
+
+// Automatic stagger: half a tile's time (2 BM BN K flop at ~1.65 TFLOP/s per resident workgroup, the path rate) where
+// the short workgroups are a minority (< 35 % of the grid): then they still finish first, and the chip's epilogue
+// bursts split into two half-size ones that fall mid-tile of the other group.  Measured (tools/stagger_ab.py,
+// profiles/r6/stagger_ab.json, 192x128 tiles): enc.qkv 81.3 -> 78.2 us at 1500 ticks, enc.fc1 111.6 -> 109.5;
+// aat.fc1 neutral; where most workgroups are short (aat.qkv: 492 of 512) any delay only adds to the kernel
+// (49.1 -> 52.1 us at 500 ticks), so none is applied there.  Bitwise-neutral: the same tiles, the same K order.
+static int pers_auto_stagger(int64_t tiles, int G, int bm, int bn, int K) {
+  const int64_t rem = tiles % G;
+  if (rem == 0 || tiles < G || (G - rem) * 100 >= 35 * (int64_t)G) return 0;
+  const double tile_us = 2.0 * bm * bn * (double)K / 1.65e6;
+  return (int)(0.5 * tile_us * 100.0);  // 100 ticks per microsecond
 }
 
 int pers_pick_shape(int M, int N, int K, int cus) {
@@ -571,6 +603,10 @@ static GemmKernel pers_kernel_diag(int s) {  // bf16, act -> 16-bit epilogue onl
     case 4: return gemm_pers_kernel<1, 192, 128, 128, 4, 2, 2, false, 1>;
     case 5: return gemm_pers_kernel<1, 192, 128, 128, 4, 2, 2, false, 0, 1>;
     case 6: return gemm_pers_kernel<1, 256, 128, 64, 4, 3, 2, false, 0, 1>;
+    // 4-wave workgroups (2 waves / SIMD at 2 per CU, 256 VGPRs): 192x128 as 2x2 waves of 96x64; 256x128 in 32-deep K
+    // tiles, 3 stages, 2x2 waves of 128x64
+    case 7: return gemm_pers_kernel<1, 192, 128, 128, 2, 2, 2, false, 0, 0, 4>;
+    case 8: return gemm_pers_kernel<1, 256, 128, 64, 2, 3, 2, false, 0, 0, 4>;
     default: return nullptr;
   }
 }
@@ -607,16 +643,21 @@ bool launch_gemm_pers(const GemmArgs& a, int shape, int cus, hipStream_t stream)
     if (mode != 1) return false;  // the residual pattern: the tile kernels measured as fast or faster (pers_ab)
     shape = pers_pick_shape(a.M, a.N, a.K, cus);
   }
-  if (shape > 6) return false;
-  int bm, bn, pc;
-  pers_shape(shape, bm, bn, pc);
+  if (shape > 8) return false;
+  int bm, bn, pc, nw;
+  pers_shape(shape, bm, bn, pc, nw);
   const int64_t tiles = (int64_t)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
   const int G = (int)std::min<int64_t>(tiles, (int64_t)cus * pc);
   const GemmKernel k = pers_kernel(mode, a.lp_f16 != 0, shape);
   if (!k) return false;
-  hipLaunchKernelGGL(k, dim3(G), dim3(PTHREADS), 0, stream, a);
+  GemmArgs b = a;
+  if (g_pers_stagger == -2) g_pers_stagger = getenv("MAPA_GEMM_STAGGER") ? atoi(getenv("MAPA_GEMM_STAGGER")) : -1;
+  b.stagger = g_pers_stagger >= 0 ? g_pers_stagger : pers_auto_stagger(tiles, G, bm, bn, a.K);
+  hipLaunchKernelGGL(k, dim3(G), dim3(nw * 64), 0, stream, b);
   return true;
 }
+
+void pers_set_stagger(int ticks) { g_pers_stagger = ticks >= 0 ? ticks : -1; }
 
 // The LayerNorm-fused residual linear on 192x128 tiles, 2 workgroups per CU (gemm_pers_ln_kernel): N = 768 or 1024
 // (6 / 8 column tiles per band), bf16, the in-place residual pattern.  Workspace as launch_gemm_big_ln (the GEMM

@@ -488,7 +488,7 @@ def attention_workspace(d) -> torch.Tensor:
 
 
 TUNE_CONV_HALO, TUNE_TAIL_STREAMK, TUNE_HALO_SPLIT, TUNE_TILE_GROUP, TUNE_LN_FUSE = 0, 1, 2, 3, 4
-TUNE_LN_SPIN, TUNE_LN_TEST_SKIP, TUNE_DIAG_GRID, TUNE_PERS, TUNE_PERS_LN = 5, 6, 7, 8, 9
+TUNE_LN_SPIN, TUNE_LN_TEST_SKIP, TUNE_DIAG_GRID, TUNE_PERS, TUNE_PERS_LN, TUNE_PERS_STAGGER = 5, 6, 7, 8, 9, 10
 
 
 def gemm_tune(key: int, value: int):
