@@ -15,7 +15,8 @@ from mapanything import _native as nat  # noqa: E402
 V, T = 8, 1369
 R, L = V * (T + 1), V * T + 1
 SHAPES = [("enc.qkv", R, 3072, 1024, "plain"), ("enc.fc1", R, 4096, 1024, "gelu"), ("aat.qkv", L, 2304, 768, "plain"),
-          ("aat.fc1", L, 3072, 768, "gelu"), ("enc.fc2", R, 1024, 4096, "resid"), ("aat.fc2", L, 768, 3072, "resid")]
+          ("aat.fc1", L, 3072, 768, "gelu"), ("enc.fc2", R, 1024, 4096, "resid"), ("aat.fc2", L, 768, 3072, "resid"),
+          ("enc.proj", R, 1024, 1024, "resid"), ("aat.proj", L, 768, 768, "resid")]
 if os.environ.get("SA_ONLY"):
     SHAPES = [s for s in SHAPES if s[0] in os.environ["SA_ONLY"].split(",")]
 
