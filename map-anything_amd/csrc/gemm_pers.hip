@@ -59,44 +59,82 @@ __device__ __forceinline__ int pswz(int row) {
 template <int BM, int BN, int RB, int WM, int TAG, int NW = 8>
 struct Src {
   using C = PCfg<BM, BN, RB, WM, NW>;
-  const char* a[C::NLA];
-  const char* w[C::NLB];
-  int asc[C::NLA], wsc[C::NLB];
+  // per-lane byte offsets of this lane's source rows from A / W (rows clamped to M-1 / N-1); the K offset of a tile
+  // rides in the buffer load's soffset, so no 64-bit per-lane pointer lives across the K loop (fast path: K a
+  // multiple of BK and both operands under 2 GiB — the path's linears; otherwise the zero-page form below)
+  uint32_t ao[C::NLA], wo[C::NLB];
   __device__ __forceinline__ void setup(const GemmArgs& p, int bm, int bn, int wave, int lane) {
     const int lrow = lane / C::CPR, pos = lane % C::CPR;
 #pragma unroll
     for (int i = 0; i < C::NLA; ++i) {
       const int r = (i * NW + wave) * C::RPI + lrow;
-      asc[i] = pos ^ pswz<RB>(r);
       const int m = min(bm + r, p.M - 1);
-      a[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + asc[i] * 8) * 2;
+      ao[i] = (uint32_t)(((int64_t)m * p.lda + (pos ^ pswz<RB>(r)) * 8) * 2);
     }
 #pragma unroll
     for (int i = 0; i < C::NLB; ++i) {
       const int r = (i * NW + wave) * C::RPI + lrow;
-      wsc[i] = pos ^ pswz<RB>(r);
       const int n = min(bn + r, p.N - 1);
-      w[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + wsc[i] * 8) * 2;
+      wo[i] = (uint32_t)(((int64_t)n * p.ldw + (pos ^ pswz<RB>(r)) * 8) * 2);
     }
   }
   // LDS-DMA of K tile kt into ring slot `slot`
-  __device__ __forceinline__ void stage(const GemmArgs& p, char* lds, int slot, int kt, int lds_wave, bool k_exact) const {
-    const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  __device__ __forceinline__ void stage(const GemmArgs& p, char* lds, int slot, int kt, int lds_wave, bool fast,
+                                        int wave, int lane) const {
     char* As = lds + slot * C::STAGE;
     char* Bs = As + C::A_BYTES;
+    typedef __attribute__((address_space(3))) void* lds_ptr_t;
+    if (fast) {
+      const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, 0x7fffffff, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, 0x7fffffff, 0x00020000);
+      const int koff = kt * C::BK * 2;
+#pragma unroll
+      for (int i = 0; i < C::NLA; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(As + lds_wave + i * NW * 1024), 16, (int)ao[i], koff,
+                                                 0, 0);
+#pragma unroll
+      for (int i = 0; i < C::NLB; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(Bs + lds_wave + i * NW * 1024), 16, (int)wo[i], koff,
+                                                 0, 0);
+      return;
+    }
+    // K-tail form: the same offsets as plain pointers, the chunks past K from the zero page (the empty asm hides the
+    // offsets' loop invariance, so no 64-bit pointer per piece is hoisted into registers across the K loop)
+    const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+    const int lrow = lane / C::CPR, pos = lane % C::CPR;
     const int64_t koff = (int64_t)kt * C::BK * 2;
 #pragma unroll
     for (int i = 0; i < C::NLA; ++i) {
-      const bool kin = k_exact || kt * C::BK + asc[i] * 8 < p.K;
-      __builtin_amdgcn_global_load_lds(kin ? a[i] + koff : zero, As + lds_wave + i * NW * 1024, 16, 0, 0);
+      const int r = (i * NW + wave) * C::RPI + lrow;
+      const bool kin = kt * C::BK + (pos ^ pswz<RB>(r)) * 8 < p.K;
+      uint32_t off = ao[i];
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds(kin ? reinterpret_cast<const char*>(p.A) + off + koff : zero,
+                                       As + lds_wave + i * NW * 1024, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < C::NLB; ++i) {
-      const bool kin = k_exact || kt * C::BK + wsc[i] * 8 < p.K;
-      __builtin_amdgcn_global_load_lds(kin ? w[i] + koff : zero, Bs + lds_wave + i * NW * 1024, 16, 0, 0);
+      const int r = (i * NW + wave) * C::RPI + lrow;
+      const bool kin = kt * C::BK + (pos ^ pswz<RB>(r)) * 8 < p.K;
+      uint32_t off = wo[i];
+      asm volatile("" : "+v"(off));
+      __builtin_amdgcn_global_load_lds(kin ? reinterpret_cast<const char*>(p.W) + off + koff : zero,
+                                       Bs + lds_wave + i * NW * 1024, 16, 0, 0);
     }
   }
 };
+
+// The buffer-offset staging form applies: whole K tiles (both operands are under 2 GiB: launch_gemm_pers checks)
+template <int BK>
+__device__ __forceinline__ bool pers_fast_staging(const GemmArgs& p) {
+  return p.K % BK == 0;
+}
+
+// 32-bit byte offsets reach every staged element (ao / wo + the K offset of the last tile)
+static bool pers_operands_fit(const GemmArgs& a) {
+  return (int64_t)a.M * a.lda * 2 + (int64_t)a.K * 2 + 256 < 0x7fffffff &&
+         (int64_t)a.N * a.ldw * 2 + (int64_t)a.K * 2 + 256 < 0x7fffffff;
+}
 
 // Epilogue of one tile straight from the (swapped-operand) accumulators: lane (r16 = lane & 15, g = lane >> 4) holds
 // output row bm + wm*TM + i*16 + r16, columns bn + wn*TN + j*16 + g*4 + {0..3} in acc[i][j].
@@ -202,7 +240,7 @@ __global__ void __launch_bounds__(NW * 64, MINB) gemm_pers_kernel(GemmArgs p) {
   const int ntm = (p.M + BM - 1) / BM, ntn = (p.N + BN - 1) / BN;
   const int tiles = ntm * ntn, G = gridDim.x;
   const int nk = (p.K + C::BK - 1) / C::BK;
-  const bool k_exact = (p.K % C::BK) == 0;
+  const bool fast = pers_fast_staging<C::BK>(p);
   const int lds_wave = wave * 1024;
   const int g = lane >> 4, r16 = lane & 15;
 
@@ -228,7 +266,7 @@ __global__ void __launch_bounds__(NW * 64, MINB) gemm_pers_kernel(GemmArgs p) {
   src.setup(p, tm * BM, tn * BN, wave, lane);
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
-    if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, k_exact);
+    if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, fast, wave, lane);
   // Stagger: the workgroups with one tile fewer (no tile in the last, partial round) start p.stagger ticks late, so
   // their tile boundaries fall mid-tile of the others' and the chip's epilogue store bursts no longer coincide; they
   // still finish before the full-length workgroups as long as the delay is under one tile time.
@@ -259,7 +297,7 @@ __global__ void __launch_bounds__(NW * 64, MINB) gemm_pers_kernel(GemmArgs p) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every wave's DMA for tile kt landed; every wave done with tile kt-1
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + STAGES - 1 < nk) src.stage(p, lds, slot == 0 ? STAGES - 1 : slot - 1, kt + STAGES - 1, lds_wave, k_exact);
+      if (kt + STAGES - 1 < nk) src.stage(p, lds, slot == 0 ? STAGES - 1 : slot - 1, kt + STAGES - 1, lds_wave, fast, wave, lane);
       const char* base = lds + slot * C::STAGE;
       bf16x8 af[C::KG][C::FM], bfr[C::KG][C::FN];
 #pragma unroll
@@ -291,7 +329,7 @@ __global__ void __launch_bounds__(NW * 64, MINB) gemm_pers_kernel(GemmArgs p) {
       src.setup(p, tm * BM, tn * BN, wave, lane);
 #pragma unroll
       for (int s0 = 0; s0 < STAGES - 1; ++s0)
-        if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, k_exact);
+        if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, fast, wave, lane);
     }
     if (DIAG != 1 || p.M < 0) pers_epilogue<MODE, F16, C::FM, C::FN, C::TM, C::TN>(p, acc, bm, bn, wm, wn, lane);
     if (!more) break;
@@ -487,7 +525,7 @@ __global__ void __launch_bounds__(PTHREADS, MINB) gemm_pers_ln_kernel(GemmArgs p
   const int ntm = (p.M + BM - 1) / BM, ntn = p.N / BN;
   const int tiles = ntm * ntn, G = gridDim.x;
   const int nk = (p.K + C::BK - 1) / C::BK;
-  const bool k_exact = (p.K % C::BK) == 0;
+  const bool fast = pers_fast_staging<C::BK>(p);
   const int lds_wave = wave * 1024;
   const int g = lane >> 4, r16 = lane & 15;
   int a_off[C::KG][C::FM], b_off[C::KG][C::FN];
@@ -514,7 +552,7 @@ __global__ void __launch_bounds__(PTHREADS, MINB) gemm_pers_ln_kernel(GemmArgs p
     src.setup(p, tm * BM, tn * BN, wave, lane);
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
-      if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, k_exact);
+      if (s0 < nk) src.stage(p, lds, s0, s0, lds_wave, fast, wave, lane);
 #pragma unroll
     for (int i = 0; i < C::FM; ++i)
 #pragma unroll
@@ -529,7 +567,7 @@ __global__ void __launch_bounds__(PTHREADS, MINB) gemm_pers_ln_kernel(GemmArgs p
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      if (kt + STAGES - 1 < nk) src.stage(p, lds, slot == 0 ? STAGES - 1 : slot - 1, kt + STAGES - 1, lds_wave, k_exact);
+      if (kt + STAGES - 1 < nk) src.stage(p, lds, slot == 0 ? STAGES - 1 : slot - 1, kt + STAGES - 1, lds_wave, fast, wave, lane);
       const char* sb = lds + slot * C::STAGE;
       bf16x8 af[C::KG][C::FM], bfr[C::KG][C::FN];
 #pragma unroll
@@ -637,7 +675,8 @@ static GemmKernel pers_kernel(int mode, bool f16, int s) {
 bool launch_gemm_pers(const GemmArgs& a, int shape, int cus, hipStream_t stream) {
   // dense A, one of the two transformer epilogue patterns, 16-B aligned rows
   const int mode = epi_mode(a);
-  if (!mode || a.sp_half != 0x7fffffff || a.N % 4 || a.ldo % 4 || a.lda % 8 || a.ldw % 8) return false;
+  if (!mode || a.sp_half != 0x7fffffff || a.N % 4 || a.ldo % 4 || a.lda % 8 || a.ldw % 8 || !pers_operands_fit(a))
+    return false;
   if (mode == 1 && a.act != MAPA_ACT_NONE && a.act != MAPA_ACT_GELU) return false;
   if (shape < 0) {
     if (mode != 1) return false;  // the residual pattern: the tile kernels measured as fast or faster (pers_ab)
@@ -668,7 +707,8 @@ bool launch_gemm_pers_ln(const GemmArgs& a, void* ws, int64_t ws_bytes, int cus,
       (reinterpret_cast<uintptr_t>(a.ln_out) & 15))
     return false;
   if (a.out_mode != 0 || !a.out_f32 || !a.resid1 || a.resid2 || a.out_lp || a.out_lp_relu || a.out_s3 ||
-      a.out_s3_relu || a.act != MAPA_ACT_NONE || a.ldo % 4 || a.lda % 8 || a.ldw % 8 || a.sp_half != 0x7fffffff)
+      a.out_s3_relu || a.act != MAPA_ACT_NONE || a.ldo % 4 || a.lda % 8 || a.ldw % 8 || a.sp_half != 0x7fffffff ||
+      !pers_operands_fit(a))
     return false;
   const int ntm = (a.M + BM - 1) / BM, ntn = a.N / BN;
   if (2 * ntm >= LN_TICKET_WORDS || !ws || ws_bytes < GEMM_TICKET_BYTES + (int64_t)ntm * LN_MAX_NTN_P * BM * 16)

@@ -12,6 +12,9 @@ import torch  # noqa: E402
 
 from mapanything import _native as nat  # noqa: E402
 
+if os.environ.get("MAPA_AB_LIB"):  # A/B builds (tools/ab_build.sh): load before any other call
+    nat.load_library(os.environ["MAPA_AB_LIB"])
+
 V, T = 8, 1369
 R, L = V * (T + 1), V * T + 1
 SHAPES = [("enc.qkv", R, 3072, 1024, "plain"), ("enc.fc1", R, 4096, 1024, "gelu"), ("aat.qkv", L, 2304, 768, "plain"),
