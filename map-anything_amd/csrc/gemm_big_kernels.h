@@ -54,23 +54,45 @@ __device__ __forceinline__ int swz(int row) {
 }
 
 // LDS-DMA of K tile kt into stage buf: NLA 1-KiB wave instructions of A rows, NLB of W rows per wave.
+// fast (dense plain A, whole K tiles, both operands under 2 GiB: big_fast_staging): buffer loads from per-lane 32-bit
+// row offsets a_o / w_o with the tile's K offset in soffset — no 64-bit pointer per piece in registers, no zero-page
+// select.  Otherwise the general form: row pointers recomputed from (bm, bn) per tile (the empty asm keeps them out of
+// the loop-invariant code motion that would pin them in registers), K-tail chunks and conv padding from the zero page.
 template <int AMODE, int BN, int RB, int BM = BBM>
 __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf, int kt, int lds_wave, bool k_exact,
-                                          const char* const* a_src, const int* a_sc, const int* cv_pix,
-                                          const int* cv_yx, const char* const* w_src,
-                                          const int* w_sc) {
+                                          const uint32_t* a_o, const int* a_sc, const int* cv_pix,
+                                          const int* cv_yx, const uint32_t* w_o, const int* w_sc, bool fast, int bm,
+                                          int bn, int wave, int lane) {
   using C = Cfg<BN, RB, BM>;
-  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
+  typedef __attribute__((address_space(3))) void* lds_ptr_t;
   char* As = lds + buf * C::STAGE;
   char* Bs = As + C::A_BYTES;
+  if (AMODE == 0 && fast) {
+    const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, 0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.W, 0, 0x7fffffff, 0x00020000);
+    const int koff = kt * C::BK * 2;
+#pragma unroll
+    for (int i = 0; i < C::NLA; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)(As + lds_wave + i * 8192), 16, (int)a_o[i], koff, 0, 0);
+#pragma unroll
+    for (int i = 0; i < C::NLB; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_ptr_t)(Bs + lds_wave + i * 8192), 16, (int)w_o[i], koff, 0, 0);
+    return;
+  }
+  const char* zero = reinterpret_cast<const char*>(g_mapa_zero_page);
   const int64_t koff = (int64_t)kt * C::BK * 2;
+  const int lrow = lane / C::CPR;
 #pragma unroll
   for (int i = 0; i < C::NLA; ++i) {
     const int kc = kt * C::BK + a_sc[i] * 8;
     const bool kin = k_exact || kc < p.K;
     const char* src;
     if constexpr (AMODE == 0) {
-      src = kin ? a_src[i] + koff - split_koff(p, kc, 2) : zero;
+      int m = min(bm + (i * 8 + wave) * C::RPI + lrow, p.M - 1);
+      asm volatile("" : "+v"(m));
+      src = kin ? reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + a_sc[i] * 8) * 2 + koff -
+                      split_koff(p, kc, 2)
+                : zero;
     } else {
       int tap, ci;
       conv_kmap(p, kc, tap, ci);
@@ -85,8 +107,19 @@ __device__ __forceinline__ void stage_big(const GemmArgs& p, char* lds, int buf,
   for (int i = 0; i < C::NLB; ++i) {
     const int kc = kt * C::BK + w_sc[i] * 8;
     const bool kin = k_exact || kc < p.K;
-    __builtin_amdgcn_global_load_lds(kin ? w_src[i] + koff : zero, Bs + lds_wave + i * 8192, 16, 0, 0);
+    int n = min(bn + (i * 8 + wave) * C::RPI + lrow, p.N - 1);
+    asm volatile("" : "+v"(n));
+    const char* src = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + w_sc[i] * 8) * 2 + koff;
+    __builtin_amdgcn_global_load_lds(kin ? src : zero, Bs + lds_wave + i * 8192, 16, 0, 0);
   }
+}
+
+// stage_big's fast form applies to this launch (dense plain A, K a multiple of BK, 32-bit offsets reach every byte)
+template <int AMODE, int BK>
+__device__ __forceinline__ bool big_fast_staging(const GemmArgs& p) {
+  return AMODE == 0 && p.K % BK == 0 && p.sp_half == 0x7fffffff &&
+         (int64_t)p.M * p.lda * 2 + (int64_t)p.K * 2 + 256 < 0x7fffffff &&
+         (int64_t)p.N * p.ldw * 2 + (int64_t)p.K * 2 + 256 < 0x7fffffff;
 }
 
 // ---- epilogue: 32 rows x 64 fp32 per wave per pass through LDS; 8 columns per lane (16-B bf16 stores) -------
@@ -387,10 +420,10 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
 
   // ---- staging geometry: wave instruction i of this wave covers rows (i*8 + wave)*RPI .. +RPI-1
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
-  const char* a_src[C::NLA];
+  uint32_t a_src[C::NLA];  // stage_big's fast-path row offsets (bytes from A / W)
   int a_sc[C::NLA];
   int cv_pix[C::NLA], cv_yx[C::NLA];
-  const char* w_src[C::NLB];
+  uint32_t w_src[C::NLB];
   int w_sc[C::NLB];
 #pragma unroll
   for (int i = 0; i < C::NLA; ++i) {
@@ -398,7 +431,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
     a_sc[i] = pos ^ swz<RB>(r);
     const int m = min(bm + r, p.M - 1);
     if constexpr (AMODE == 0) {
-      a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + a_sc[i] * 8) * 2;
+      a_src[i] = (uint32_t)(((int64_t)m * p.lda + a_sc[i] * 8) * 2);
     } else {
       const int hw = p.cv_OH * p.cv_OW;
       const int img = m / hw, rem = m - img * hw;
@@ -411,10 +444,11 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
     const int r = (i * 8 + wave) * C::RPI + lrow;
     w_sc[i] = pos ^ swz<RB>(r);
     const int n = min(bn + r, p.N - 1);
-    w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + w_sc[i] * 8) * 2;
+    w_src[i] = (uint32_t)(((int64_t)n * p.ldw + w_sc[i] * 8) * 2);
   }
   const int nk = (p.K + C::BK - 1) / C::BK;
   const bool k_exact = (p.K % C::BK) == 0;
+  const bool fast = big_fast_staging<AMODE, C::BK>(p);
   const int lds_wave = wave * 1024;
 
   f32x4 acc[C::FM][C::FN];
@@ -483,12 +517,12 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
   };
 
   if constexpr (STAGES == 2) {
-    stage_big<AMODE, BN, RB, BM>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src, w_sc);
+    stage_big<AMODE, BN, RB, BM>(p, lds, 0, 0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src, w_sc, fast, bm, bn, wave, lane);
     for (int kt = 0; kt < nk; ++kt) {
       __syncthreads();  // tile kt landed (vmcnt(0) before the barrier); every wave is done with tile kt-1
       if (kt + 1 < nk && DIAG != 1)
         stage_big<AMODE, BN, RB, BM>(p, lds, (kt + 1) & 1, kt + 1, lds_wave, k_exact, a_src, a_sc, cv_pix,
-                                 cv_yx, w_src, w_sc);
+                                 cv_yx, w_src, w_sc, fast, bm, bn, wave, lane);
       if (DIAG != 2) compute(kt & 1);
     }
   } else {
@@ -496,7 +530,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
 #pragma unroll
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
       if (s0 < nk)
-        stage_big<AMODE, BN, RB, BM>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src, w_sc);
+        stage_big<AMODE, BN, RB, BM>(p, lds, s0, s0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src, w_sc, fast, bm, bn, wave, lane);
     int slot = 0;
     for (int kt = 0; kt < nk; ++kt) {
       const int ahead = min(STAGES - 2, nk - 1 - kt);  // tiles issued after kt that may still be in flight
@@ -510,7 +544,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_big_kernel(GemmArgs p) {
       if (kt + STAGES - 1 < nk && DIAG != 1) {
         const int ns = slot == 0 ? STAGES - 1 : slot - 1;  // (kt + STAGES - 1) % STAGES
         stage_big<AMODE, BN, RB, BM>(p, lds, ns, kt + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_pix,
-                                 cv_yx, w_src, w_sc);
+                                 cv_yx, w_src, w_sc, fast, bm, bn, wave, lane);
       }
       if (DIAG != 2) compute(slot);
       slot = slot + 1 == STAGES ? 0 : slot + 1;
@@ -777,6 +811,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
   const int ntn = (p.N + BN - 1) / BN, ntm = (p.M + BBM - 1) / BBM;
   const int vb = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ranges (shared tiles) on one XCD
   const bool k_exact = (p.K % C::BK) == 0;
+  const bool fast = big_fast_staging<AMODE, C::BK>(p);
   const int lds_wave = wave * 1024;
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
   const int g = lane >> 4, r16 = lane & 15;
@@ -792,10 +827,10 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
     group_coords<4>(t, ntm, ntn, tm, tn);
     const int bm = tm * BBM, bn = tn * BN;
 
-    const char* a_src[C::NLA];
+    uint32_t a_src[C::NLA];  // stage_big's fast-path row offsets
     int a_sc[C::NLA];
     int cv_pix[C::NLA], cv_yx[C::NLA];
-    const char* w_src[C::NLB];
+    uint32_t w_src[C::NLB];
     int w_sc[C::NLB];
 #pragma unroll
     for (int i = 0; i < C::NLA; ++i) {
@@ -803,7 +838,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
       a_sc[i] = pos ^ swz<RB>(r);
       const int m = min(bm + r, p.M - 1);
       if constexpr (AMODE == 0) {
-        a_src[i] = reinterpret_cast<const char*>(p.A) + ((int64_t)m * p.lda + a_sc[i] * 8) * 2;
+        a_src[i] = (uint32_t)(((int64_t)m * p.lda + a_sc[i] * 8) * 2);
       } else {
         const int hw = p.cv_OH * p.cv_OW;
         const int img = m / hw, rem = m - img * hw;
@@ -816,7 +851,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
       const int r = (i * 8 + wave) * C::RPI + lrow;
       w_sc[i] = pos ^ swz<RB>(r);
       const int n = min(bn + r, p.N - 1);
-      w_src[i] = reinterpret_cast<const char*>(p.W) + ((int64_t)n * p.ldw + w_sc[i] * 8) * 2;
+      w_src[i] = (uint32_t)(((int64_t)n * p.ldw + w_sc[i] * 8) * 2);
     }
 
     f32x4 acc[C::FM][C::FN];
@@ -861,7 +896,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
     for (int s0 = 0; s0 < STAGES - 1; ++s0)
       if (s0 < n)
         stage_big<AMODE, BN, RB>(p, lds, s0, k0 + s0, lds_wave, k_exact, a_src, a_sc, cv_pix, cv_yx, w_src,
-                                 w_sc);
+                                 w_sc, fast, bm, bn, wave, lane);
     int slot = 0;
     for (int kk = 0; kk < n; ++kk) {
       const int ahead = min(STAGES - 2, n - 1 - kk);
@@ -875,7 +910,7 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
       if (kk + STAGES - 1 < n) {
         const int ns = slot == 0 ? STAGES - 1 : slot - 1;
         stage_big<AMODE, BN, RB>(p, lds, ns, k0 + kk + STAGES - 1, lds_wave, k_exact, a_src, a_sc, cv_pix,
-                                 cv_yx, w_src, w_sc);
+                                 cv_yx, w_src, w_sc, fast, bm, bn, wave, lane);
       }
       compute(slot);
       slot = slot + 1 == STAGES ? 0 : slot + 1;
