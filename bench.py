@@ -53,6 +53,31 @@ def enc_linear_flops_per_view(T):
     return 24 * per_block + 2 * T * 588 * 1024
 
 
+_JSON_FD = None  # a private dup of the real stdout: the one JSON line goes there (_protect_stdout)
+
+
+def _protect_stdout():
+    """Native libraries write to fd 1 — RCCL prints its version banner to stdout when a communicator is created (the
+    N > 1 path and --shard-rehearsal) — which would put non-JSON lines in front of rank 0's JSON line.  Keep a dup of
+    the real stdout for that line and point fd 1 (and with it Python's own prints) at stderr."""
+    global _JSON_FD
+    if _JSON_FD is not None:
+        return
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
+
+
+def _emit(obj):
+    """The bench's one JSON line, on the real stdout."""
+    line = json.dumps(obj) + "\n"
+    if _JSON_FD is None:
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    else:
+        os.write(_JSON_FD, line.encode())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,6 +134,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    _protect_stdout()
     if args.dry_run:
         return dry_run(args, world, rank)
     if args.lib:
@@ -385,7 +411,7 @@ def main():
             "hip_graph_fallback": None if not sharded else model.shard_graph_fallback,
             "shard_graph_check": shard_check,
         }
-        print(json.dumps(line), flush=True)
+        _emit(line)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -556,6 +582,9 @@ def dry_run(args, world, rank):
     observed = 1
     if world > 1:
         _, observed = init_distributed("gloo")
+    if os.environ.get("MAPA_BENCH_STDOUT_NOISE"):  # test hook: a native library writing to fd 1 (RCCL's banner)
+        os.write(1, b"RCCL version : (native stdout noise)\n")
+        print("python-level stdout noise", flush=True)
     if rank == args.fail_rank:
         raise SystemExit(f"rank {rank}: injected failure (--fail-rank)")
     comm = DistComm() if world > 1 else None
@@ -600,9 +629,9 @@ def dry_run(args, world, rank):
         raise SystemExit(f"rank {rank}: {e}")
     if rank == 0:
         kvo = kv_overlap({k: {"ms": sum(v), "count": len(v)} for k, v in phases.items()}) if world > 1 else None
-        print(json.dumps({"metric": "dry-run (launcher rehearsal, no GPU)", "value": args.steps / dt, "unit": "steps/s",
-                          "n_gpus": world, "world_size_observed": observed, "steps": args.steps,
-                          "warmup": args.warmup, "dry_run": True, "kv_overlap": kvo}), flush=True)
+        _emit({"metric": "dry-run (launcher rehearsal, no GPU)", "value": args.steps / dt, "unit": "steps/s",
+               "n_gpus": world, "world_size_observed": observed, "steps": args.steps, "warmup": args.warmup,
+               "dry_run": True, "kv_overlap": kvo})
     if world > 1:
         dist.destroy_process_group()
 

@@ -38,6 +38,18 @@ def test_bench_gpus_n_launches_n_ranks():
         assert k in kvo and kvo[k] is not None and kvo[k] >= 0, (k, kvo)
 
 
+def test_bench_stdout_is_one_json_line_despite_native_prints():
+    """Native libraries print to fd 1 (RCCL's version banner at communicator init, on every N > 1 rank): bench.py sends
+    fd 1 to stderr and writes rank 0's JSON line to a private dup of the real stdout, so the job's stdout is exactly
+    that one line (the driver parses it)."""
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1"], MAPA_BENCH_STDOUT_NOISE="1")
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    assert json.loads(lines[0])["dry_run"]
+    assert "native stdout noise" in r.stderr
+
+
 def test_bench_failing_rank_fails_the_job():
     r = _bench(["--gpus", "2", "--dry-run", "--steps", "3", "--warmup", "1", "--fail-rank", "1"])
     assert r.returncode != 0
