@@ -1,3 +1,7 @@
+# Same-box A/B of an earlier round's head against this one (its own tree and library):
+#   git worktree add -f ab_r5 <commit> && make -C ab_r5/map-anything_amd/csrc -j8
+#   (add "ab_r5/tests/golden/*.npz" and "ab_r5/profiles" to .gpurunignore while the worktree exists), then on the box
+#   bash tools/round_ab.sh; remove the worktree afterwards (git worktree remove --force ab_r5).
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
