@@ -12,12 +12,15 @@ import torch  # noqa: E402
 
 from mapanything import _native as nat  # noqa: E402
 
+if os.environ.get("MAPA_AB_LIB"):  # A/B builds (tools/ab_build.sh): load before any other call
+    nat.load_library(os.environ["MAPA_AB_LIB"])
+
 SHAPES = [("encoder", 8, 16, 1370), ("frame", 8, 12, 1369), ("global", 1, 12, 8 * 1369 + 1)]
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    res = {"arm": os.environ.get("MAPA_ATTN_PP", "0")}
+    res = {"arm": os.environ.get("AB_ARM", os.environ.get("MAPA_ATTN_PP", "0"))}
     for name, B, H, S in SHAPES:
         C = H * 64
         g = torch.Generator(device="cuda").manual_seed(1234 + S)
