@@ -357,13 +357,16 @@ static int pers_mode() {
 }
 
 // The LayerNorm-fused residual linears on the persistent kernel (launch_gemm_pers_ln) instead of gemm_big's LNF tiles:
-// mapa_gemm_tune(MAPA_TUNE_PERS_LN, .) / env MAPA_GEMM_PERS_LN, 1 = on, 0 = off (default: 1-4 us slower per launch
-// than the LNF tiles on the path shapes, tools/pers_ab.py, profiles/r6/pers_ab.json); -1: env not read.
+// mapa_gemm_tune(MAPA_TUNE_PERS_LN, .) / env MAPA_GEMM_PERS_LN, 1 = always, 2 = where K <= 1024, 0 = never (default:
+// in isolation the persistent form was faster on the proj linears — enc.proj 45.5 vs 48.2 us, aat.proj 36.9 vs 37.8 —
+// and slower at K = 3072 / 4096, aat.fc2 76.7 vs 73.4, but inside the model mode 2 measured 321.8 vs 323.5 views/s,
+// profiles/r6/ln_forms_ab.txt); -1: env not read.
 static int g_pers_ln = -1;
 static int pers_ln_mode() {
   if (g_pers_ln < 0) g_pers_ln = getenv("MAPA_GEMM_PERS_LN") ? atoi(getenv("MAPA_GEMM_PERS_LN")) : 0;
   return g_pers_ln;
 }
+static bool pers_ln_takes(int K) { return pers_ln_mode() == 1 || (pers_ln_mode() == 2 && K <= 1024); }
 
 static int g_forced = -1;  // -1: not read yet; 0: automatic; else a kernel variant code (tuning / tests)
 
@@ -508,7 +511,7 @@ extern "C" int mapa_gemm(const mapa_gemm_desc* d, hipStream_t stream) {
                    : forced ? (forced == 2589 ? conv_halo_flat_split(a, gemm_streamk_slots(0), g_halo_split) : 0)
                             : pick_flat(a);
   const int lnf = pick_ln_fused(d, variant, sk);
-  if (lnf && pers_ln_mode() && !forced &&
+  if (lnf && pers_ln_takes(d->K) && !forced &&
       launch_gemm_pers_ln(a, d->workspace, d->workspace_bytes, gemm_streamk_slots(1), stream)) {
     MAPA_CHECK_LAUNCH("mapa_gemm (LayerNorm fused, persistent)");
     return 0;
@@ -596,7 +599,7 @@ extern "C" int mapa_gemm_tune(int key, int value) {
     return 0;
   }
   if (key == MAPA_TUNE_PERS_LN) {
-    g_pers_ln = value ? 1 : 0;
+    g_pers_ln = value == 2 ? 2 : value ? 1 : 0;
     return 0;
   }
   if (key == MAPA_TUNE_PERS) {

@@ -612,14 +612,14 @@ static void pers_shape(int s, int& bm, int& bn, int& per_cu, int& nw) {
 static int g_pers_stagger = -2;
 
 // Automatic stagger: half a tile's time (2 BM BN K flop at ~1.65 TFLOP/s per resident workgroup, the path rate) where
-// the short workgroups are a minority (< 35 % of the grid): then they still finish first, and the chip's epilogue
+// the short workgroups are a minority (< 40 % of the grid): then they still finish first, and the chip's epilogue
 // bursts split into two half-size ones that fall mid-tile of the other group.  Measured (tools/stagger_ab.py,
 // profiles/r6/stagger_ab.json, 192x128 tiles): enc.qkv 81.3 -> 78.2 us at 1500 ticks, enc.fc1 111.6 -> 109.5;
 // aat.fc1 neutral; where most workgroups are short (aat.qkv: 492 of 512) any delay only adds to the kernel
 // (49.1 -> 52.1 us at 500 ticks), so none is applied there.  Bitwise-neutral: the same tiles, the same K order.
 static int pers_auto_stagger(int64_t tiles, int G, int bm, int bn, int K) {
   const int64_t rem = tiles % G;
-  if (rem == 0 || tiles < G || (G - rem) * 100 >= 35 * (int64_t)G) return 0;
+  if (rem == 0 || tiles < G || (G - rem) * 100 >= 40 * (int64_t)G) return 0;
   const double tile_us = 2.0 * bm * bn * (double)K / 1.65e6;
   return (int)(0.5 * tile_us * 100.0);  // 100 ticks per microsecond
 }

@@ -208,14 +208,15 @@ def _ln_flag(nat):
                                          (10953, 768, 3072, False), (150, 768, 768, False), (4001, 1024, 1024, True),
                                          (21905, 768, 3072, False), (80001, 1024, 1024, True),
                                          (136901, 768, 768, False)])
-@pytest.mark.parametrize("pers_ln", [0, 1])
+@pytest.mark.parametrize("pers_ln", [0, 1, 2])
 def test_gemm_layernorm_fused(nat, M, N, K, gamma, pers_ln):
     """mapa_gemm with ln_out (the next sub-block's LayerNorm fused into the residual linear): the fp32 residual
     stream bitwise equal to the plain GEMM's, the bf16 normalised rows within one bf16 rounding of the standalone
     two-pass LayerNorm of that stream (mapa_layernorm) and of torch's fp32 LayerNorm, repeatable bit for bit, and no
     band barrier timed out.  MAPA_TUNE_LN_FUSE=0 (GEMM, then LayerNorm) is the A side, 1 fuses only where the tile
     choice is the 192-row kernel, 2 (the default) whatever it is.  pers_ln = 1: the fused forms on the persistent
-    register-epilogue kernel (MAPA_TUNE_PERS_LN; whole 192-row bands per round)."""
+    register-epilogue kernel (MAPA_TUNE_PERS_LN; whole 192-row bands per round); 2: that form where K <= 1024, the
+    LNF tiles above."""
     A = _rand(M, K, seed=61).to(torch.bfloat16)
     W = _rand(N, K, scale=K ** -0.5, seed=62).to(torch.bfloat16)
     b = _rand(N, seed=63)
@@ -238,7 +239,7 @@ def test_gemm_layernorm_fused(nat, M, N, K, gamma, pers_ln):
         xa, ya = run(2)  # the default: the fused kernel whatever the tile choice (B = 2: more tiles than CUs)
     finally:
         nat.gemm_tune(nat.TUNE_LN_FUSE, 2)  # the default
-        nat.gemm_tune(nat.TUNE_PERS_LN, 0)
+        nat.gemm_tune(nat.TUNE_PERS_LN, 0)  # the default
     assert _ln_flag(nat) == 0
     assert torch.equal(xf, xs) and torch.equal(xf2, xf) and torch.equal(yf2, yf)
     assert not torch.isnan(yf.float()).any() and not torch.isnan(ya.float()).any()
@@ -252,7 +253,43 @@ def test_gemm_layernorm_fused(nat, M, N, K, gamma, pers_ln):
     assert rel_l2(xa.cpu(), xs.cpu()) < 1e-6  # another tile kernel for the residual when the choice differed
 
 
-@pytest.mark.parametrize("pers_ln", [0, 1])
+def test_gemm_layernorm_forms_interleave_in_one_workspace(nat):
+    """MAPA_TUNE_PERS_LN = 2 alternates the persistent LayerNorm form (K <= 1024: the proj linears) with the LNF tiles
+    (K = 4096: fc2) on one stream's workspace, as a transformer block does.  Both forms key their row statistics on the
+    same 192-row bands and per-band generation words, so a granule left by one form never carries the epoch the other
+    waits for: every call of an interleaved sequence equals the same call run alone, bit for bit."""
+    M, N = 10960, 1024
+    lw, lb = 1.0 + 0.2 * _rand(N, seed=91), 0.1 * _rand(N, seed=92)
+    shapes = [1024, 4096, 1024, 4096, 1024]
+    ops = []
+    for i, K in enumerate(shapes):
+        A = _rand(M, K, seed=100 + i).to(torch.bfloat16)
+        W = _rand(N, K, scale=K ** -0.5, seed=200 + i).to(torch.bfloat16)
+        ops.append((A, W, K, _rand(N, seed=300 + i), _rand(M, N, seed=400 + i)))
+
+    def run(op):
+        A, W, K, b, x0 = op
+        x = x0.clone()
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        nat.gemm(A, W, M, N, K, bias=b, resid1=x, out_f32=x, ln=(lw, lb, 1e-6, y))
+        return x, y
+
+    nat.gemm_tune(nat.TUNE_PERS_LN, 2)
+    alone = []
+    for op in ops:  # each call after a fresh call of the same shape only
+        run(op)
+        alone.append(run(op))
+    torch.cuda.synchronize()
+    for _ in range(2):
+        seq = [run(op) for op in ops]
+        torch.cuda.synchronize()
+        for (xa, ya), (xs, ys) in zip(alone, seq):
+            assert torch.equal(xa, xs) and torch.equal(ya, ys)
+    nat.gemm_tune(nat.TUNE_PERS_LN, 0)  # the default
+    assert _ln_flag(nat) == 0
+
+
+@pytest.mark.parametrize("pers_ln", [0, 1, 2])
 def test_gemm_layernorm_barrier_timeout_is_reported(nat, pers_ln):
     """A band that never completes (the test hook drops tile (0, 0)'s statistics publish; MAPA_TUNE_LN_SPIN shortens
     the bounded wait) must not hang and must not pass silently: the fault word carries MAPA_FAULT_LN_BARRIER, a
@@ -303,7 +340,7 @@ def test_gemm_layernorm_barrier_timeout_is_reported(nat, pers_ln):
     assert torch.equal(y_bad[192:], y_ok[192:])  # only band 0's normalised rows are invalid
     x2, y2 = run()
     torch.cuda.synchronize()
-    nat.gemm_tune(nat.TUNE_PERS_LN, 0)
+    nat.gemm_tune(nat.TUNE_PERS_LN, 0)  # the default
     assert nat.fault_status(reset=False) == 0
     assert torch.equal(x2, x_ok) and torch.equal(y2, y_ok)
 
