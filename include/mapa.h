@@ -212,10 +212,10 @@ int mapa_regressor_head_out(const mapa_gemm_desc* d, const float* w6, const floa
  *     per round, all co-resident); 2 = that form where K <= 1024 only; 0 = the 192-row LNF tile kernel (measured
  *     fastest inside the model).  Every form keys its row statistics on the same 192-row bands and per-band
  *     generation words, so they may alternate on one workspace.
- *   MAPA_TUNE_PERS_STAGGER (default -1 = automatic, or the environment's MAPA_GEMM_STAGGER): the persistent kernel's
+ *   MAPA_TUNE_PERS_STAGGER (default 0 = off, or the environment's MAPA_GEMM_STAGGER): the persistent kernel's
  *     workgroups that get one tile fewer start `value` 100-MHz ticks (10 ns) late, so the chip's epilogue store bursts
- *     do not coincide (0 = off, up to 100000); automatic = half a tile's time where those workgroups are < 40 % of
- *     the grid, else none.  Results are bitwise the same either way.
+ *     do not coincide (up to 100000); -1 = automatic: half a tile's time where those workgroups are < 40 % of the
+ *     grid, else none.  Results are bitwise the same either way.
  *   MAPA_TUNE_DIAG_GRID (timing diagnostic, default 0): the data-parallel 256-row / 192-row tile kernels launch only
  *     their first `value` workgroups (0 = every tile); outputs of the other tiles are left unwritten. */
 enum { MAPA_TUNE_CONV_HALO = 0, MAPA_TUNE_TAIL_STREAMK = 1, MAPA_TUNE_HALO_SPLIT = 2, MAPA_TUNE_TILE_GROUP = 3,

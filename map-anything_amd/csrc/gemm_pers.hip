@@ -608,7 +608,9 @@ static void pers_shape(int s, int& bm, int& bn, int& per_cu, int& nw) {
 }
 
 // Start delay of the workgroups with one tile fewer (gemm_pers_kernel): mapa_gemm_tune(MAPA_TUNE_PERS_STAGGER, .) /
-// env MAPA_GEMM_STAGGER = 100-MHz ticks, 0 = off, -1 = automatic (pers_auto_stagger); -2: env not read yet.
+// env MAPA_GEMM_STAGGER = 100-MHz ticks, 0 = off (default), -1 = automatic (pers_auto_stagger); -2: env not read yet.
+// Off by default: the bench-level gain did not hold across boxes (+0.5 % on one, -0.2 / -0.5 % at 35 / 40 % on
+// another, profiles/r6/stagger_bench_ab.txt) — a fixed delay in ticks cannot track the box's clock.
 static int g_pers_stagger = -2;
 
 // Automatic stagger: half a tile's time (2 BM BN K flop at ~1.65 TFLOP/s per resident workgroup, the path rate) where
@@ -619,7 +621,9 @@ static int g_pers_stagger = -2;
 // (49.1 -> 52.1 us at 500 ticks), so none is applied there.  Bitwise-neutral: the same tiles, the same K order.
 static int pers_auto_stagger(int64_t tiles, int G, int bm, int bn, int K) {
   const int64_t rem = tiles % G;
-  if (rem == 0 || tiles < G || (G - rem) * 100 >= 40 * (int64_t)G) return 0;
+  static int pct = -1;  // MAPA_GEMM_STAGGER_PCT: the short-workgroup share below which the stagger applies (A/B)
+  if (pct < 0) pct = getenv("MAPA_GEMM_STAGGER_PCT") ? atoi(getenv("MAPA_GEMM_STAGGER_PCT")) : 40;
+  if (rem == 0 || tiles < G || (G - rem) * 100 >= pct * (int64_t)G) return 0;
   const double tile_us = 2.0 * bm * bn * (double)K / 1.65e6;
   return (int)(0.5 * tile_us * 100.0);  // 100 ticks per microsecond
 }
@@ -690,7 +694,7 @@ bool launch_gemm_pers(const GemmArgs& a, int shape, int cus, hipStream_t stream)
   const GemmKernel k = pers_kernel(mode, a.lp_f16 != 0, shape);
   if (!k) return false;
   GemmArgs b = a;
-  if (g_pers_stagger == -2) g_pers_stagger = getenv("MAPA_GEMM_STAGGER") ? atoi(getenv("MAPA_GEMM_STAGGER")) : -1;
+  if (g_pers_stagger == -2) g_pers_stagger = getenv("MAPA_GEMM_STAGGER") ? atoi(getenv("MAPA_GEMM_STAGGER")) : 0;
   b.stagger = g_pers_stagger >= 0 ? g_pers_stagger : pers_auto_stagger(tiles, G, bm, bn, a.K);
   hipLaunchKernelGGL(k, dim3(G), dim3(nw * 64), 0, stream, b);
   return true;
