@@ -328,6 +328,10 @@ class MapAnything:
 
         if gather_outputs not in (None, "rank0", "all"):
             raise ValueError(f"gather_outputs must be None, 'rank0' or 'all', got {gather_outputs!r}")
+        if getattr(self, "_comm_dead", None):
+            # a fresh communicator after an abort (_comm_failed): sharded HIP graphs are allowed again
+            self._shard_graphs = os.environ.get("MAPA_SHARD_GRAPHS", "1") != "0"
+            self.shard_graph_fallback = None if self._shard_graphs else "MAPA_SHARD_GRAPHS=0"
         if comm is None:
             comm = DistComm(group)
             if self._shard_graphs and dist.get_backend(group) == "nccl":

@@ -185,3 +185,42 @@ def test_batched_scene_layout_round_trip():
         assert torch.equal(out[v]["non_ambiguous_mask"], per_view[v][:, 0] > 102)
         assert torch.equal(out[v]["metric_scaling_factor"], msf)
     assert torch.equal(MapAnything._scene_major(rows, 1), rows)
+
+
+def test_aborted_communicator_drops_sharded_graphs_and_refuses_sharded_calls():
+    """after a sharded call's communicator is aborted (a hung or failed collective), the HIP
+    graphs captured against it hold its freed RCCL state.  MapAnything._comm_failed drops exactly those graphs (the
+    unsharded ones stay), marks the communicator and the model unfit for sharded capture, and every later sharded
+    call raises CommError — no replay on the dead communicator — until enable_view_sharding() installs a new one,
+    which allows sharded graphs again."""
+    import torch
+
+    from mapanything.parallel import CommError
+
+    class FakeComm:
+        world, rank, graph_safe = 2, 0, True
+
+        def __init__(self):
+            self.closed = False
+
+        def close(self, abort=False):
+            self.closed = True
+
+    m = _released_model()
+    c1 = FakeComm()
+    m.enable_view_sharding(comm=c1)
+    assert m._shard_graphs
+    m._graphs[("bf16", "tf32", (4, 3, 518, 518), 0, 1, None, None)] = "unsharded graph"
+    m._graphs[("bf16", "tf32", (4, 3, 518, 518), 0, 1, None, (2, 0, (4, 4), False, False, "1"))] = "sharded graph"
+    m._comm_failed(c1, "rank 0: forward not complete (test)")
+    assert list(m._graphs.values()) == ["unsharded graph"]
+    assert not c1.graph_safe and not m._shard_graphs
+    assert m.shard_graph_fallback.startswith("communicator aborted")
+    views = [{"img": torch.zeros(1, 3, 518, 518)} for _ in range(8)]
+    with pytest.raises(CommError, match="enable_view_sharding"):
+        m._local_views(views)
+    c2 = FakeComm()
+    m.enable_view_sharding(comm=c2)
+    assert c1.closed and m._comm is c2 and m._shard_graphs and m.shard_graph_fallback is None
+    local, plan = m._local_views(views)
+    assert plan.world == 2 and plan.rank == 0 and len(local) == 4
