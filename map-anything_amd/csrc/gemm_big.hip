@@ -74,6 +74,10 @@ int ln_take_test_skip() {
   return 1;
 }
 unsigned ln_spin_value() { return g_ln_spin; }
+int ln_diag_bits() {  // DIAG (timing only, wrong results): MAPA_LN_DIAG 2 = no band wait, 4 = no LN stores, 8 = no f32 stores
+  static int v = getenv("MAPA_LN_DIAG") ? (atoi(getenv("MAPA_LN_DIAG")) & 14) : 0;
+  return v;
+}
 
 
 // Workgroups of an LNF kernel the current device holds at once (occupancy per CU x CUs), per device and variant.
@@ -112,9 +116,9 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
   b.ln_ctr = reinterpret_cast<int*>(ws) + (GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS);
   b.ln_stats = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + GEMM_TICKET_BYTES);
   b.ln_spin = g_ln_spin;
-  b.ln_skip = 0;
+  b.ln_skip = ln_diag_bits();
   if (g_ln_skip > 0) {
-    b.ln_skip = 1;
+    b.ln_skip |= 1;
     --g_ln_skip;
   }
   for (int b0 = 0; b0 < ntm; b0 += nb) {
@@ -127,7 +131,7 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
       return false;
     }
     hipLaunchKernelGGL(k, dim3(grid), dim3(BTHREADS), 0, stream, b);
-    b.ln_skip = 0;
+    b.ln_skip &= ~1;
   }
   return true;
 }

@@ -309,7 +309,7 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
   // (another ntn) can carry this launch's epoch
   const auto srs = __builtin_amdgcn_make_buffer_rsrc(p.ln_stats + (int64_t)tm * LN_MAX_NTN * BM * 4, 0, ntn * BM * 16,
                                                      0x00020000);
-  if (tid < BM && !(p.ln_skip && tm == 0 && tn == 0)) {  // (ln_skip: the test hook's missing tile)
+  if (tid < BM && !((p.ln_skip & 1) && tm == 0 && tn == 0)) {  // (ln_skip: the test hook's missing tile)
     float m2 = 0.f;
 #pragma unroll
     for (int w = 0; w < WN; ++w) m2 += red[w * BM + tid];
@@ -322,7 +322,7 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {
       const int m = bm + wm * TM + part * 32 + pass * 8 + (lane >> 3);
-      if (col_ok && m < p.M) {
+      if (col_ok && m < p.M && !(p.ln_skip & 8)) {
         const int64_t off = (int64_t)m * p.ldo + n0;
         *reinterpret_cast<f32x4*>(p.out_f32 + off) = keep[part][pass][0];
         *reinterpret_cast<f32x4*>(p.out_f32 + off + 4) = keep[part][pass][1];
@@ -334,6 +334,7 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
     u32x4 gv[LN_MAX_NTN];
     unsigned spins = 0;
     for (;;) {
+      if (p.ln_skip & 2) break;  // (MAPA_LN_DIAG timing only)
 #pragma unroll
       for (int t = 0; t < LN_MAX_NTN; ++t)
         gv[t] = t < ntn ? __builtin_amdgcn_raw_buffer_load_b128(srs, (t * BM + tid) * 16, 0, 16) : u32x4{epoch, 0u, 0u, ~epoch};
@@ -379,7 +380,7 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
     for (int pass = 0; pass < 4; ++pass) {
       const int r = wm * TM + part * 32 + pass * 8 + (lane >> 3);
       const int m = bm + r;
-      if (!col_ok || m >= p.M) continue;
+      if (!col_ok || m >= p.M || (p.ln_skip & 4)) continue;
       const float mu = rmean[r], rs = rrstd[r];
       const f32x4 a = keep[part][pass][0], b = keep[part][pass][1];
       f32x4 y0, y1;

@@ -45,7 +45,8 @@ struct GemmArgs {
   unsigned* ln_stats;            // [bands][LN_MAX_NTN][BM] 16-B granules {epoch, sum, M2, ~epoch} (scratch)
   int ln_band0, ln_nbands;       // this launch's bands [ln_band0, ln_band0 + ln_nbands) (co-resident by construction)
   unsigned ln_spin;              // bounded wait: polls before the band barrier gives up and raises the fault word
-  int ln_skip;                   // test hook: tile (band 0, column 0) skips its publish (mapa_gemm_tune LN_TEST_SKIP)
+  int ln_skip;                   // bit 0, test hook: tile (band 0, column 0) skips its publish (mapa_gemm_tune
+                                 // LN_TEST_SKIP); bits 1-3: env MAPA_LN_DIAG timing diagnostics (ln_diag_bits)
   unsigned* fault;               // the library's device fault word (f16 split outputs out of binary16 range)
   int stagger;                   // gemm_pers_kernel: 100-MHz ticks the workgroups with one tile fewer start late
 };
@@ -432,6 +433,7 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
 void ln_set_spin(unsigned spins);
 void ln_arm_test_skip(int n);
 int ln_take_test_skip();    // 1 if an armed test skip is consumed by this launch
+int ln_diag_bits();         // MAPA_LN_DIAG: 2 no band wait, 4 no LN stores, 8 no residual stores (timing only)
 unsigned ln_spin_value();   // the band barrier's poll bound
 // The LayerNorm-fused residual linear on the persistent register-epilogue kernel (gemm_pers.hip): 192x128 tiles at 2
 // workgroups per CU, N = 768 / 1024, the workspace of launch_gemm_big_ln.  false if it does not qualify.

@@ -417,7 +417,7 @@ __device__ __forceinline__ void pers_epilogue_ln(const GemmArgs& p, f32x4 (&acc)
   if (tid < BM) {
 #pragma unroll
     for (int w = 0; w < WN; ++w) tsum += red[w * BM + tid];
-    if (!(p.ln_skip && tm == 0 && tn == 0)) {  // (ln_skip: the test hook's missing tile)
+    if (!((p.ln_skip & 1) && tm == 0 && tn == 0)) {  // (ln_skip: the test hook's missing tile)
       float m2 = 0.f;
 #pragma unroll
       for (int w = 0; w < WN; ++w) m2 += red2[w * BM + tid];
@@ -430,13 +430,14 @@ __device__ __forceinline__ void pers_epilogue_ln(const GemmArgs& p, f32x4 (&acc)
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       const int m = bm + wm * TM + i * 16 + r16;
-      if (m < p.M) *reinterpret_cast<f32x4*>(p.out_f32 + (int64_t)m * p.ldo + col0 + j * 16) = acc[i][j];
+      if (m < p.M && !(p.ln_skip & 8)) *reinterpret_cast<f32x4*>(p.out_f32 + (int64_t)m * p.ldo + col0 + j * 16) = acc[i][j];
     }
   // 4. the band's granules, merged in column order
   if (tid < BM) {
     u32x4p gv[LN_MAX_NTN_P];
     unsigned spins = 0;
     for (;;) {
+      if (p.ln_skip & 2) break;  // (MAPA_LN_DIAG timing only)
 #pragma unroll
       for (int t = 0; t < LN_MAX_NTN_P; ++t)
         gv[t] = t < ntn ? __builtin_amdgcn_raw_buffer_load_b128(srs, (t * BM + tid) * 16, 0, 16)
@@ -502,7 +503,7 @@ __device__ __forceinline__ void pers_epilogue_ln(const GemmArgs& p, f32x4 (&acc)
       uint2 rcv;
       rcv.x = __shfl_xor(snd.x, 16);
       rcv.y = __shfl_xor(snd.y, 16);
-      if (bm + rl < p.M)
+      if (bm + rl < p.M && !(p.ln_skip & 4))
         *reinterpret_cast<uint4*>(lout + (int64_t)(bm + rl) * p.ln_ldo + col) =
             odd ? uint4{rcv.x, rcv.y, ub.x, ub.y} : uint4{ua.x, ua.y, rcv.x, rcv.y};
     }
@@ -731,7 +732,7 @@ bool launch_gemm_pers_ln(const GemmArgs& a, void* ws, int64_t ws_bytes, int cus,
   GemmArgs b = a;
   b.ln_ctr = reinterpret_cast<int*>(ws) + (GEMM_TICKET_BYTES / 4 - LN_TICKET_WORDS);
   b.ln_stats = reinterpret_cast<unsigned*>(reinterpret_cast<char*>(ws) + GEMM_TICKET_BYTES);
-  b.ln_skip = ln_take_test_skip();
+  b.ln_skip = ln_take_test_skip() | ln_diag_bits();
   b.ln_spin = ln_spin_value();
   hipLaunchKernelGGL(k, dim3(G), dim3(PTHREADS), 0, stream, b);
   return true;
