@@ -816,7 +816,6 @@ __global__ void __launch_bounds__(BTHREADS, MINB) gemm_sk_kernel(GemmArgs p, SkA
   const int lds_wave = wave * 1024;
   const int lrow = lane / C::CPR, pos = lane % C::CPR;
   const int g = lane >> 4, r16 = lane & 15;
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
 
   // data-parallel whole tiles first, then this block's stream-K iteration range (mapa_idx::sk_next)
   mapa_idx::SkCursor cur = mapa_idx::sk_begin(s, vb);
