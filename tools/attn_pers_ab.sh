@@ -1,5 +1,7 @@
 # Persistent attention A/B: tests, then tools/attn_ab.py alternating the round-6 kernel (ab_libs/orig), the
-# persistent form and the persistent build with one block per task (MAPA_ATTN_PERSIST=0); outputs' SHA compared
+# persistent form and the persistent build with one block per task (MAPA_ATTN_PERSIST=0); outputs' SHA compared.
+# (The persistent form was not kept: profiles/r6/attn_pipelined_ab.txt.  Baseline lib: tools/ab_build.sh orig
+# <baseline attention.hip> attention.hip)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
