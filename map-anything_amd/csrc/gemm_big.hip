@@ -74,8 +74,9 @@ int ln_take_test_skip() {
   return 1;
 }
 unsigned ln_spin_value() { return g_ln_spin; }
-int ln_diag_bits() {  // DIAG (timing only, wrong results): MAPA_LN_DIAG 2 = no band wait, 4 = no LN stores, 8 = no f32 stores
-  static int v = getenv("MAPA_LN_DIAG") ? (atoi(getenv("MAPA_LN_DIAG")) & 14) : 0;
+int ln_diag_bits() {  // DIAG (timing only, wrong results): MAPA_LN_DIAG 2 = no band wait, 4 = no LN stores, 8 = no f32 stores,
+                      // 16 = no statistics / exchange at all (gemm_big LNF only)
+  static int v = getenv("MAPA_LN_DIAG") ? (atoi(getenv("MAPA_LN_DIAG")) & 30) : 0;
   return v;
 }
 
