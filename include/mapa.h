@@ -52,7 +52,7 @@ int mapa_device_check(int device);
 int mapa_stream_check(mapa_stream_t stream, const char* what);
 
 /* Device-side fault channel (round 5).  Kernels that can detect a failed assumption at run time set a bit of the
- * library's sticky per-device fault word instead of hanging or failing silently; today one: MAPA_FAULT_LN_BARRIER, a
+ * library's sticky fault word (below) instead of hanging or failing silently; today one: MAPA_FAULT_LN_BARRIER, a
  * LayerNorm-fused GEMM band barrier (mapa_gemm_desc.ln_out) that did not complete within its bounded wait — that
  * launch's LayerNorm rows are invalid.
  *   mapa_fault_slot_create: 64 bytes of coherent, device-mapped pinned host memory (the one allocation the library
@@ -66,8 +66,12 @@ int mapa_stream_check(mapa_stream_t stream, const char* what);
  *     reports only faults of its own call.
  *   mapa_fault_status: synchronous read of the fault word (and reset to 0 when `reset`); -1 on a HIP error.
  *   mapa_stream_check also reports and clears it.
- * The word is per device; the library's cached device properties (CU counts, co-resident slot counts of the
- * LayerNorm-fused GEMM) are kept per device too, so one process may drive several devices. */
+ * The word is per device and per calling host thread (round 6: a thread's word is fixed at its first library call;
+ * 64 words, threads beyond share round robin): every launch, reset, publish and status call of a thread uses its own
+ * word, so concurrent callers on different streams of one process (one thread each) neither see nor clear each
+ * other's faults.  A captured graph keeps the word of the thread that captured it.  The library's cached device
+ * properties (CU counts, co-resident slot counts of the LayerNorm-fused GEMM) are kept per device too, so one process
+ * may drive several devices. */
 /* MAPA_FAULT_F16_RANGE: a MAPA_F16 / MAPA_F16X2 producer met a value outside binary16's range (the TF32-equivalent
  * heads' operands); the outputs of that forward are not trustworthy: MapAnything.infer / forward re-run the call with
  * the fp32-exact split-precision heads (MapAnything._range_fallback) instead of returning them. */

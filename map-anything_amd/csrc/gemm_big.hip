@@ -1,14 +1,20 @@
 // 256-row bf16 GEMM / implicit-GEMM convolution (gfx950): kernel choice and launch, the LayerNorm-fused residual
 // linears, and the library's device fault word.  The kernel templates live in gemm_big_kernels.h and are instantiated
 // in gemm_big_dense.hip / _conv / _f16 / _diag / _sk.hip (parallel build); see gemm_big_kernels.h for the design.
+#include <atomic>
+
 #include "gemm_big_kernels.h"
 
 namespace mapa_gemm_impl {
 
 // Sticky fault bits of the library (MAPA_FAULT_* in mapa.h), set by device code, read by mapa_fault_publish (into a
 // host-visible slot, stream-ordered) and mapa_fault_status (synchronously).  Written with vector atomics only.  One
-// copy in this code object: kernels of the other translation units get its address (GemmArgs.fault, fault_word()).
-__device__ unsigned g_mapa_fault;
+// word per calling host thread (FAULT_WORDS of them, 64 B apart; a thread's word is fixed at its first call): the
+// per-call reset of one thread must not clear a fault another thread's concurrent call raised (two callers on two
+// streams of one process — the in-thread sharded tests, a server with a model per stream).  One copy in this code
+// object: kernels of the other translation units get the calling thread's word (GemmArgs.fault, fault_word()).
+constexpr int FAULT_WORDS = 64, FAULT_STRIDE = 16;
+__device__ unsigned g_mapa_fault[FAULT_WORDS * FAULT_STRIDE];
 
 static int g_diag_grid = 0;  // mapa_gemm_tune(MAPA_TUNE_DIAG_GRID, .): timing diagnostic, 0 = the whole grid
 void diag_set_grid(int blocks) { g_diag_grid = blocks; }
@@ -74,8 +80,9 @@ int ln_take_test_skip() {
   return 1;
 }
 unsigned ln_spin_value() { return g_ln_spin; }
-int ln_diag_bits() {  // DIAG (timing only, wrong results): MAPA_LN_DIAG 2 = no band wait, 4 = no LN stores, 8 = no f32 stores,
-                      // 16 = no statistics / exchange at all (gemm_big LNF only)
+// DIAG (timing only, wrong results): MAPA_LN_DIAG 2 = no band wait, 4 = no LN stores, 8 = no f32 stores, 16 = no
+// statistics / exchange at all (gemm_big LNF only)
+int ln_diag_bits() {
   static int v = getenv("MAPA_LN_DIAG") ? (atoi(getenv("MAPA_LN_DIAG")) & 30) : 0;
   return v;
 }
@@ -137,28 +144,31 @@ bool launch_gemm_big_ln(const GemmArgs& a, int variant, void* ws, int64_t ws_byt
   return true;
 }
 
-// The library's fault word (g_mapa_fault): stream-ordered reset and publish into a host-visible slot, synchronous
-// read / reset.
-__global__ void fault_reset_kernel() {
-  if (threadIdx.x == 0) __hip_atomic_store(&g_mapa_fault, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// The calling thread's fault word: stream-ordered reset and publish into a host-visible slot, synchronous read / reset.
+__global__ void fault_reset_kernel(unsigned* word) {
+  if (threadIdx.x == 0) __hip_atomic_store(word, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ void fault_publish_kernel(unsigned* slot) {
+__global__ void fault_publish_kernel(const unsigned* word, unsigned* slot) {
   if (threadIdx.x == 0) {
-    const unsigned f = __hip_atomic_load(&g_mapa_fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned f = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(slot, 1u | (f << 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
+static std::atomic<int> g_next_fault_word{0};
+
 unsigned* fault_word() {
-  static unsigned* cache[16] = {nullptr};
+  static unsigned* base[16] = {nullptr};
+  thread_local int word = -1;  // this host thread's word (threads past FAULT_WORDS share, round robin)
+  if (word < 0) word = g_next_fault_word.fetch_add(1) % FAULT_WORDS;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) dev = 0;
-  if (!cache[dev]) {
+  if (!base[dev]) {
     void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mapa_fault)) == hipSuccess) cache[dev] = static_cast<unsigned*>(p);
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_mapa_fault)) == hipSuccess) base[dev] = static_cast<unsigned*>(p);
   }
-  return cache[dev];
+  return base[dev] ? base[dev] + word * FAULT_STRIDE : nullptr;
 }
 
 }  // namespace mapa_gemm_impl
@@ -189,29 +199,37 @@ extern "C" int mapa_fault_slot_destroy(uint32_t* host) {
 
 extern "C" int mapa_fault_publish(uint32_t* dev_slot, hipStream_t stream) {
   MAPA_CHECK_ARG(dev_slot != nullptr, "mapa_fault_publish: null slot");
-  hipLaunchKernelGGL(mapa_gemm_impl::fault_publish_kernel, dim3(1), dim3(64), 0, stream,
+  unsigned* word = mapa_gemm_impl::fault_word();
+  MAPA_CHECK_ARG(word != nullptr, "mapa_fault_publish: no fault word on this device");
+  hipLaunchKernelGGL(mapa_gemm_impl::fault_publish_kernel, dim3(1), dim3(64), 0, stream, word,
                      reinterpret_cast<unsigned*>(dev_slot));
   MAPA_CHECK_LAUNCH("mapa_fault_publish");
   return 0;
 }
 
 extern "C" int mapa_fault_reset(hipStream_t stream) {
-  hipLaunchKernelGGL(mapa_gemm_impl::fault_reset_kernel, dim3(1), dim3(64), 0, stream);
+  unsigned* word = mapa_gemm_impl::fault_word();
+  MAPA_CHECK_ARG(word != nullptr, "mapa_fault_reset: no fault word on this device");
+  hipLaunchKernelGGL(mapa_gemm_impl::fault_reset_kernel, dim3(1), dim3(64), 0, stream, word);
   MAPA_CHECK_LAUNCH("mapa_fault_reset");
   return 0;
 }
 
 extern "C" int mapa_fault_status(int reset) {
   unsigned v = 0;
-  hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(mapa_gemm_impl::g_mapa_fault), sizeof(v), 0,
-                                     hipMemcpyDeviceToHost);
+  unsigned* word = mapa_gemm_impl::fault_word();
+  if (!word) {
+    mapa_set_error("mapa_fault_status: no fault word on this device");
+    return -1;
+  }
+  hipError_t e = hipMemcpy(&v, word, sizeof(v), hipMemcpyDeviceToHost);
   if (e != hipSuccess) {
     mapa_set_error("mapa_fault_status: %s", hipGetErrorString(e));
     return -1;
   }
   if (reset && v) {
     const unsigned zero = 0;
-    e = hipMemcpyToSymbol(HIP_SYMBOL(mapa_gemm_impl::g_mapa_fault), &zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+    e = hipMemcpy(word, &zero, sizeof(zero), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       mapa_set_error("mapa_fault_status: reset: %s", hipGetErrorString(e));
       return -1;

@@ -351,7 +351,7 @@ __device__ __forceinline__ void big_epilogue_ln(const GemmArgs& p, f32x4 (&acc)[
       __builtin_amdgcn_s_sleep(1);
       asm volatile("" ::: "memory");  // re-issue the granule loads every pass
       if (++spins > p.ln_spin) {  // a band tile never published: raise the fault word, do not hang the device
-        if (p.fault)  // the library's fault word (gemm_big.hip g_mapa_fault, passed in: one copy per code object)
+        if (p.fault)  // the calling thread's fault word (gemm_big.hip fault_word(), passed in)
           __hip_atomic_fetch_or(p.fault, (unsigned)MAPA_FAULT_LN_BARRIER, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }

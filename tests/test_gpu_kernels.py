@@ -345,6 +345,82 @@ def test_gemm_layernorm_barrier_timeout_is_reported(nat, pers_ln):
     assert torch.equal(x2, x_ok) and torch.equal(y2, y_ok)
 
 
+def test_fault_words_are_per_thread(nat):
+    """Two host threads, each on its own stream (the in-thread sharded ranks, a server with a model per stream):
+    thread A raises MAPA_FAULT_LN_BARRIER (the test hook) and stops before its publish; thread B then starts a call —
+    reset, clean work, publish — on its own word.  B's publish is clean and B's reset does not clear A's fault, which
+    A's publish still carries (with one shared word a concurrent caller's per-call reset dropped another caller's
+    fault: a range fault lost that way left the TF32-equivalent heads' overflow in the outputs)."""
+    import threading
+
+    M, N, K = 10953, 768, 768
+    A = _rand(M, K, seed=91).to(torch.bfloat16)
+    W = _rand(N, K, scale=K ** -0.5, seed=92).to(torch.bfloat16)
+    b, x0 = _rand(N, seed=93), _rand(M, N, seed=94)
+    lw, lb = 1.0 + 0.2 * _rand(N, seed=95), 0.1 * _rand(N, seed=96)
+    bar, res, errs = threading.Barrier(2, timeout=120), {}, []
+
+    def outcome(slot):
+        try:
+            slot.wait(timeout_s=60)
+            return "clean"
+        except nat.NativeError as e:
+            return str(e)
+
+    def thread_a():
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                nat.fault_status(reset=True)
+                slot = nat.FaultSlot()
+                slot.arm()
+                x = x0.clone()
+                y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+                nat.gemm_tune(nat.TUNE_LN_SPIN, 4096)
+                nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 1)
+                try:
+                    nat.gemm(A, W, M, N, K, bias=b, resid1=x, out_f32=x, ln=(lw, lb, 1e-6, y))
+                    s.synchronize()  # the fault is in A's word now
+                finally:
+                    nat.gemm_tune(nat.TUNE_LN_SPIN, 0)
+                    nat.gemm_tune(nat.TUNE_LN_TEST_SKIP, 0)
+                bar.wait()  # B runs its whole call
+                bar.wait()
+                slot.publish()
+                res["a"] = outcome(slot)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            bar.abort()
+
+    def thread_b():
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                bar.wait()
+                slot = nat.FaultSlot()
+                slot.arm()
+                nat.FaultSlot.reset()
+                o = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+                nat.gemm(A, W, M, N, K, bias=b, out_lp=o)
+                slot.publish()
+                res["b"] = outcome(slot)
+                bar.wait()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            bar.abort()
+
+    th = [threading.Thread(target=thread_a), threading.Thread(target=thread_b)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    torch.cuda.synchronize()
+    assert not errs, errs
+    assert res["b"] == "clean", res
+    assert "LayerNorm" in res["a"], res
+    assert nat.fault_status(reset=False) == 0  # this thread's word saw neither
+
+
 @pytest.mark.parametrize("variant", [2580, 2581, 2582, 2572, 2573, 2574])
 def test_conv3x3_big_variants(nat, variant):
     n, H, W, C, Co = 2, 37, 37, 256, 256
